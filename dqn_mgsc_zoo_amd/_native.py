@@ -1,0 +1,150 @@
+"""ctypes binding of libdqz.so, the C ABI declared in include/dqz.h.
+
+This is the only way the package reaches the device hot path.  There is no
+CPU fallback: if the shared library is missing or fails to load, every
+product entry point raises `NativeLibraryError`.
+"""
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libdqz.so')
+
+DQZ_OK = 0
+ALGO_DQN = 0
+ALGO_DOUBLE = 1
+ALGO_PER = 2
+NUM_LEAVES = 10
+FRAME_H = 84
+FRAME_W = 84
+STACK = 4
+FRAME_BYTES = FRAME_H * FRAME_W
+
+
+class NativeLibraryError(RuntimeError):
+  """libdqz.so is missing, failed to load, or a call returned an error."""
+
+
+class DqzStore(ctypes.Structure):
+  _fields_ = [
+      ('frames', ctypes.c_void_p),
+      ('fidx', ctypes.c_void_p),
+      ('action', ctypes.c_void_p),
+      ('reward', ctypes.c_void_p),
+      ('discount', ctypes.c_void_p),
+      ('capacity', ctypes.c_int64),
+      ('num_frames', ctypes.c_int64),
+  ]
+
+
+class DqzParams(ctypes.Structure):
+  _fields_ = [
+      ('online', ctypes.c_void_p),
+      ('target', ctypes.c_void_p),
+      ('mu', ctypes.c_void_p),
+      ('nu', ctypes.c_void_p),
+  ]
+
+
+class DqzLearnerConfig(ctypes.Structure):
+  _fields_ = [
+      ('batch', ctypes.c_int),
+      ('num_actions', ctypes.c_int),
+      ('algo', ctypes.c_int),
+      ('learning_rate', ctypes.c_float),
+      ('decay', ctypes.c_float),
+      ('eps', ctypes.c_float),
+      ('grad_error_bound', ctypes.c_float),
+  ]
+
+
+# name -> (restype, argtypes); must match include/dqz.h exactly.
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+SIGNATURES = {
+    'dqz_last_error': (ctypes.c_char_p, []),
+    'dqz_param_layout': (
+        _int,
+        [_int, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+         ctypes.POINTER(_i64)],
+    ),
+    'dqz_learner_create': (
+        _int, [ctypes.POINTER(DqzLearnerConfig), ctypes.POINTER(_vp)]),
+    'dqz_learner_destroy': (_int, [_vp]),
+    'dqz_learner_step': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
+         _vp],
+    ),
+    'dqz_learner_outputs': (_int, [_vp, _vp, _vp, _vp, _vp]),
+    'dqz_forward': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
+    'dqz_forward_slots': (
+        _int, [_vp, _vp, ctypes.POINTER(DqzStore), _vp, _int, _int, _vp, _vp]),
+    'dqz_sample_uniform': (
+        _int, [_i64, _i64, _i64, _int, ctypes.c_uint64, _vp, _vp, _vp]),
+    'dqz_gather_stacks': (
+        _int, [ctypes.POINTER(DqzStore), _vp, _int, _int, _vp, _vp]),
+    'dqz_target_copy': (_int, [_vp, _vp, _i64, _vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+  """Loads libdqz.so once; raises NativeLibraryError if it is unavailable."""
+  global _lib
+  if _lib is not None:
+    return _lib
+  with _lock:
+    if _lib is None:
+      if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            '%s not found: build it with `python -c "import __graft_entry__ '
+            'as g; g.build()"` (hipcc --offload-arch=gfx950).' % LIB_PATH)
+      try:
+        handle = ctypes.CDLL(LIB_PATH)
+      except OSError as e:
+        raise NativeLibraryError('failed to load %s: %s' % (LIB_PATH, e)) from e
+      for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+      _lib = handle
+  return _lib
+
+
+def check(rc):
+  """Raises NativeLibraryError with dqz_last_error() on a non-zero status."""
+  if rc != DQZ_OK:
+    msg = lib().dqz_last_error()
+    raise NativeLibraryError(
+        'libdqz error %d: %s' % (rc, msg.decode() if msg else ''))
+  return rc
+
+
+def param_layout(num_actions, shared_bias):
+  """Returns (offsets, sizes, total) of the flat parameter buffer."""
+  offs = (_i64 * NUM_LEAVES)()
+  sizes = (_i64 * NUM_LEAVES)()
+  total = _i64()
+  check(lib().dqz_param_layout(
+      int(num_actions), int(bool(shared_bias)), offs, sizes,
+      ctypes.byref(total)))
+  return list(offs), list(sizes), int(total.value)
+
+
+def ptr(t):
+  """Device pointer of a torch tensor (None -> NULL)."""
+  if t is None:
+    return None
+  return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+  import torch  # pylint: disable=g-import-not-at-top
+  s = stream if stream is not None else torch.cuda.current_stream()
+  return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,157 @@
+"""Device learner: owns params / optimizer state and drives libdqz.
+
+`Learner.step(store, slots)` is the jitted `update` of the reference
+(dqn/agent.py:109-119, double_q/agent.py, prioritized/agent.py:115-127):
+forward of online(s_tm1) and target(s_t) [and online(s_t)], TD loss with
+clip_gradient, backward and centered RMSProp, in place.  Everything runs in
+libdqz.so on the current HIP stream; there is no host fallback.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from dqn_mgsc_zoo_amd import _native
+from dqn_mgsc_zoo_amd import networks as networks_lib
+
+ALGOS = {'dqn': _native.ALGO_DQN, 'double': _native.ALGO_DOUBLE,
+         'per': _native.ALGO_PER}
+
+
+class RMSPropConfig:
+  """optax.rmsprop(learning_rate, decay, eps, centered=True) stand-in."""
+
+  def __init__(self, learning_rate, decay=0.9, eps=1e-8, centered=False):
+    if not centered:
+      raise NotImplementedError(
+          'only centered RMSProp is on the hot path (dqn/run_atari.py:208-213)')
+    self.learning_rate = float(learning_rate)
+    self.decay = float(decay)
+    self.eps = float(eps)
+    self.centered = True
+
+
+def rmsprop(learning_rate, decay=0.9, eps=1e-8, centered=False):
+  return RMSPropConfig(learning_rate, decay, eps, centered)
+
+
+class Learner:
+  """Online/target params + RMSProp moments in HBM and a libdqz handle."""
+
+  def __init__(self, network: networks_lib.NetworkSpec, batch_size, algo='dqn',
+               optimizer=None, grad_error_bound=1.0 / 32, device='cuda'):
+    if algo not in ALGOS:
+      raise ValueError('algo must be one of %s' % sorted(ALGOS))
+    if (algo == 'dqn') == network.shared_bias:
+      raise ValueError(
+          "algo 'dqn' uses dqn_atari_network; 'double'/'per' use "
+          'double_dqn_atari_network (shared bias)')
+    optimizer = optimizer or rmsprop(2.5e-4, 0.95, 0.01 / 32**2, True)
+    self.network = network
+    self.algo = algo
+    self.batch_size = int(batch_size)
+    self.optimizer = optimizer
+    self.device = torch.device(device)
+    self.offsets, self.sizes, self.total = network.layout()
+    self.online = torch.zeros((self.total,), dtype=torch.float32, device=self.device)
+    self.target = torch.zeros_like(self.online)
+    self.mu = torch.zeros_like(self.online)
+    self.nu = torch.zeros_like(self.online)
+    self.q_tm1 = torch.zeros((self.batch_size, network.num_actions),
+                             dtype=torch.float32, device=self.device)
+    self.td = torch.zeros((self.batch_size,), dtype=torch.float32, device=self.device)
+    self.loss = torch.zeros((1,), dtype=torch.float32, device=self.device)
+    cfg = _native.DqzLearnerConfig(
+        self.batch_size, network.num_actions, ALGOS[algo],
+        optimizer.learning_rate, optimizer.decay, optimizer.eps,
+        float(grad_error_bound))
+    handle = ctypes.c_void_p()
+    _native.check(_native.lib().dqz_learner_create(ctypes.byref(cfg),
+                                                   ctypes.byref(handle)))
+    self._h = handle
+    self._params_c = _native.DqzParams(
+        self.online.data_ptr(), self.target.data_ptr(), self.mu.data_ptr(),
+        self.nu.data_ptr())
+
+  def __del__(self):
+    h = getattr(self, '_h', None)
+    if h is not None and h.value and _native._lib is not None:  # pylint: disable=protected-access
+      _native.lib().dqz_learner_destroy(h)
+      self._h = None
+
+  # -- state -------------------------------------------------------------
+
+  def set_params(self, tree, target_tree=None):
+    flat = torch.from_numpy(self.network.flatten(tree))
+    self.online.copy_(flat)
+    if target_tree is None:
+      self.target.copy_(flat)
+    else:
+      self.target.copy_(torch.from_numpy(self.network.flatten(target_tree)))
+
+  def set_opt_state(self, mu_tree, nu_tree):
+    self.mu.copy_(torch.from_numpy(self.network.flatten(mu_tree)))
+    self.nu.copy_(torch.from_numpy(self.network.flatten(nu_tree)))
+
+  def params_tree(self, which='online'):
+    t = {'online': self.online, 'target': self.target, 'mu': self.mu,
+         'nu': self.nu}[which]
+    return self.network.unflatten(t.detach().cpu().numpy())
+
+  def sync_target(self, stream=None):
+    """target <- online (dqn/agent.py:155-156)."""
+    _native.check(_native.lib().dqz_target_copy(
+        _native.ptr(self.target), _native.ptr(self.online), self.total,
+        _native.stream_handle(stream)))
+
+  # -- hot path ------------------------------------------------------------
+
+  def step(self, store, slots, weights=None, stream=None):
+    """One learner step on replay `slots` (device int32 [B])."""
+    if slots.dtype != torch.int32 or slots.numel() != self.batch_size:
+      raise ValueError('slots must be a device int32 tensor of batch size')
+    if self.algo == 'per' and weights is None:
+      raise ValueError('PER step needs importance weights')
+    _native.check(_native.lib().dqz_learner_step(
+        self._h, ctypes.byref(self._params_c), store.c_ref(),
+        _native.ptr(slots), _native.ptr(weights), _native.stream_handle(stream)))
+
+  def fetch_outputs(self, stream=None):
+    """Copies (q_tm1, td, loss) of the last step into self tensors."""
+    _native.check(_native.lib().dqz_learner_outputs(
+        self._h, _native.ptr(self.q_tm1), _native.ptr(self.td),
+        _native.ptr(self.loss), _native.stream_handle(stream)))
+    return self.q_tm1, self.td, self.loss
+
+  def q_values(self, states, params=None, stream=None):
+    """network.apply(params, s).q_values for uint8 [n,84,84,4] device states."""
+    params = self.online if params is None else params
+    states = states.contiguous()
+    n = int(states.shape[0])
+    out = torch.empty((n, self.network.num_actions), dtype=torch.float32,
+                      device=self.device)
+    for i in range(0, n, self.batch_size):
+      j = min(n, i + self.batch_size)
+      _native.check(_native.lib().dqz_forward(
+          self._h, _native.ptr(params), _native.ptr(states[i:j]), j - i,
+          _native.ptr(out[i:j]), _native.stream_handle(stream)))
+    return out
+
+  def q_values_slots(self, store, slots, which, params=None, stream=None):
+    params = self.online if params is None else params
+    n = int(slots.numel())
+    out = torch.empty((n, self.network.num_actions), dtype=torch.float32,
+                      device=self.device)
+    _native.check(_native.lib().dqz_forward_slots(
+        self._h, _native.ptr(params), store.c_ref(), _native.ptr(slots), n,
+        int(which), _native.ptr(out), _native.stream_handle(stream)))
+    return out
+
+
+def sample_uniform(base, size, capacity, n, seed, counter, out, stream=None):
+  """Device Philox uniform sampler (replay.py:119-125 distribution)."""
+  _native.check(_native.lib().dqz_sample_uniform(
+      int(base), int(size), int(capacity), int(n), int(seed) & (2**64 - 1),
+      _native.ptr(counter), _native.ptr(out), _native.stream_handle(stream)))
+  return out

@@ -1,0 +1,155 @@
+/*
+ * dqz.h — C ABI of the MI355X-native DQN learner step (libdqz.so).
+ *
+ * Plain C: raw pointers, sizes and a hipStream_t passed as void*.  No torch
+ * types cross this boundary.  Every function returns DQZ_OK (0) on success or
+ * a negative status; dqz_last_error() returns a thread-local message.
+ *
+ * Ownership: the caller owns every device buffer that holds
+ * state (parameters, optimizer moments, frame pool, transition table, sampled
+ * slot buffers).  The library borrows those pointers for the duration of an
+ * enqueue and owns only the opaque learner handle and its scratch.  All work
+ * is enqueued on the given stream; no call synchronises the device except
+ * where it documents a host output.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * Stalfoes/dqn_mgsc_zoo).
+ */
+#ifndef DQZ_H_
+#define DQZ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQZ_OK 0
+#define DQZ_ERR_INVALID (-1)
+#define DQZ_ERR_HIP (-2)
+#define DQZ_ERR_UNSUPPORTED (-3)
+
+/* Learner algorithm: which TD loss and which network head.
+ *  DQN     : rlax.q_learning, dqn_atari_network          (dqn/agent.py:85-107)
+ *  DOUBLE  : rlax.double_q_learning, double_dqn_atari_network (shared bias)
+ *            (double_q/agent.py:85-107, networks.py:338-349)
+ *  PER     : DOUBLE + importance weights, |td| returned   (prioritized/agent.py:86-127)
+ */
+#define DQZ_ALGO_DQN 0
+#define DQZ_ALGO_DOUBLE 1
+#define DQZ_ALGO_PER 2
+
+/* Frame geometry (processors.py:488-505): 84x84 grayscale frames, 4-stack,
+ * HWC layout, channel order oldest -> newest, trailing zero padding. */
+#define DQZ_FRAME_H 84
+#define DQZ_FRAME_W 84
+#define DQZ_STACK 4
+#define DQZ_FRAME_BYTES (DQZ_FRAME_H * DQZ_FRAME_W)
+#define DQZ_NUM_LEAVES 10
+
+/* Thread-local message for the last failing call on this thread. */
+const char* dqz_last_error(void);
+
+/* Flat parameter layout of the NatureQNetwork (networks.py:181-221,352-363):
+ * leaves in Haiku order
+ *   0 conv2_d/w [8,8,4,32]   1 conv2_d/b [32]
+ *   2 conv2_d_1/w [4,4,32,64] 3 conv2_d_1/b [64]
+ *   4 conv2_d_2/w [3,3,64,64] 5 conv2_d_2/b [64]
+ *   6 linear/w [3136,512]    7 linear/b [512]
+ *   8 linear_1/w [512,A]     9 linear_1/b [A]   (shared_bias: [1])
+ * Each leaf starts on a 64-float boundary; padding stays zero.
+ * offsets/sizes are in floats; total is the padded buffer length. */
+int dqz_param_layout(int num_actions, int shared_bias, int64_t offsets[DQZ_NUM_LEAVES],
+                     int64_t sizes[DQZ_NUM_LEAVES], int64_t* total);
+
+/* Replay storage in HBM (replaces the snappy-compressed per-transition
+ * storage of replay.py:163-206 / replay_circular.py:90-146).
+ *   frames   uint8 [num_frames][84*84]         frame pool
+ *   fidx     int32 [capacity][8]               frame index of each stack
+ *                                              channel: 0..3 = s_tm1, 4..7 = s_t,
+ *                                              -1 = zero padding
+ *   action   int32 [capacity]   reward f32 [capacity]   discount f32 [capacity]
+ * A transition lives in a slot; slots are what the samplers return. */
+typedef struct dqz_store {
+  const uint8_t* frames;
+  const int32_t* fidx;
+  const int32_t* action;
+  const float* reward;
+  const float* discount;
+  int64_t capacity;
+  int64_t num_frames;
+} dqz_store;
+
+/* Online/target parameters and centered-RMSProp moments, all [total] f32
+ * in the dqz_param_layout order (optax.rmsprop(centered=True) state,
+ * dqn/run_atari.py:208-213). */
+typedef struct dqz_params {
+  float* online;
+  float* target;
+  float* mu;
+  float* nu;
+} dqz_params;
+
+typedef struct dqz_learner_config {
+  int batch;            /* B (replay.sample(batch_size)), 1..256 */
+  int num_actions;      /* A, 1..32 */
+  int algo;             /* DQZ_ALGO_* */
+  float learning_rate;  /* dqn/run_atari.py:81 */
+  float decay;          /* 0.95 */
+  float eps;            /* dqn/run_atari.py:82 */
+  float grad_error_bound; /* dqn/run_atari.py:80 (rlax.clip_gradient bound) */
+} dqz_learner_config;
+
+typedef struct dqz_learner dqz_learner;
+
+/* Allocates the learner's scratch (activations, split-K partials). */
+int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out);
+int dqz_learner_destroy(dqz_learner* learner);
+
+/* One learner step = jitted `update` of dqn/agent.py:109-119
+ * (prioritized/agent.py:115-127 for PER): forward online(s_tm1),
+ * target(s_t) [+ online(s_t)], TD loss with clip_gradient, backward,
+ * centered RMSProp, in place on params->online / mu / nu.
+ * slots: device int32 [B] replay slots of the minibatch (from a sampler or
+ * injected by the caller).  is_weights: device f32 [B] or NULL (PER only). */
+int dqz_learner_step(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                     const int32_t* slots, const float* is_weights, void* stream);
+
+/* Device-to-device copies of the last step's outputs (any may be NULL):
+ * q_tm1 [B][A] online Q(s_tm1), td [B] TD errors, loss [1] mean loss. */
+int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* loss, void* stream);
+
+/* Q-values of the NatureQNetwork for uint8 HWC states [n][84][84][4]
+ * (network.apply(...).q_values, networks.py:352-363; used by select_action,
+ * dqn/agent.py:121-131).  q_out: device f32 [n][A]. n <= learner batch. */
+int dqz_forward(dqz_learner* learner, const float* params, const uint8_t* states, int n,
+                float* q_out, void* stream);
+
+/* Q-values for replay slots without materialising stacks:
+ * which = 0 -> s_tm1, 1 -> s_t. */
+int dqz_forward_slots(dqz_learner* learner, const float* params, const dqz_store* store,
+                      const int32_t* slots, int n, int which, float* q_out, void* stream);
+
+/* Uniform sampling with replacement over live transitions, on device
+ * (UniformDistribution.sample, replay.py:119-125; replay_circular.py:283-289).
+ * Live slots are (base + j) mod capacity for j in [0, size).  FIFO replay:
+ * base = t - size; reservoir replay: base = 0.  Philox4x32-10 keyed by seed,
+ * counter = (*counter_dev, lane); *counter_dev is incremented on device, so
+ * the call is hipGraph-replayable. */
+int dqz_sample_uniform(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
+                       uint64_t* counter_dev, int32_t* out_slots, void* stream);
+
+/* Materialise stacked uint8 states [n][84][84][4] for the given slots
+ * (the np.stack of TransitionReplay.sample, replay.py:200-206).
+ * which = 0 -> s_tm1, 1 -> s_t. */
+int dqz_gather_stacks(const dqz_store* store, const int32_t* slots, int n, int which,
+                      uint8_t* out, void* stream);
+
+/* Target sync: target <- online (dqn/agent.py:155-156; hard copy, not Polyak). */
+int dqz_target_copy(float* target, const float* online, int64_t total, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DQZ_H_ */

@@ -1,0 +1,209 @@
+"""ORACLE — test infrastructure only.  Never imported by the product.
+
+fp64 numpy restatement of the DQN learner step that the HIP path must match
+(BASELINE.json north_star: Q-values / TD errors within 1e-4 fp32).  Only
+`tests/`, `__graft_entry__.smoke()` and `bench.py`'s cpu_baseline leg may
+use it, and only as the checker / CPU baseline.
+
+What it restates (reference file:line; the arithmetic itself lives in
+un-vendored dependencies pinned at docker_requirements.txt:6-26):
+  * networks.dqn_torso / dqn_value_head (networks.py:181-221): x/255,
+    Haiku Conv2D NHWC/HWIO VALID + bias + ReLU x3, Flatten (h,w,c), Linear +
+    ReLU, Linear; shared-bias head (networks.py:120-134) -- dm-haiku 0.0.6.
+  * rlax 0.1.2 q_learning / double_q_learning / clip_gradient / l2_loss as
+    called at dqn/agent.py:85-107, double_q/agent.py:85-107,
+    prioritized/agent.py:86-113.  clip_gradient is identity forward and clips
+    the incoming cotangent backward.
+  * optax 0.1.2 rmsprop(centered=True) = scale_by_stddev + scale(-lr)
+    (dqn/run_atari.py:208-213): mu=(1-d)g+d mu, nu=(1-d)g^2+d nu,
+    u = -lr g rsqrt(nu - mu^2 + eps).
+  * optax 0.1.2 adam (dqn_mgsc_batched/run_atari.py:241-243).
+
+Parity status: the reference's own tests pin only parameter names/shapes and
+the shared-bias output (networks_test.py:36-103); no Q-value, gradient or
+optimizer golden vector exists in the reference, and JAX is not installable
+here, so this restatement is *parity unpinned* against the reference's
+numbers.  It is cross-checked against an independent torch-CPU autograd
+implementation in tests/test_oracle.py.
+"""
+
+import numpy as np
+
+CONV_SPECS = (  # (kernel, stride, c_in, c_out)
+    (8, 4, 4, 32),
+    (4, 2, 32, 64),
+    (3, 1, 64, 64),
+)
+_TORSO = 'sequential/sequential'
+_HEAD = 'sequential/sequential_1'
+CONV_NAMES = (_TORSO + '/conv2_d', _TORSO + '/conv2_d_1', _TORSO + '/conv2_d_2')
+
+
+def _im2col(x, k, s):
+  """x [B,H,W,C] -> [B,OH,OW,k*k*C] ordered (kh, kw, c) like HWIO."""
+  b, h, w, c = x.shape
+  oh, ow = (h - k) // s + 1, (w - k) // s + 1
+  cols = np.empty((b, oh, ow, k, k, c), dtype=x.dtype)
+  for kh in range(k):
+    for kw in range(k):
+      cols[:, :, :, kh, kw, :] = x[:, kh:kh + s * (oh - 1) + 1:s,
+                                   kw:kw + s * (ow - 1) + 1:s, :]
+  return cols.reshape(b, oh, ow, k * k * c)
+
+
+def _col2im(dcols, x_shape, k, s):
+  b, h, w, c = x_shape
+  oh, ow = dcols.shape[1], dcols.shape[2]
+  dcols = dcols.reshape(b, oh, ow, k, k, c)
+  dx = np.zeros(x_shape, dtype=dcols.dtype)
+  for kh in range(k):
+    for kw in range(k):
+      dx[:, kh:kh + s * (oh - 1) + 1:s, kw:kw + s * (ow - 1) + 1:s, :] += (
+          dcols[:, :, :, kh, kw, :])
+  return dx
+
+
+def head_params(params, shared_bias):
+  w2 = np.asarray(params[_HEAD + '/linear_1']['w'], np.float64)
+  if shared_bias:
+    b2 = np.asarray(params[_HEAD]['b'], np.float64)
+  else:
+    b2 = np.asarray(params[_HEAD + '/linear_1']['b'], np.float64)
+  return w2, b2
+
+
+def forward(params, s, shared_bias=False):
+  """Q-values and intermediates for uint8 states s [B,84,84,4]."""
+  x = np.asarray(s).astype(np.float32).astype(np.float64) / 255.0
+  cache = {'x0': x}
+  for i, ((k, st, _, co), name) in enumerate(zip(CONV_SPECS, CONV_NAMES)):
+    w = np.asarray(params[name]['w'], np.float64)
+    b = np.asarray(params[name]['b'], np.float64)
+    cols = _im2col(x, k, st)
+    z = cols @ w.reshape(-1, co) + b
+    x = np.maximum(z, 0.0)
+    cache['cols%d' % i] = cols
+    cache['y%d' % i] = x
+  flat = x.reshape(x.shape[0], -1)
+  w1 = np.asarray(params[_HEAD + '/linear']['w'], np.float64)
+  b1 = np.asarray(params[_HEAD + '/linear']['b'], np.float64)
+  h1 = np.maximum(flat @ w1 + b1, 0.0)
+  w2, b2 = head_params(params, shared_bias)
+  q = h1 @ w2 + b2
+  cache.update(flat=flat, h1=h1)
+  return q, cache
+
+
+def backward(params, cache, dq, shared_bias=False):
+  """Gradient tree of sum(dq * q) w.r.t. the online parameters."""
+  grads = {}
+  h1, flat = cache['h1'], cache['flat']
+  w2, _ = head_params(params, shared_bias)
+  grads[_HEAD + '/linear_1'] = {'w': h1.T @ dq}
+  if shared_bias:
+    grads[_HEAD] = {'b': np.array([dq.sum()])}
+  else:
+    grads[_HEAD + '/linear_1']['b'] = dq.sum(axis=0)
+  dh1 = (dq @ w2.T) * (h1 > 0)
+  w1 = np.asarray(params[_HEAD + '/linear']['w'], np.float64)
+  grads[_HEAD + '/linear'] = {'w': flat.T @ dh1, 'b': dh1.sum(axis=0)}
+  dflat = dh1 @ w1.T
+  dy = dflat.reshape(cache['y2'].shape)
+  for i in (2, 1, 0):
+    k, st, _, co = CONV_SPECS[i]
+    y = cache['y%d' % i]
+    dz = dy * (y > 0)
+    cols = cache['cols%d' % i]
+    grads[CONV_NAMES[i]] = {
+        'w': (cols.reshape(-1, cols.shape[-1]).T @ dz.reshape(-1, co)).reshape(
+            np.asarray(params[CONV_NAMES[i]]['w']).shape),
+        'b': dz.reshape(-1, co).sum(axis=0),
+    }
+    if i > 0:
+      w = np.asarray(params[CONV_NAMES[i]]['w'], np.float64).reshape(-1, co)
+      dcols = dz @ w.T
+      x_shape = cache['y%d' % (i - 1)].shape
+      dy = _col2im(dcols, x_shape, k, st)
+  return grads
+
+
+def td_loss(q_tm1, a_tm1, r_t, discount_t, q_target_t, q_selector_t=None,
+            weights=None, grad_error_bound=1.0 / 32):
+  """TD errors, mean loss and d loss / d q_tm1.
+
+  q_learning: target = r + d * max_a q_target_t; double_q_learning: target =
+  r + d * q_target_t[argmax q_selector_t] (first maximum).  loss =
+  mean(0.5 td^2 [* w]).  The cotangent at td is clip(w td / B, +-bound)
+  because rlax.clip_gradient sits between td and l2_loss.
+  """
+  b = q_tm1.shape[0]
+  idx = np.arange(b)
+  a_tm1 = np.asarray(a_tm1, np.int64)
+  if q_selector_t is None:
+    v = q_target_t.max(axis=1)
+  else:
+    v = q_target_t[idx, np.argmax(q_selector_t, axis=1)]
+  target = np.asarray(r_t, np.float64) + np.asarray(discount_t, np.float64) * v
+  td = target - q_tm1[idx, a_tm1]
+  w = np.ones(b) if weights is None else np.asarray(weights, np.float64)
+  loss = np.mean(0.5 * td * td * w)
+  g_td = np.clip(w * td / b, -grad_error_bound, grad_error_bound)
+  dq = np.zeros_like(q_tm1)
+  dq[idx, a_tm1] = -g_td
+  return td, loss, dq
+
+
+def rmsprop_centered(params, grads, mu, nu, lr, decay, eps):
+  """optax 0.1.2 rmsprop(centered=True); returns new (params, mu, nu)."""
+  new_p, new_mu, new_nu = {}, {}, {}
+  for mod in params:
+    new_p[mod], new_mu[mod], new_nu[mod] = {}, {}, {}
+    for name in params[mod]:
+      g = np.asarray(grads[mod][name], np.float64)
+      m = (1.0 - decay) * g + decay * np.asarray(mu[mod][name], np.float64)
+      v = (1.0 - decay) * g * g + decay * np.asarray(nu[mod][name], np.float64)
+      new_mu[mod][name] = m
+      new_nu[mod][name] = v
+      new_p[mod][name] = (np.asarray(params[mod][name], np.float64) -
+                          lr * g / np.sqrt(v - m * m + eps))
+  return new_p, new_mu, new_nu
+
+
+def adam(params, grads, m, v, count, lr, b1=0.9, b2=0.999, eps=1e-8):
+  """optax 0.1.2 adam on a flat array; returns (params, m, v, count)."""
+  g = np.asarray(grads, np.float64)
+  m = b1 * np.asarray(m, np.float64) + (1 - b1) * g
+  v = b2 * np.asarray(v, np.float64) + (1 - b2) * g * g
+  count = count + 1
+  m_hat = m / (1 - b1**count)
+  v_hat = v / (1 - b2**count)
+  return np.asarray(params, np.float64) - lr * m_hat / (np.sqrt(v_hat) + eps), m, v, count
+
+
+def learner_step(online, target, mu, nu, s_tm1, a_tm1, r_t, discount_t, s_t,
+                 algo='dqn', weights=None, lr=2.5e-4, decay=0.95,
+                 eps=0.01 / 32**2, grad_error_bound=1.0 / 32):
+  """One `update` (dqn/agent.py:109-119; prioritized/agent.py:115-127).
+
+  algo: 'dqn' (q_learning, per-action bias), 'double' or 'per'
+  (double_q_learning, shared-bias head; 'per' weights the loss).
+  Returns dict(q_tm1, td, loss, params, mu, nu, grads).
+  """
+  shared = algo != 'dqn'
+  q_tm1, cache = forward(online, s_tm1, shared)
+  q_target_t, _ = forward(target, s_t, shared)
+  q_sel = None
+  if algo != 'dqn':
+    q_sel, _ = forward(online, s_t, shared)
+  td, loss, dq = td_loss(q_tm1, a_tm1, r_t, discount_t, q_target_t, q_sel,
+                         weights if algo == 'per' else None, grad_error_bound)
+  grads = backward(online, cache, dq, shared)
+  new_p, new_mu, new_nu = rmsprop_centered(online, grads, mu, nu, lr, decay,
+                                           eps)
+  return dict(q_tm1=q_tm1, q_target_t=q_target_t, td=td, loss=loss,
+              params=new_p, mu=new_mu, nu=new_nu, grads=grads)
+
+
+def zeros_like_tree(tree):
+  return {m: {n: np.zeros_like(np.asarray(v, np.float64)) for n, v in d.items()}
+          for m, d in tree.items()}

@@ -1,0 +1,50 @@
+"""Shared test fixtures: seeded replay contents and parameter trees."""
+
+import numpy as np
+
+FRAME = 84 * 84
+
+
+def random_store_contents(capacity, num_frames, num_actions, seed, pad_frac=0.2):
+  """Random frame pool + transition table (host numpy).
+
+  Each slot's stacks follow the processor layout: s_t = s_tm1 shifted by one
+  frame, with trailing zero padding (-1) at the start of an episode.
+  """
+  rng = np.random.default_rng(seed)
+  frames = rng.integers(0, 256, size=(num_frames, FRAME), dtype=np.uint8)
+  fidx = np.empty((capacity, 8), np.int32)
+  for i in range(capacity):
+    k = int(rng.integers(1, 8))  # in-episode index of s_t
+    if rng.random() > pad_frac:
+      k = max(k, 4)
+    newest = int(rng.integers(0, num_frames))
+    def stack(kk, pos):
+      n = min(kk, 3)
+      ch = [-1] * 4
+      for c in range(n + 1):
+        ch[c] = (pos - n + c) % num_frames
+      return ch
+    fidx[i, :4] = stack(k - 1, newest - 1)
+    fidx[i, 4:] = stack(k, newest)
+  action = rng.integers(0, num_actions, size=capacity).astype(np.int32)
+  reward = rng.choice([-1.0, 0.0, 1.0], size=capacity).astype(np.float32)
+  discount = (0.99 * (rng.random(capacity) > 0.1)).astype(np.float32)
+  return frames, fidx, action, reward, discount
+
+
+def stacks_from(frames, fidx, slots, which):
+  """Host reference of the device gather: uint8 [n,84,84,4]."""
+  out = np.zeros((len(slots), 84, 84, 4), np.uint8)
+  for b, s in enumerate(slots):
+    for c in range(4):
+      f = fidx[s, which * 4 + c]
+      if f >= 0:
+        out[b, :, :, c] = frames[f].reshape(84, 84)
+  return out
+
+
+def perturbed_tree(tree, seed, scale=0.02):
+  rng = np.random.default_rng(seed)
+  return {m: {n: (v + scale * rng.standard_normal(v.shape)).astype(np.float32)
+              for n, v in d.items()} for m, d in tree.items()}

@@ -1,0 +1,128 @@
+"""CPU: the fp64 oracle vs an independent torch autograd restatement.
+
+The reference holds no Q-value / gradient golden vectors (networks_test.py
+pins only shapes and the shared-bias output), so the oracle's network, loss
+and optimizer math is cross-checked against torch.nn.functional +
+autograd, written from the same reference call sites.
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import learner_ref
+from tests import helpers
+
+_T = 'sequential/sequential'
+_H = 'sequential/sequential_1'
+
+
+def _init(num_actions, shared, seed):
+  rng = np.random.default_rng(seed)
+  shapes = {
+      _T + '/conv2_d': ((8, 8, 4, 32), 256), _T + '/conv2_d_1': ((4, 4, 32, 64), 512),
+      _T + '/conv2_d_2': ((3, 3, 64, 64), 576), _H + '/linear': ((3136, 512), 3136),
+      _H + '/linear_1': ((512, num_actions), 512)}
+  tree = {}
+  for mod, (shape, fan) in shapes.items():
+    bnd = 1 / np.sqrt(fan)
+    tree[mod] = {'w': rng.uniform(-bnd, bnd, shape).astype(np.float32)}
+    if not (shared and mod.endswith('linear_1')):
+      tree[mod]['b'] = rng.uniform(-bnd, bnd, shape[-1:]).astype(np.float32)
+  if shared:
+    tree[_H] = {'b': rng.uniform(-0.04, 0.04, (1,)).astype(np.float32)}
+  return tree
+
+
+def _torch_q(tree, s, shared):
+  x = torch.as_tensor(s).to(torch.float64).permute(0, 3, 1, 2) / 255.0
+  for mod, stride in ((_T + '/conv2_d', 4), (_T + '/conv2_d_1', 2), (_T + '/conv2_d_2', 1)):
+    w = tree[mod]['w'].permute(3, 2, 0, 1)  # HWIO -> OIHW
+    x = F.relu(F.conv2d(x, w, tree[mod]['b'], stride=stride))
+  flat = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # Haiku Flatten of NHWC
+  h = F.relu(flat @ tree[_H + '/linear']['w'] + tree[_H + '/linear']['b'])
+  b2 = tree[_H]['b'] if shared else tree[_H + '/linear_1']['b']
+  return h @ tree[_H + '/linear_1']['w'] + b2
+
+
+class _ClipGrad(torch.autograd.Function):
+  @staticmethod
+  def forward(ctx, x, lo, hi):
+    ctx.lo, ctx.hi = lo, hi
+    return x.clone()
+
+  @staticmethod
+  def backward(ctx, g):
+    return g.clamp(ctx.lo, ctx.hi), None, None
+
+
+@pytest.mark.parametrize('algo', ['dqn', 'double', 'per'])
+def test_oracle_matches_torch_autograd(algo):
+  shared = algo != 'dqn'
+  a = 6
+  online = _init(a, shared, 1)
+  target = helpers.perturbed_tree(online, 2)
+  rng = np.random.default_rng(3)
+  b = 4
+  s_tm1 = rng.integers(0, 256, (b, 84, 84, 4), dtype=np.uint8)
+  s_t = rng.integers(0, 256, (b, 84, 84, 4), dtype=np.uint8)
+  s_t[0, :, :, 2:] = 0  # trailing zero padding
+  act = rng.integers(0, a, b)
+  r = np.array([1.0, 0.0, -1.0, 0.0])
+  d = np.array([0.99, 0.0, 0.99, 0.99])
+  w = rng.uniform(0.3, 1.0, b) if algo == 'per' else None
+  zeros = learner_ref.zeros_like_tree(online)
+  # a large error bound exercises both sides of clip_gradient
+  bound = 0.05
+  ref = learner_ref.learner_step(online, target, zeros, zeros, s_tm1, act, r, d,
+                                 s_t, algo=algo, weights=w,
+                                 grad_error_bound=bound)
+
+  tp = {m: {n: torch.tensor(v, dtype=torch.float64, requires_grad=True)
+            for n, v in dd.items()} for m, dd in online.items()}
+  tt = {m: {n: torch.tensor(v, dtype=torch.float64) for n, v in dd.items()}
+        for m, dd in target.items()}
+  q_tm1 = _torch_q(tp, s_tm1, shared)
+  with torch.no_grad():
+    q_tgt = _torch_q(tt, s_t, shared)
+    if algo == 'dqn':
+      v = q_tgt.max(dim=1).values
+    else:
+      sel = _torch_q(tp, s_t, shared).argmax(dim=1)
+      v = q_tgt[torch.arange(b), sel]
+    target_v = torch.as_tensor(r) + torch.as_tensor(d) * v
+  td = target_v - q_tm1[torch.arange(b), torch.as_tensor(act)]
+  td_c = _ClipGrad.apply(td, -bound, bound)
+  losses = 0.5 * td_c**2
+  if w is not None:
+    losses = losses * torch.as_tensor(w)
+  loss = losses.mean()
+  loss.backward()
+
+  np.testing.assert_allclose(ref['q_tm1'], q_tm1.detach().numpy(), atol=1e-10)
+  np.testing.assert_allclose(ref['td'], td.detach().numpy(), atol=1e-10)
+  np.testing.assert_allclose(ref['loss'], loss.item(), rtol=1e-10)
+  for m in online:
+    for n in online[m]:
+      np.testing.assert_allclose(ref['grads'][m][n], tp[m][n].grad.numpy(),
+                                 atol=1e-12, rtol=1e-8, err_msg=m + '/' + n)
+
+
+def test_rmsprop_and_adam_formulas():
+  p = {'l': {'w': np.array([1.0, -2.0, 0.5])}}
+  g = {'l': {'w': np.array([0.1, -0.3, 0.0])}}
+  z = learner_ref.zeros_like_tree(p)
+  newp, mu, nu = learner_ref.rmsprop_centered(p, g, z, z, 0.1, 0.95, 1e-4)
+  gg = g['l']['w']
+  m = 0.05 * gg
+  v = 0.05 * gg * gg
+  np.testing.assert_allclose(mu['l']['w'], m)
+  np.testing.assert_allclose(nu['l']['w'], v)
+  np.testing.assert_allclose(newp['l']['w'],
+                             p['l']['w'] - 0.1 * gg / np.sqrt(v - m * m + 1e-4))
+  x, m1, v1, c = learner_ref.adam(np.zeros(2), np.array([1.0, -1.0]),
+                                  np.zeros(2), np.zeros(2), 0, lr=0.01)
+  # first bias-corrected Adam step moves by lr * g/|g| (up to eps)
+  np.testing.assert_allclose(x, [-0.01, 0.01], rtol=1e-6)
+  assert c == 1
