@@ -17,6 +17,10 @@ ALGO_DQN = 0
 ALGO_DOUBLE = 1
 ALGO_PER = 2
 NUM_LEAVES = 10
+NUM_PHASES = 11
+PHASE_NAMES = (
+    'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'fc1_reduce', 'head',
+    'fc1_dx', 'bwd_conv3_fc1dw', 'bwd_conv2', 'conv1_dw', 'update')
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4
@@ -80,6 +84,11 @@ SIGNATURES = {
          _vp],
     ),
     'dqz_learner_outputs': (_int, [_vp, _vp, _vp, _vp, _vp]),
+    'dqz_learner_profile': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
+         _int, ctypes.POINTER(ctypes.c_float), _vp],
+    ),
     'dqz_forward': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
     'dqz_forward_slots': (
         _int, [_vp, _vp, ctypes.POINTER(DqzStore), _vp, _int, _int, _vp, _vp]),

@@ -695,8 +695,17 @@ static int check_store(const dqz_store* S) {
 }
 
 // Forward of Z network copies; leaves h1/q in the learner scratch.
+// Phase markers for dqz_learner_profile: ev[i] is recorded before phase i.
+struct PhaseEvents {
+  hipEvent_t* ev;
+  void mark(int i, hipStream_t st) const {
+    if (ev) (void)hipEventRecord(ev[i], st);
+  }
+};
+
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_store* S, const int32_t* slots,
-                        const uint8_t* states, hipStream_t st) {
+                        const uint8_t* states, hipStream_t st, PhaseEvents pe = PhaseEvents{nullptr}) {
+  pe.mark(0, st);
   Conv1Fwd c1;
   static_cast<Shape&>(c1) = make_shape<CfgConv1>(Z, B * C1M, C1CO, C1KK, 1);
   c1.frames = S ? S->frames : nullptr;
@@ -708,6 +717,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_
   c1.b_off = L->off[1];
   c1.out = L->y1;
   DQZ_HIP((launch_gemm<CfgConv1>(st, c1)));
+  pe.mark(1, st);
 
   Conv2Fwd c2;
   static_cast<Shape&>(c2) = make_shape<CfgConv>(Z, B * C2M, C2CO, C2KK, 1);
@@ -718,6 +728,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_
   c2.b_off = L->off[3];
   c2.out = L->y2;
   DQZ_HIP((launch_gemm<CfgConv>(st, c2)));
+  pe.mark(2, st);
 
   Conv3Fwd c3;
   static_cast<Shape&>(c3) = make_shape<CfgConv>(Z, B * C3M, C3CO, C3KK, 1);
@@ -728,6 +739,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_
   c3.b_off = L->off[5];
   c3.out = L->y3;
   DQZ_HIP((launch_gemm<CfgConv>(st, c3)));
+  pe.mark(3, st);
 
   Fc1Fwd f1;
   static_cast<Shape&>(f1) = make_shape<CfgFc1>(Z, B, HID, FLAT, L->S_fc1);
@@ -736,6 +748,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_
   f1.w_off = L->off[6];
   f1.part = L->fc1p;
   DQZ_HIP((launch_gemm<CfgFc1>(st, f1)));
+  pe.mark(4, st);
 
   const int n = Z * B * HID;
   hipLaunchKernelGGL(fc1_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, L->fc1p, nz, L->off[7], Z,
@@ -744,8 +757,8 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const dqz_
   return DQZ_OK;
 }
 
-int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
-                     const float* is_weights, void* stream) {
+static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                     const float* is_weights, void* stream, PhaseEvents pe) {
   if (!L || !P || !P->online || !P->target || !P->mu || !P->nu || !slots)
     return fail(DQZ_ERR_INVALID, "null argument");
   if (int rc = check_store(S)) return rc;
@@ -759,7 +772,8 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   nz.which[0] = 0;
   nz.which[1] = 1;
   nz.which[2] = 1;
-  if (int rc = forward_impl(L, nz, Z, B, S, slots, nullptr, st)) return rc;
+  if (int rc = forward_impl(L, nz, Z, B, S, slots, nullptr, st, pe)) return rc;
+  pe.mark(5, st);
 
   Rms rms;
   rms.lr = L->cfg.learning_rate;
@@ -791,6 +805,7 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.gfc = L->gfc;
   hipLaunchKernelGGL(head_kernel, dim3(1), dim3(1024), 0, st, h);
   DQZ_HIP(hipGetLastError());
+  pe.mark(6, st);
 
   // fc1 dX -> dy3
   Fc1Dx fdx;
@@ -800,6 +815,7 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fdx.y3 = L->y3;
   fdx.dy3 = L->dy3;
   DQZ_HIP((launch_gemm<CfgFc1Dx>(st, fdx)));
+  pe.mark(7, st);
 
   // {conv3 dX, conv3 dW, fc1 dW + RMSProp}
   Conv3Dx c3dx;
@@ -823,6 +839,7 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   f1dw.w_off = L->off[6];
   f1dw.rms = rms;
   DQZ_HIP((launch_gemm<CfgBwd2>(st, c3dx, c3dw, f1dw)));
+  pe.mark(8, st);
 
   // {conv2 dX (phased), conv2 dW}
   Conv2DxPhased c2dx;
@@ -837,6 +854,7 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2dw.dy = L->dy2;
   c2dw.part = L->p2;
   DQZ_HIP((launch_gemm<CfgBwd3>(st, c2dx, c2dw)));
+  pe.mark(9, st);
 
   // conv1 dW
   Conv1Dw c1dw;
@@ -848,6 +866,7 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
   DQZ_HIP((launch_gemm<CfgBwd3>(st, c1dw)));
+  pe.mark(10, st);
 
   UpdArgs u;
   u.th = P->online;
@@ -870,7 +889,39 @@ int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   const int64_t nupd = L->sz[0] + L->sz[1] + L->sz[2] + L->sz[3] + L->sz[4] + L->sz[5] + HID + (int64_t)HID * A + u.nb2;
   hipLaunchKernelGGL(update_kernel, dim3((unsigned)((nupd + 255) / 256)), dim3(256), 0, st, u);
   DQZ_HIP(hipGetLastError());
+  pe.mark(DQZ_NUM_PHASES, st);
   return DQZ_OK;
+}
+
+int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                     const float* is_weights, void* stream) {
+  return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr});
+}
+
+int dqz_learner_profile(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                        const float* is_weights, int iters, float* phase_ms, void* stream) {
+  if (!phase_ms || iters < 1) return fail(DQZ_ERR_INVALID, "phase_ms must be non-null and iters >= 1");
+  hipStream_t st = (hipStream_t)stream;
+  hipEvent_t ev[DQZ_NUM_PHASES + 1];
+  for (int i = 0; i <= DQZ_NUM_PHASES; ++i) DQZ_HIP(hipEventCreate(&ev[i]));
+  for (int i = 0; i < DQZ_NUM_PHASES; ++i) phase_ms[i] = 0.f;
+  int rc = DQZ_OK;
+  for (int it = 0; it < iters && rc == DQZ_OK; ++it) {
+    rc = step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{ev});
+    if (rc) break;
+    if (hipEventSynchronize(ev[DQZ_NUM_PHASES]) != hipSuccess) {
+      rc = fail(DQZ_ERR_HIP, "hipEventSynchronize failed");
+      break;
+    }
+    for (int i = 0; i < DQZ_NUM_PHASES; ++i) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      phase_ms[i] += ms / (float)iters;
+    }
+  }
+  (void)st;
+  for (int i = 0; i <= DQZ_NUM_PHASES; ++i) (void)hipEventDestroy(ev[i]);
+  return rc;
 }
 
 int dqz_learner_outputs(dqz_learner* L, float* q_tm1, float* td, float* loss, void* stream) {

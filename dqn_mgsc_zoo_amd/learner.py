@@ -117,6 +117,15 @@ class Learner:
         self._h, ctypes.byref(self._params_c), store.c_ref(),
         _native.ptr(slots), _native.ptr(weights), _native.stream_handle(stream)))
 
+  def profile(self, store, slots, weights=None, iters=20, stream=None):
+    """Average ms per phase (HIP events on the launch stream), dict."""
+    out = (ctypes.c_float * _native.NUM_PHASES)()
+    _native.check(_native.lib().dqz_learner_profile(
+        self._h, ctypes.byref(self._params_c), store.c_ref(),
+        _native.ptr(slots), _native.ptr(weights), int(iters), out,
+        _native.stream_handle(stream)))
+    return dict(zip(_native.PHASE_NAMES, [float(x) for x in out]))
+
   def fetch_outputs(self, stream=None):
     """Copies (q_tm1, td, loss) of the last step into self tensors."""
     _native.check(_native.lib().dqz_learner_outputs(

@@ -1,0 +1,55 @@
+"""Synthetic replay contents for the learner benchmark.
+
+Frames ~ U{0..255}; fixed-length episodes so the trailing zero padding of
+the first three stacks of every episode (processors.py:57-69) occurs;
+a_tm1 ~ U{0..A-1}; r_t in {-1, 0, +1} with P = (0.01, 0.98, 0.01);
+discount_t = 0.99 except 0 on each episode's last transition.  The store is
+pre-filled to capacity directly on device (mirrors the 1e5-transition
+pre-fill of dqn_mgsc_batched_profiling/timing_atari.py).
+"""
+
+import torch
+
+from dqn_mgsc_zoo_amd import store as store_lib
+
+
+def fill_episodic(capacity, num_actions, episode_len=1000, seed=0,
+                  device='cuda'):
+  """Returns a FrameStore holding `capacity` transitions of fixed-length
+  episodes; frame pool = capacity + episodes frames (dedup'd stacks)."""
+  device = torch.device(device)
+  num_eps = (capacity + episode_len - 1) // episode_len
+  num_frames = num_eps * (episode_len + 1)
+  st = store_lib.FrameStore(capacity, num_frames, device=device)
+  gen = torch.Generator(device=device)
+  gen.manual_seed(int(seed))
+  chunk = 1 << 16
+  for i in range(0, num_frames, chunk):
+    j = min(num_frames, i + chunk)
+    st.frames[i:j] = torch.randint(0, 256, (j - i, store_lib.FRAME_BYTES),
+                                   generator=gen, dtype=torch.uint8,
+                                   device=device)
+  t = torch.arange(capacity, device=device, dtype=torch.int64)
+  ep = t // episode_len
+  k = t % episode_len + 1  # in-episode index of obs s_t (1..L)
+  base = ep * (episode_len + 1)
+  c = torch.arange(4, device=device, dtype=torch.int64)[None, :]
+
+  def stack(kk, newest):
+    n = torch.clamp(kk, max=3)[:, None]
+    idx = newest[:, None] - n + c
+    return torch.where(c <= n, idx, torch.full_like(idx, -1))
+
+  fidx = torch.cat([stack(k - 1, base + k - 1), stack(k, base + k)], dim=1)
+  st.fidx.copy_(fidx.to(torch.int32))
+  st.action.copy_(torch.randint(0, num_actions, (capacity,), generator=gen,
+                                device=device, dtype=torch.int32))
+  u = torch.rand((capacity,), generator=gen, device=device)
+  reward = torch.zeros((capacity,), device=device)
+  reward = torch.where(u < 0.01, torch.full_like(reward, -1.0), reward)
+  reward = torch.where(u > 0.99, torch.full_like(reward, 1.0), reward)
+  st.reward.copy_(reward)
+  last = k == episode_len
+  st.discount.copy_(torch.where(last, torch.zeros_like(reward),
+                                torch.full_like(reward, 0.99)))
+  return st

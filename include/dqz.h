@@ -115,6 +115,22 @@ int dqz_learner_destroy(dqz_learner* learner);
 int dqz_learner_step(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
                      const int32_t* slots, const float* is_weights, void* stream);
 
+/* Phases of one learner step, in launch order (dqz_learner_profile):
+ *  0 conv1 fwd (frame gather fused)   1 conv2 fwd   2 conv3 fwd
+ *  3 fc1 fwd (split-K)                4 fc1 reduce+bias+ReLU
+ *  5 head: fc2 + TD loss + dq + fc2/fc1b grads
+ *  6 fc1 dX                           7 {conv3 dX, conv3 dW, fc1 dW+RMSProp}
+ *  8 {conv2 dX, conv2 dW}             9 conv1 dW
+ * 10 dW reduce + RMSProp (all leaves but fc1/w) */
+#define DQZ_NUM_PHASES 11
+
+/* Runs `iters` learner steps with a hipEvent recorded on `stream` before
+ * every phase and returns the average milliseconds per phase in
+ * phase_ms[DQZ_NUM_PHASES].  Synchronises the stream (host output). */
+int dqz_learner_profile(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                        const int32_t* slots, const float* is_weights, int iters, float* phase_ms,
+                        void* stream);
+
 /* Device-to-device copies of the last step's outputs (any may be NULL):
  * q_tm1 [B][A] online Q(s_tm1), td [B] TD errors, loss [1] mean loss. */
 int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* loss, void* stream);
