@@ -49,7 +49,6 @@ def phase_flops(algo, batch):
       'conv2_fwd': 2 * z * b * MAC['conv2'],
       'conv3_fwd': 2 * z * b * MAC['conv3'],
       'fc1_fwd': 2 * z * b * MAC['fc1'],
-      'fc1_reduce': 0,
       'head': 2 * z * b * MAC['fc2'],
       'fc1_dx': 2 * b * MAC['fc1'],
       'bwd_conv3_fc1dw': 2 * b * (2 * MAC['conv3'] + MAC['fc1']),

@@ -17,10 +17,10 @@ ALGO_DQN = 0
 ALGO_DOUBLE = 1
 ALGO_PER = 2
 NUM_LEAVES = 10
-NUM_PHASES = 11
+NUM_PHASES = 10
 PHASE_NAMES = (
-    'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'fc1_reduce', 'head',
-    'fc1_dx', 'bwd_conv3_fc1dw', 'bwd_conv2', 'conv1_dw', 'update')
+    'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_dx',
+    'bwd_conv3_fc1dw', 'bwd_conv2', 'conv1_dw', 'update')
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4

@@ -1,0 +1,103 @@
+// common.hpp — geometry of the NatureQNetwork, error plumbing, small device
+// helpers shared by the libdqz kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "dqz.h"
+
+namespace dqz {
+
+// ---------------------------------------------------------------------------
+// errors (thread-local message behind dqz_last_error)
+
+inline std::string& err_buf() {
+  static thread_local std::string s;
+  return s;
+}
+
+inline int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  err_buf() = buf;
+  return code;
+}
+
+#define DQZ_HIP(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) return fail(DQZ_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// geometry (networks.py:181-221): NHWC activations, HWIO weights
+
+constexpr int FH = 84, FW = 84, FC = 4, FB = FH * FW;
+constexpr int C1K = 8, C1S = 4, C1CO = 32, C1O = 20, C1M = C1O * C1O, C1KK = C1K * C1K * FC;       // 400, 256
+constexpr int C2K = 4, C2S = 2, C2CI = 32, C2CO = 64, C2O = 9, C2M = C2O * C2O, C2KK = 16 * C2CI;  // 81, 512
+constexpr int C3K = 3, C3CI = 64, C3CO = 64, C3O = 7, C3M = C3O * C3O, C3KK = 9 * C3CI;           // 49, 576
+constexpr int FLAT = C3M * C3CO;                                                                  // 3136
+constexpr int HID = 512;
+constexpr int MAXA = 32;
+constexpr int MAXB = 256;
+
+// conv1 work unit: 5 output rows (100 positions) of one sample; its input
+// window is 24 rows x 84 columns x 4 channels.
+constexpr int C1_ROWS = 5;
+constexpr int C1_BLOCKS = C1O / C1_ROWS;          // 4
+constexpr int C1_POS = C1_ROWS * C1O;             // 100
+constexpr int C1_IN_ROWS = C1S * C1_ROWS + 4;     // 24
+constexpr int C1_PLANE = C1_IN_ROWS * FW;         // 2016 floats per channel
+constexpr int C1_IN_FLOATS = FC * C1_PLANE;       // 8064
+
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+// networks.py:192: x.astype(jnp.float32) / 255.0 (IEEE division, not a reciprocal multiply)
+__device__ __forceinline__ float u8n(unsigned v) { return (float)v / 255.0f; }
+
+struct NetZ {
+  const float* p[3];  // parameter buffer of network copy z
+  int which[3];       // input stack of copy z: 0 = s_tm1, 1 = s_t
+};
+
+// optax 0.1.2 scale_by_stddev + scale(-lr) (dqn/run_atari.py:208-213):
+//   mu = (1-decay) g + decay mu ; nu = (1-decay) g^2 + decay nu
+//   theta += -lr * g * rsqrt(nu - mu^2 + eps)
+struct Rms {
+  float lr, decay, c1, eps;
+  __device__ __forceinline__ void apply(float* th, float* mu, float* nu, int64_t i, float g) const {
+    const float m = c1 * g + decay * mu[i];
+    const float v = c1 * (g * g) + decay * nu[i];
+    mu[i] = m;
+    nu[i] = v;
+    th[i] = th[i] + (-lr) * (g * rsqrtf(v - m * m + eps));
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Philox4x32-10 (Salmon et al., SC'11).
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+}  // namespace dqz

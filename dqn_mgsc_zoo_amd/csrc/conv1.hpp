@@ -1,0 +1,176 @@
+// conv1.hpp — conv1 (8x8 stride 4, 4->32) forward and weight-gradient
+// kernels with the replay frame gather fused in.
+//
+// A workgroup owns 5 output rows (100 positions) of one sample.  It gathers
+// the 24x84 input window of the sample's four stack channels straight from
+// the HBM frame pool (16-byte loads; a channel whose frame index is -1 is
+// the trailing zero padding of processors.py:57-69), normalises it with
+// x / 255.0 (networks.py:192) into a [channel][row][col] f32 LDS image, and
+// runs v_mfma_f32_32x32x2_f32 with both operands read from LDS by
+// ds_read_b32 at compile-time immediate offsets.  Stacks never exist in HBM.
+#pragma once
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace dqz {
+
+struct Conv1Src {
+  const uint8_t* frames;  // frame pool (null when `states` is used)
+  const int32_t* fidx;    // [capacity][8]
+  const int32_t* slots;   // [B]
+  const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
+};
+
+__device__ __forceinline__ void store_bytes_as_f32(float* dst, uint4 v) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float4 f;
+    f.x = u8n(w[i] & 0xFF);
+    f.y = u8n((w[i] >> 8) & 0xFF);
+    f.z = u8n((w[i] >> 16) & 0xFF);
+    f.w = u8n(w[i] >> 24);
+    *reinterpret_cast<float4*>(dst + 4 * i) = f;
+  }
+}
+
+// Stages input rows [20*rb, 20*rb + 24) of sample b, stack `which`, as
+// s_in[ci][row][col] = pixel / 255.
+__device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& src, int b, int which, int rb) {
+  const int row0 = rb * C1S * C1_ROWS;
+  constexpr int QPC = C1_PLANE / 16;  // 126 16-byte pieces per channel
+  if (src.states) {
+    const uint4* g = reinterpret_cast<const uint4*>(src.states + ((int64_t)b * FH + row0) * FW * FC);
+    for (int i = threadIdx.x; i < C1_PLANE * FC / 16; i += blockDim.x) {
+      const uint4 v = g[i];  // 4 pixels x 4 channels
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+      const int p = 4 * i;
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) {
+        float4 f;
+        f.x = u8n((w[0] >> (8 * ci)) & 0xFF);
+        f.y = u8n((w[1] >> (8 * ci)) & 0xFF);
+        f.z = u8n((w[2] >> (8 * ci)) & 0xFF);
+        f.w = u8n((w[3] >> (8 * ci)) & 0xFF);
+        *reinterpret_cast<float4*>(s_in + ci * C1_PLANE + p) = f;
+      }
+    }
+  } else {
+    const int slot = src.slots[b];
+    for (int i = threadIdx.x; i < FC * QPC; i += blockDim.x) {
+      const int ci = i / QPC, j = i % QPC;
+      const int f = src.fidx[(int64_t)slot * 8 + which * 4 + ci];
+      float* dst = s_in + ci * C1_PLANE + j * 16;
+      if (f < 0) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(dst + 4 * q) = z;
+      } else {
+        const uint4* g = reinterpret_cast<const uint4*>(src.frames + (int64_t)f * FB + row0 * FW);
+        store_bytes_as_f32(dst, g[j]);
+      }
+    }
+  }
+}
+
+struct Conv1FwdArgs {
+  Conv1Src src;
+  NetZ nz;
+  int64_t w_off, b_off;
+  int B;
+  float* out;  // y1 [Z][B][400][32]
+};
+
+// grid (4 row blocks, B, Z); 256 threads; each wave owns 32 positions x 32
+// channels (the 4th wave's tile is 4/32 live).
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_in = smem;                  // 8064
+  float* s_w = smem + C1_IN_FLOATS;    // 256 x 32
+  const int rb = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const float* w = a.nz.p[z] + a.w_off;
+  for (int i = threadIdx.x; i < C1KK * C1CO / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(s_w)[i] = reinterpret_cast<const float4*>(w)[i];
+  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, i = lane & 31;
+  const int p = min(32 * wave + i, C1_POS - 1);
+  const int oh = p / C1O, ow = p % C1O;
+  const float* pa = s_in + h * C1_PLANE + (C1S * oh) * FW + C1S * ow;
+  const float* pb = s_w + h * C1CO + i;
+  f32x16 acc = {};
+#pragma unroll
+  for (int j = 0; j < 128; ++j) {
+    // k = 2j + h  ->  kh = j >> 4, kw = (j >> 1) & 7, ci = 2 (j & 1) + h
+    const float av = pa[2 * (j & 1) * C1_PLANE + (j >> 4) * FW + ((j >> 1) & 7)];
+    const float bv = pb[64 * j];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  }
+  // C/D map of 32x32x2: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+  const float bias = a.nz.p[z][a.b_off + i];
+  float* out = a.out + (((int64_t)z * a.B + b) * C1M + rb * C1_POS) * C1CO;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int pos = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (pos < C1_POS) out[pos * C1CO + i] = relu(acc[r] + bias);
+  }
+}
+
+struct Conv1DwArgs {
+  Conv1Src src;
+  int which;
+  const float* dy1;  // [B][400][32] (online copy)
+  float* part;       // [B*4][257][32]: dW rows 0..255 (HWIO order), db row 256
+};
+
+// Partial dW/db of one 100-position block: part[k][co] = sum_p x(p,k) dy(p,co).
+// grid (4 row blocks, B); wave w owns kernel rows [64w, 64w+64) (two 32-row
+// MFMA tiles; row = kh*32 + kw*4 + ci), K' = 100 positions.
+__global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_in = smem;                 // 8064
+  float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
+  const int rb = blockIdx.x, b = blockIdx.y;
+  const float* dy = a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO;
+  for (int i = threadIdx.x; i < C1_POS * C1CO / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(s_dy)[i] = reinterpret_cast<const float4*>(dy)[i];
+  stage_conv1_input(s_in, a.src, b, a.which, rb);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, i = lane & 31;
+  const int kw = i >> 2, ci = i & 3;
+  float* part = a.part + ((int64_t)b * C1_BLOCKS + rb) * (C1KK + 1) * C1CO;
+  if (threadIdx.x < C1CO) {  // bias row
+    float s = 0.f;
+    for (int p = 0; p < C1_POS; ++p) s += s_dy[p * C1CO + threadIdx.x];
+    part[C1KK * C1CO + threadIdx.x] = s;
+  }
+  const float* pa = s_in + ci * C1_PLANE + kw + 4 * h;
+  const float* pb = s_dy + h * C1CO + i;
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    const int kh = 2 * wave + t2;  // 32-row tile index == kh
+    const float* pat = pa + kh * FW;
+    f32x16 acc = {};
+#pragma unroll
+    for (int j = 0; j < C1_POS / 2; ++j) {
+      const int p0 = 2 * j;  // positions p0 + h share an output row
+      const float av = pat[(C1S * (p0 / C1O)) * FW + C1S * (p0 % C1O)];
+      const float bv = pb[64 * j];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      part[(kh * 32 + row) * C1CO + i] = acc[r];
+    }
+  }
+}
+
+constexpr size_t kConv1FwdSmem = (C1_IN_FLOATS + C1KK * C1CO) * sizeof(float);
+constexpr size_t kConv1DwSmem = (C1_IN_FLOATS + C1_POS * C1CO) * sizeof(float);
+
+}  // namespace dqz

@@ -1,0 +1,225 @@
+// head.hpp — fc1 split-K reduce + fc2 + TD loss (one workgroup per sample),
+// the optimizer update kernel, and the replay sampler / gather kernels.
+#pragma once
+#include "common.hpp"
+
+namespace dqz {
+
+struct HeadArgs {
+  const float* fc1p;  // fc1 split-K partials [Z][S][B][512]
+  int S;
+  float* h1;  // [Z][B][512] (written)
+  NetZ nz;
+  int64_t b1_off, w2_off, b2_off;
+  int Z, B, A, algo, shared_bias, fwd_only;
+  const int32_t* slots;
+  const int32_t* action;
+  const float* reward;
+  const float* discount;
+  const float* weights;  // PER importance weights or null
+  float bound;           // grad_error_bound
+  float* q;              // [Z][B][A]
+  float* td;             // [B]
+  float* loss_part;      // [B] per-sample 0.5 td^2 w
+  float* gq;             // [B] d loss / d q_tm1[b, a_b]
+  int32_t* ga;           // [B] a_b
+  float* dz1;            // [B][512] d loss / d fc1 pre-activation (online)
+};
+
+// One workgroup (512 threads = hidden units) per sample b:
+//   h1 = relu(b1 + sum_s partial), q = h1 @ W2 + b2 for every copy z,
+//   TD error (rlax 0.1.2 q_learning / double_q_learning as called at
+//   dqn/agent.py:94-106, double_q/agent.py:97-106, prioritized/agent.py:97-113):
+//   td = stopgrad(r + d * v) - q_tm1[a]; loss_b = 0.5 td^2 [* w];
+//   the cotangent at td is clip(w td / B, +-bound) because rlax.clip_gradient
+//   clips the incoming gradient; dq[b, a_b] = -that; dz1 = dq W2[:, a_b] relu'.
+// Cross-sample sums (fc2/fc1-bias grads, mean loss) happen in update_kernel.
+__global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
+  __shared__ float s_red[8][MAXA];
+  __shared__ float s_q[3][MAXA];
+  __shared__ float s_g;
+  __shared__ int s_a;
+  const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = n >> 6;
+  const int A = h.A, B = h.B;
+  // Issue the per-sample batch loads early (their latency overlaps the fc1 sums).
+  int a_tm1 = 0;
+  float r = 0.f, d = 0.f, w = 1.f;
+  if (!h.fwd_only && n == 0) {
+    const int slot = h.slots[b];
+    a_tm1 = h.action[slot];
+    r = h.reward[slot];
+    d = h.discount[slot];
+    if (h.weights) w = h.weights[b];
+  }
+  float h0 = 0.f;
+  for (int z = 0; z < h.Z; ++z) {
+    const float* part = h.fc1p + ((int64_t)z * h.S * B + b) * HID + n;
+    float acc0 = h.nz.p[z][h.b1_off + n], acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int s = 0;
+    for (; s + 4 <= h.S; s += 4) {
+      acc0 += part[(int64_t)(s + 0) * B * HID];
+      acc1 += part[(int64_t)(s + 1) * B * HID];
+      acc2 += part[(int64_t)(s + 2) * B * HID];
+      acc3 += part[(int64_t)(s + 3) * B * HID];
+    }
+    for (; s < h.S; ++s) acc0 += part[(int64_t)s * B * HID];
+    const float hv = relu((acc0 + acc1) + (acc2 + acc3));
+    h.h1[((int64_t)z * B + b) * HID + n] = hv;
+    if (z == 0) h0 = hv;
+    const float* w2 = h.nz.p[z] + h.w2_off + n * A;
+    for (int a = 0; a < A; ++a) {
+      const float sa = wave_sum(hv * w2[a]);
+      if (lane == 0) s_red[wave][a] = sa;
+    }
+    __syncthreads();
+    if (n < A) {
+      float sa = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) sa += s_red[ww][n];
+      const float qv = sa + h.nz.p[z][h.b2_off + (h.shared_bias ? 0 : n)];
+      s_q[z][n] = qv;
+      h.q[((int64_t)z * B + b) * A + n] = qv;
+    }
+    __syncthreads();
+  }
+  if (h.fwd_only) return;
+  if (n == 0) {
+    float v;
+    if (h.algo == DQZ_ALGO_DQN) {
+      v = s_q[1][0];
+      for (int a = 1; a < A; ++a) v = fmaxf(v, s_q[1][a]);
+    } else {
+      int am = 0;  // online Q(s_t) selects, jnp.argmax: first maximum
+      for (int a = 1; a < A; ++a)
+        if (s_q[2][a] > s_q[2][am]) am = a;
+      v = s_q[1][am];
+    }
+    const float td = (r + d * v) - s_q[0][a_tm1];
+    float g = w * td / (float)B;  // d mean(l2(td) * w) / d td
+    g = fminf(fmaxf(g, -h.bound), h.bound);
+    h.td[b] = td;
+    h.loss_part[b] = 0.5f * td * td * w;
+    h.gq[b] = -g;
+    h.ga[b] = a_tm1;
+    s_g = -g;
+    s_a = a_tm1;
+  }
+  __syncthreads();
+  const float wv = h.nz.p[0][h.w2_off + n * A + s_a];
+  h.dz1[(int64_t)b * HID + n] = h0 > 0.f ? s_g * wv : 0.f;
+}
+
+struct UpdArgs {
+  float *th, *mu, *nu;
+  int64_t off[10];
+  int64_t sz[10];
+  const float* p1;  // conv1 dW partials [S1][257][32]
+  const float* p2;  // conv2 dW partials [S2][513][64]
+  const float* p3;  // conv3 dW partials [S3][577][64]
+  int S1, S2, S3;
+  const float* h1;   // [B][512] online fc1 output (z = 0)
+  const float* dz1;  // [B][512]
+  const float* gq;   // [B]
+  const int32_t* ga; // [B]
+  const float* loss_part;
+  float* loss;
+  int A, B, nb2;
+  Rms rms;
+};
+
+constexpr int UPD_PARAMS = 64;  // parameters per workgroup
+constexpr int UPD_GROUPS = 4;   // threads sharing one parameter's reduction
+
+// Sum of p[s * stride + i] over s = g, g + G, g + 2G, ... < S.
+__device__ __forceinline__ float sum_split(const float* p, int S, int64_t stride, int64_t i, int g) {
+  float a0 = 0.f, a1 = 0.f;
+  int s = g;
+  for (; s + UPD_GROUPS < S; s += 2 * UPD_GROUPS) {
+    a0 += p[s * stride + i];
+    a1 += p[(s + UPD_GROUPS) * stride + i];
+  }
+  if (s < S) a0 += p[s * stride + i];
+  return a0 + a1;
+}
+
+// Reduces every gradient that crosses samples or split-K chunks and applies
+// centered RMSProp to every leaf except fc1/w (fused into its dW epilogue).
+// 256 threads = 64 parameters x 4 reduction groups, combined through LDS.
+__global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
+  __shared__ float s_part[UPD_GROUPS][UPD_PARAMS];
+  const int pl = threadIdx.x % UPD_PARAMS, grp = threadIdx.x / UPD_PARAMS;
+  const int64_t i = (int64_t)blockIdx.x * UPD_PARAMS + pl;
+  const int64_t n0 = u.sz[0] + u.sz[1], n1 = n0 + u.sz[2] + u.sz[3], n2 = n1 + u.sz[4] + u.sz[5];
+  const int64_t n3 = n2 + HID, n4 = n3 + (int64_t)HID * u.A, n5 = n4 + u.nb2;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < u.B; ++b) s += u.loss_part[b];
+    u.loss[0] = s / (float)u.B;
+  }
+  float g = 0.f;
+  int64_t dst = -1;
+  if (i < n0) {  // conv1: w rows 0..255, bias row 256
+    g = sum_split(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, i, grp);
+    dst = i < u.sz[0] ? u.off[0] + i : u.off[1] + (i - u.sz[0]);
+  } else if (i < n1) {
+    const int64_t j = i - n0;
+    g = sum_split(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, j, grp);
+    dst = j < u.sz[2] ? u.off[2] + j : u.off[3] + (j - u.sz[2]);
+  } else if (i < n2) {
+    const int64_t j = i - n1;
+    g = sum_split(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, j, grp);
+    dst = j < u.sz[4] ? u.off[4] + j : u.off[5] + (j - u.sz[4]);
+  } else if (i < n3) {  // fc1 bias: sum_b dz1
+    const int j = (int)(i - n2);
+    for (int b = grp; b < u.B; b += UPD_GROUPS) g += u.dz1[(int64_t)b * HID + j];
+    dst = u.off[7] + j;
+  } else if (i < n4) {  // fc2 w[j][a] = sum_{b: a_b = a} h1[b][j] gq[b]
+    const int64_t jj = i - n3;
+    const int j = (int)(jj / u.A), a = (int)(jj % u.A);
+    for (int b = grp; b < u.B; b += UPD_GROUPS)
+      if (u.ga[b] == a) g += u.h1[(int64_t)b * HID + j] * u.gq[b];
+    dst = u.off[8] + jj;
+  } else if (i < n5) {  // fc2 b
+    const int a = (int)(i - n4);
+    for (int b = grp; b < u.B; b += UPD_GROUPS)
+      if (u.nb2 == 1 || u.ga[b] == a) g += u.gq[b];
+    dst = u.off[9] + a;
+  }
+  s_part[grp][pl] = g;
+  __syncthreads();
+  if (grp == 0 && dst >= 0) {
+    const float gs = (s_part[0][pl] + s_part[1][pl]) + (s_part[2][pl] + s_part[3][pl]);
+    u.rms.apply(u.th, u.mu, u.nu, dst, gs);
+  }
+}
+
+__global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
+                                      uint64_t* counter, int32_t* out) {
+  const uint64_t ctr = *counter;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x5EED5u),
+                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+    const uint64_t u = ((uint64_t)r.x << 32) | r.y;
+    const int64_t j = (int64_t)__umul64hi(u, (uint64_t)size);  // uniform in [0, size)
+    out[i] = (int32_t)((base + j) % capacity);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *counter = ctr + 1;
+}
+
+__global__ void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx, const int32_t* slots, int n,
+                                     int which, uint8_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * FB) return;
+  const int b = (int)(i / FB), p = (int)(i % FB);
+  const int slot = slots[b];
+  unsigned c[4];
+#pragma unroll
+  for (int ci = 0; ci < 4; ++ci) {
+    const int f = fidx[(int64_t)slot * 8 + which * 4 + ci];
+    c[ci] = f < 0 ? 0u : frames[(int64_t)f * FB + p];
+  }
+  reinterpret_cast<uchar4*>(out)[i] = make_uchar4(c[0], c[1], c[2], c[3]);
+}
+
+}  // namespace dqz

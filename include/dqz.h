@@ -117,12 +117,12 @@ int dqz_learner_step(dqz_learner* learner, const dqz_params* params, const dqz_s
 
 /* Phases of one learner step, in launch order (dqz_learner_profile):
  *  0 conv1 fwd (frame gather fused)   1 conv2 fwd   2 conv3 fwd
- *  3 fc1 fwd (split-K)                4 fc1 reduce+bias+ReLU
- *  5 head: fc2 + TD loss + dq + fc2/fc1b grads
- *  6 fc1 dX                           7 {conv3 dX, conv3 dW, fc1 dW+RMSProp}
- *  8 {conv2 dX, conv2 dW}             9 conv1 dW
- * 10 dW reduce + RMSProp (all leaves but fc1/w) */
-#define DQZ_NUM_PHASES 11
+ *  3 fc1 fwd (split-K)
+ *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample)
+ *  5 fc1 dX                           6 {conv3 dX, conv3 dW, fc1 dW+RMSProp}
+ *  7 {conv2 dX, conv2 dW}             8 conv1 dW (frame gather fused)
+ *  9 gradient reductions + RMSProp (all leaves but fc1/w) */
+#define DQZ_NUM_PHASES 10
 
 /* Runs `iters` learner steps with a hipEvent recorded on `stream` before
  * every phase and returns the average milliseconds per phase in
