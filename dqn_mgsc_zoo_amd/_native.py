@@ -97,6 +97,17 @@ SIGNATURES = {
     'dqz_gather_stacks': (
         _int, [ctypes.POINTER(DqzStore), _vp, _int, _int, _vp, _vp]),
     'dqz_target_copy': (_int, [_vp, _vp, _i64, _vp]),
+    'dqz_logit_buffer_create': (_int, [_i64, _int, ctypes.POINTER(_vp)]),
+    'dqz_logit_buffer_destroy': (_int, [_vp]),
+    'dqz_logits_add': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    'dqz_logits_sample': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
+    'dqz_uniform_philox': (_int, [ctypes.c_uint64, _vp, _int, _vp, _vp]),
+    'dqz_sumtree_set': (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
+    'dqz_sumtree_query': (_int, [_vp, _i64, _vp, _int, _vp, _vp]),
+    'dqz_per_sample': (
+        _int,
+        [_vp, _i64, _i64, _i64, _i64, _int, ctypes.c_double, ctypes.c_double,
+         _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

@@ -19,6 +19,7 @@
 #include "conv1.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
+#include "sampling.hpp"
 
 namespace dqz {
 
@@ -610,6 +611,135 @@ int dqz_gather_stacks(const dqz_store* S, const int32_t* slots, int n, int which
   const int64_t total = (int64_t)n * FB;
   hipLaunchKernelGGL(gather_stacks_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      S->frames, S->fidx, slots, n, which, out);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// learned-logit and prioritized samplers
+
+struct dqz_logit_buffer {
+  int64_t capacity;
+  int nblocks, max_queries;
+  void* block;  // MaxSum[nblocks] | double bsum[nblocks] | float lse
+  MaxSum* part;
+  double* bsum;
+  float* lse;
+};
+
+int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out) {
+  if (!out || capacity < 1 || max_queries < 1) return fail(DQZ_ERR_INVALID, "bad logit buffer arguments");
+  dqz_logit_buffer* b = new dqz_logit_buffer();
+  b->capacity = capacity;
+  b->max_queries = max_queries;
+  b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
+  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double)) + 64;
+  if (hipMalloc(&b->block, bytes) != hipSuccess) {
+    delete b;
+    return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
+  }
+  char* p = (char*)b->block;
+  b->bsum = (double*)p;
+  b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
+  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
+  *out = b;
+  return DQZ_OK;
+}
+
+int dqz_logit_buffer_destroy(dqz_logit_buffer* b) {
+  if (!b) return DQZ_OK;
+  if (b->block) (void)hipFree(b->block);
+  delete b;
+  return DQZ_OK;
+}
+
+static int logits_lse(dqz_logit_buffer* b, const float* logits, float* write_logits, int64_t write_pos,
+                      int64_t size, float* lse_out, hipStream_t st) {
+  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part, b->nblocks, lse_out ? lse_out : b->lse,
+                     write_logits, write_pos, size);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_logits_add(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
+                   float* lse_out, void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
+  if (write_pos < 0 || write_pos >= b->capacity || clear_pos >= b->capacity)
+    return fail(DQZ_ERR_INVALID, "position out of range");
+  if (size < 0) return fail(DQZ_ERR_INVALID, "size must be >= 0");
+  hipStream_t st = (hipStream_t)stream;
+  if (clear_pos >= 0) {
+    hipLaunchKernelGGL(logit_clear_kernel, dim3(1), dim3(64), 0, st, logits, clear_pos);
+    DQZ_HIP(hipGetLastError());
+  }
+  if (int rc = logits_lse(b, logits, logits, write_pos, size, lse_out, st)) return rc;
+  if (lse_out) DQZ_HIP(hipMemcpyAsync(b->lse, lse_out, sizeof(float), hipMemcpyDeviceToDevice, st));
+  return DQZ_OK;
+}
+
+int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
+                      void* stream) {
+  if (!b || !logits || !uniforms || !out_idx) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 1 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = logits_lse(b, logits, nullptr, -1, 0, nullptr, st)) return rc;
+  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse,
+                     b->bsum);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(softmax_choice_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse, b->bsum,
+                     b->nblocks, uniforms, out_idx);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream) {
+  if (!counter_dev || !out || n < 1 || n > 65536) return fail(DQZ_ERR_INVALID, "bad argument");
+  hipLaunchKernelGGL(philox_uniform_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, seed, counter_dev, n, out);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+static int tree_levels(int64_t cap) {
+  int l = 0;
+  while ((int64_t(1) << l) < cap) ++l;
+  return l;
+}
+
+int dqz_sumtree_set(double* tree, int64_t cap, const int64_t* idx, const double* values, int n, void* stream) {
+  if (!tree || !idx || !values) return fail(DQZ_ERR_INVALID, "null argument");
+  if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
+  if (n < 0 || n > 65536) return fail(DQZ_ERR_INVALID, "n out of range");
+  if (n == 0) return DQZ_OK;
+  hipLaunchKernelGGL(sumtree_set_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, tree_levels(cap), idx,
+                     values, n);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_sumtree_query(const double* tree, int64_t cap, const double* targets, int n, int64_t* out, void* stream) {
+  if (!tree || !targets || !out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
+  if (n < 0) return fail(DQZ_ERR_INVALID, "n must be >= 0");
+  if (n == 0) return DQZ_OK;
+  hipLaunchKernelGGL(sumtree_query_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, tree, cap, targets,
+                     n, out);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t size, int64_t capacity, int n,
+                   double usp, double beta, int normalize, uint64_t seed, uint64_t* counter_dev, int32_t* out_slots,
+                   float* out_weights, double* out_probs, void* stream) {
+  if (!tree || !counter_dev || !out_slots || !out_weights) return fail(DQZ_ERR_INVALID, "null argument");
+  if (cap < capacity || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two >= capacity");
+  if (size < 1) return fail(DQZ_ERR_INVALID, "No IDs to sample.");
+  if (n < 1 || n > 1024) return fail(DQZ_ERR_INVALID, "n must be in [1, 1024]");
+  if (!(beta >= 0.0 && beta <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= exponent <= 1.");
+  if (!(usp >= 0.0 && usp <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= uniform_sample_probability <= 1.");
+  hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, live_base, size,
+                     capacity, n, usp, beta, normalize, seed, counter_dev, out_slots, out_weights, out_probs);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }

@@ -78,10 +78,6 @@ class FrameStore:
     return out
 
 
-def _frame_key(frame):
-  return hash(frame.tobytes())
-
-
 class FrameAllocator:
   """Host-side assignment of pool indices to the channels of added stacks.
 
@@ -118,13 +114,16 @@ class FrameAllocator:
       if not ch.any():
         out.append(-1)
         continue
-      key = _frame_key(ch)
-      pos = self._recent.get(key)
-      if pos is not None and self._pos - pos <= self._store.num_frames:
+      raw = ch.tobytes()
+      key = hash(raw)
+      hit = self._recent.get(key)
+      if (hit is not None and hit[1] == raw and
+          self._pos - hit[0] <= self._store.num_frames):
+        pos = hit[0]
         self._recent.move_to_end(key)
       else:
         pos = self._append(ch, oldest_live_slot)
-        self._recent[key] = pos
+        self._recent[key] = (pos, raw)
         while len(self._recent) > self._window:
           self._recent.popitem(last=False)
       refs.append(pos)
@@ -168,3 +167,15 @@ class FrameAllocator:
 
   def forget(self, slot):
     self._min_ref.pop(slot, None)
+
+  def get_state(self):
+    return {'mode': self._mode, 'per_slot': self._per_slot, 'pos': self._pos,
+            'recent': list(self._recent.items()),
+            'min_ref': dict(self._min_ref)}
+
+  def set_state(self, state):
+    self._mode = state['mode']
+    self._per_slot = state['per_slot']
+    self._pos = state['pos']
+    self._recent = collections.OrderedDict(state['recent'])
+    self._min_ref = dict(state['min_ref'])

@@ -161,6 +161,52 @@ int dqz_sample_uniform(int64_t base, int64_t size, int64_t capacity, int n, uint
 int dqz_gather_stacks(const dqz_store* store, const int32_t* slots, int n, int which,
                       uint8_t* out, void* stream);
 
+/* ---- learned-logit replay sampling (dqn_mgsc_batched replays) ----------
+ * logits: device f32 [capacity], -inf marks an empty slot
+ * (CircularLogitBuffer / MGSCReservoirDistribution, replay_circular.py:148-248,
+ * 500-565).  A dqz_logit_buffer owns only the reduction scratch. */
+typedef struct dqz_logit_buffer dqz_logit_buffer;
+int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out);
+int dqz_logit_buffer_destroy(dqz_logit_buffer* buf);
+
+/* Default logit of an added item (replay_circular.py:166-179, :518-533):
+ * if clear_pos >= 0, logits[clear_pos] = -inf first (the reservoir
+ * `replace`); then logits[write_pos] = size == 0 ? 0
+ *   : logsumexp(logits[0:capacity]) - log(size).  lse_out (device f32) may be NULL. */
+int dqz_logits_add(dqz_logit_buffer* buf, float* logits, int64_t clear_pos, int64_t write_pos,
+                   int64_t size, float* lse_out, void* stream);
+
+/* Softmax sampling with replacement (CircularLogitBuffer.sample,
+ * replay_circular.py:205-217 = Generator.choice(capacity, n, p=softmax)):
+ * p = exp(x - logsumexp(x)) in f32, cdf = cumsum(float64 p) / total,
+ * out_idx[i] = first slot with cdf > uniforms[i].  uniforms: device f64 [n]
+ * in [0,1) (host Generator draws for parity, or dqz_uniform_philox). */
+int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
+                      int64_t* out_idx, void* stream);
+
+/* n uniform doubles in [0,1) from Philox4x32-10 (counter advanced on device). */
+int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream);
+
+/* ---- prioritized replay: fp64 sum tree in HBM (replay.py:379-559) -------
+ * tree: device f64 [2*cap], cap a power of two, node i has children 2i, 2i+1,
+ * root at 1, leaves at [cap, 2cap) -- the layout of the host SumTree.
+ * set: leaves idx[k] = values[k] (k < n <= 65536), ancestors recomputed as
+ * left + right (bit-identical to SumTree.set).  query: SumTree._query_single
+ * per target; out = -1 when target is outside [0, root). */
+int dqz_sumtree_set(double* tree, int64_t cap, const int64_t* idx, const double* values, int n,
+                    void* stream);
+int dqz_sumtree_query(const double* tree, int64_t cap, const double* targets, int n, int64_t* out,
+                      void* stream);
+
+/* PrioritizedDistribution.sample + importance_sampling_weights on device
+ * (replay.py:680-716, 344-376) with Philox draws; tree leaf index = replay
+ * slot; live slots are (live_base + j) mod capacity, j < size.  n <= 1024.
+ * out_probs (device f64 [n]) may be NULL. */
+int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t size, int64_t capacity,
+                   int n, double uniform_sample_probability, double importance_exponent,
+                   int normalize_weights, uint64_t seed, uint64_t* counter_dev, int32_t* out_slots,
+                   float* out_weights, double* out_probs, void* stream);
+
 /* Target sync: target <- online (dqn/agent.py:155-156; hard copy, not Polyak). */
 int dqz_target_copy(float* target, const float* online, int64_t total, void* stream);
 

@@ -1,0 +1,192 @@
+"""GPU: device samplers vs the reference's golden vectors and the oracle.
+
+* learned-logit buffers (replay_circular.py): logits after add / popleft /
+  replace / setitem within 1e-6 (f32 log-sum-exp summation order differs);
+  softmax-sampled indices bit-exact given the Generator's own uniforms.
+* fp64 sum tree: device storage bit-identical to the host SumTree after the
+  same set() calls; device queries identical to host queries.
+* device PER sampler: frequencies vs (1-usp) p^a/sum + usp/N (rtol as the
+  reference's statistical test), weights = (1/N / prob)^beta / max.
+"""
+
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import replay_ref
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), 'golden',
+                                     'replay_golden.json')))
+
+
+def _frame_item(i, rng):
+  s = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  return replay_lib.Transition(s, i % 6, float(i), 0.99, s)
+
+
+def test_circular_logit_buffer_golden(device):
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  g = GOLDEN['circular']['logit_buffer']
+  b = rc.CircularLogitBuffer(g['capacity'], np.random.default_rng(g['seed']))
+  for op in g['ops']:
+    if op[0] == 'add':
+      b.add(op[1])
+    elif op[0] == 'popleft':
+      b.popleft()
+    else:
+      b[np.array(op[1][0])] = np.array(op[1][1], np.float32)
+    np.testing.assert_allclose(b.logits.cpu().numpy(), op[2], rtol=1e-6,
+                               atol=1e-6)
+  assert b._left_head == g['left_head']  # pylint: disable=protected-access
+  assert b.sample(5).tolist() == g['sample']
+  assert b.sample_uniform(4, replace=False).tolist() == g['sample_uniform']
+
+
+def test_mgsc_fifo_replay_golden(device):
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  g = GOLDEN['circular']['mgsc_fifo']
+  r = rc.MGSCFiFoTransitionReplay(g['capacity'], rc.Transition(None, None, None, None, None),
+                                  np.random.default_rng(g['seed']))
+  for i in range(g['n_add']):
+    r.add(rc.Transition(i, 0, 0.0, 1.0, i))
+  assert r.sample(5).s_tm1.tolist() == g['sample_items']
+  ind, tr, lg = r.batch_of_ids_transitions_and_logits(3)
+  assert ind.tolist() == g['meta_indices']
+  assert tr.s_tm1.tolist() == g['meta_items']
+  np.testing.assert_allclose(lg, g['meta_logits'], rtol=1e-6, atol=1e-6)
+  r.update_priorities(ind, np.array([0.5, -0.25, 1.0], np.float32))
+  assert r.sample(4).s_tm1.tolist() == g['sample2_items']
+  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits'], rtol=1e-6,
+                             atol=1e-6)
+
+
+def test_mgsc_reservoir_replay_golden(device):
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  g = GOLDEN['circular']['mgsc_reservoir']
+  r = rc.MGSCReservoirTransitionReplay(g['capacity'], rc.Transition(None, None, None, None, None),
+                                       np.random.default_rng(g['seed']))
+  for i in range(g['n_add']):
+    r.add(rc.Transition(i, 0, 0.0, 1.0, i))
+  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits_after_adds'],
+                             rtol=1e-6, atol=1e-6)
+  items = [int(x.s_tm1[0]) for x in r.get(range(g['capacity']))]
+  assert items == g['slot_items']
+  assert r.sample(5).s_tm1.tolist() == g['sample_items']
+  ind, _, lg = r.batch_of_ids_transitions_and_logits(3)
+  assert ind.tolist() == g['meta_indices']
+  np.testing.assert_allclose(lg, g['meta_logits'], rtol=1e-6, atol=1e-6)
+  r.update_priorities(ind, np.array([1.0, 0.0, -2.0], np.float32))
+  assert r.sample(5).s_tm1.tolist() == g['sample2_items']
+  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits'], rtol=1e-6,
+                             atol=1e-6)
+
+
+def test_softmax_choice_large_capacity(device):
+  """1M logits (the MGSC capacity): oracle numpy choice vs device."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap = 1_000_000
+  rng = np.random.default_rng(0)
+  logits = rng.standard_normal(cap).astype(np.float32)
+  logits[rng.integers(0, cap, 1000)] = -np.inf  # empty slots
+  dev = rc._DeviceLogits(cap)  # pylint: disable=protected-access
+  dev.logits.copy_(torch.from_numpy(logits))
+  u = np.random.default_rng(5).random(512)
+  got = dev.sample_abs(u).cpu().numpy()
+  want = replay_ref.softmax_choice(logits, u)
+  mismatch = np.nonzero(got != want)[0]
+  assert len(mismatch) <= 1, (mismatch, got[mismatch], want[mismatch])
+  # log-mean-exp default logit over the full capacity
+  dev.add_default(write_pos=7, size=cap - 1000, clear_pos=7)
+  lg = logits.copy()
+  lg[7] = -np.inf
+  ref = replay_ref.logits_logmeanexp(lg, cap - 1000)
+  np.testing.assert_allclose(dev.logits[7].item(), ref, rtol=1e-6, atol=1e-6)
+
+
+def _tree_dev(tree):
+  return torch.from_numpy(tree.storage.copy()).to('cuda')
+
+
+def test_sumtree_device_set_and_query(device):
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  lib = _native.lib()
+  rng = np.random.default_rng(3)
+  for size in (1, 3, 37, 1000, 4096 + 17):
+    host = replay_lib.SumTree()
+    host.set_all(np.abs(rng.standard_cauchy(size)))
+    dev = _tree_dev(host)
+    cap = host.capacity
+    for _ in range(5):
+      idx = rng.integers(0, size, 64)
+      vals = np.abs(rng.standard_cauchy(64))
+      vals[::7] = 0.0
+      # the reference sets leaves in order; duplicates keep the last value
+      host.set(idx, vals)
+      last = {}
+      for i, v in zip(idx, vals):
+        last[int(i)] = v
+      di = torch.tensor(list(last.keys()), dtype=torch.int64, device=device)
+      dv = torch.tensor(list(last.values()), dtype=torch.float64, device=device)
+      _native.check(lib.dqz_sumtree_set(_native.ptr(dev), cap, _native.ptr(di),
+                                        _native.ptr(dv), len(last),
+                                        _native.stream_handle()))
+      np.testing.assert_array_equal(dev.cpu().numpy()[1:], host.storage[1:])
+      if host.root() == 0.0:
+        continue
+      targets = rng.uniform(0, host.root(), 257)
+      targets[0] = 0.0
+      dt = torch.from_numpy(targets).to(device)
+      out = torch.empty(257, dtype=torch.int64, device=device)
+      _native.check(lib.dqz_sumtree_query(_native.ptr(dev), cap, _native.ptr(dt),
+                                          257, _native.ptr(out),
+                                          _native.stream_handle()))
+      assert out.cpu().numpy().tolist() == list(host.query(targets))
+  # out of range targets -> -1
+  bad = torch.tensor([-1.0, host.root(), host.root() + 1], dtype=torch.float64,
+                     device=device)
+  out = torch.empty(3, dtype=torch.int64, device=device)
+  _native.check(lib.dqz_sumtree_query(_native.ptr(dev), cap, _native.ptr(bad),
+                                      3, _native.ptr(out), _native.stream_handle()))
+  assert out.cpu().numpy().tolist() == [-1, -1, -1]
+
+
+def test_per_device_sampler_distribution(device):
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  lib = _native.lib()
+  cap, alpha, usp, beta = 8, 0.8, 0.1, 0.4
+  prios = np.array([1.0, 0.0, 3.0, 4.0, 0.5, 2.0, 0.0, 1.5])
+  host = replay_lib.SumTree()
+  host.resize(cap)
+  host.set(np.arange(cap), replay_lib._power(prios, alpha))  # pylint: disable=protected-access
+  dev = _tree_dev(host)
+  counter = torch.zeros(1, dtype=torch.int64, device=device)
+  n = 1000
+  slots = torch.empty(n, dtype=torch.int32, device=device)
+  w = torch.empty(n, dtype=torch.float32, device=device)
+  probs = torch.empty(n, dtype=torch.float64, device=device)
+  counts = np.zeros(cap)
+  for _ in range(60):
+    _native.check(lib.dqz_per_sample(
+        _native.ptr(dev), cap, 0, cap, cap, n, usp, beta, 1, 77,
+        _native.ptr(counter), _native.ptr(slots), _native.ptr(w),
+        _native.ptr(probs), _native.stream_handle()))
+    s = slots.cpu().numpy()
+    counts += np.bincount(s, minlength=cap)
+  p = replay_lib._power(prios, alpha)  # pylint: disable=protected-access
+  expected = (1 - usp) * p / p.sum() + usp / cap
+  np.testing.assert_allclose(counts / counts.sum(), expected, rtol=2e-2,
+                             atol=2e-4)
+  s = slots.cpu().numpy()
+  np.testing.assert_allclose(probs.cpu().numpy(), expected[s], rtol=1e-12)
+  want_w = replay_lib.importance_sampling_weights(expected[s], 1.0 / cap, beta, True)
+  np.testing.assert_allclose(w.cpu().numpy(), want_w, rtol=1e-6)
