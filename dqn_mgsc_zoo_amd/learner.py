@@ -147,6 +147,27 @@ class Learner:
           _native.ptr(out[i:j]), _native.stream_handle(stream)))
     return out
 
+  def _params_tensor(self, params):
+    if params is None:
+      return self.online
+    if isinstance(params, torch.Tensor):
+      return params
+    return torch.from_numpy(self.network.flatten(params)).to(self.device)
+
+  def q_values_host(self, observation, params=None):
+    """Q-values of one host uint8 [84,84,4] state (the actor's select_action)."""
+    obs = np.ascontiguousarray(observation, dtype=np.uint8)
+    if obs.ndim == 3:
+      obs = obs[None]
+    if getattr(self, '_obs_buf', None) is None or self._obs_buf.shape[0] < obs.shape[0]:
+      self._obs_buf = torch.empty((max(obs.shape[0], 1), 84, 84, 4),
+                                  dtype=torch.uint8, device=self.device)
+    buf = self._obs_buf[:obs.shape[0]]
+    buf.copy_(torch.from_numpy(obs))
+    q = self.q_values(buf, self._params_tensor(params))
+    out = q.cpu().numpy()
+    return out[0] if observation.ndim == 3 else out
+
   def q_values_slots(self, store, slots, which, params=None, stream=None):
     params = self.online if params is None else params
     n = int(slots.numel())

@@ -151,7 +151,7 @@ class _HostStorage:
     return type(structure)(*stacked)
 
   def get_state(self):
-    return {'items': dict(self.items)}
+    return {'kind': 'host', 'items': dict(self.items)}
 
   def set_state(self, state):
     self.items = dict(state['items'])
@@ -176,6 +176,8 @@ class _DeviceStorage:
     else:
       nf = capacity * frames_per_slot
     self._torch = torch
+    self._args = {'capacity': capacity, 'mode': mode, 'num_frames': nf,
+                  'frames_per_slot': frames_per_slot}
     self.store = store_lib.FrameStore(capacity, nf, device=device)
     self.allocator = store_lib.FrameAllocator(self.store, mode,
                                               per_slot=frames_per_slot)
@@ -218,7 +220,8 @@ class _DeviceStorage:
 
   def get_state(self):
     st = self.store
-    return {'frames': st.frames.cpu().numpy(), 'fidx': st.fidx.cpu().numpy(),
+    return {'kind': 'device', 'args': dict(self._args),
+            'frames': st.frames.cpu().numpy(), 'fidx': st.fidx.cpu().numpy(),
             'action': st.action.cpu().numpy(),
             'reward': st.reward.cpu().numpy(),
             'discount': st.discount.cpu().numpy(),
@@ -243,17 +246,28 @@ class _StorageMixin:
     self._backend = None
     self._backend_args = (capacity, encoder, decoder, device, num_frames, mode)
 
+  def _make_backend(self, use_device):
+    capacity, encoder, decoder, device, num_frames, mode = self._backend_args
+    if use_device:
+      return _DeviceStorage(capacity, mode, num_frames,
+                            device if isinstance(device, str) else 'cuda',
+                            frames_per_slot=getattr(self, '_frames_per_slot', 5))
+    return _HostStorage(encoder, decoder)
+
   def _storage_for(self, item):
     if self._backend is None:
-      capacity, encoder, decoder, device, num_frames, mode = self._backend_args
-      use_device = device if device is not None else is_frame_transition(item)
-      if use_device:
-        self._backend = _DeviceStorage(capacity, mode, num_frames,
-                                       device if isinstance(device, str)
-                                       else 'cuda')
-      else:
-        self._backend = _HostStorage(encoder, decoder)
+      device = self._backend_args[3]
+      self._backend = self._make_backend(
+          device if device is not None else is_frame_transition(item))
     return self._backend
+
+  def _restore_backend(self, backend_state):
+    """set_state(): re-creates the storage kind the checkpoint was made with."""
+    if backend_state is None:
+      return
+    if self._backend is None:
+      self._backend = self._make_backend(backend_state.get('kind') == 'device')
+    self._backend.set_state(backend_state)
 
   @property
   def on_device(self) -> bool:
@@ -351,11 +365,7 @@ class TransitionReplay(_StorageMixin):
     self._order = collections.OrderedDict((i, None) for i in state['storage'])
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
-    if state.get('backend') is not None:
-      if self._backend is None:
-        raise RuntimeError('set_state on a replay whose storage kind is not '
-                           'yet known: add() one item first or pass device=')
-      self._backend.set_state(state['backend'])
+    self._restore_backend(state.get('backend'))
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._order):
@@ -390,18 +400,6 @@ class ReservoirTransitionReplay(_StorageMixin):
     self._t = 0
     self._frames_per_slot = frames_per_slot
     self._init_storage(capacity, encoder, decoder, device, None, 'slot')
-
-  def _storage_for(self, item):
-    if self._backend is None:
-      capacity, encoder, decoder, device, _, _ = self._backend_args
-      if device if device is not None else is_frame_transition(item):
-        self._backend = _DeviceStorage(
-            capacity, 'slot', None,
-            device if isinstance(device, str) else 'cuda',
-            frames_per_slot=self._frames_per_slot)
-      else:
-        self._backend = _HostStorage(encoder, decoder)
-    return self._backend
 
   def add(self, item) -> None:
     backend = self._storage_for(item)
@@ -450,8 +448,7 @@ class ReservoirTransitionReplay(_StorageMixin):
     self._slots = set(state['storage'])
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
-    if state.get('backend') is not None:
-      self._backend.set_state(state['backend'])
+    self._restore_backend(state.get('backend'))
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._slots):
@@ -876,8 +873,7 @@ class PrioritizedTransitionReplay(_StorageMixin):
     self._order = collections.OrderedDict((i, None) for i in state['storage'])
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
-    if state.get('backend') is not None:
-      self._backend.set_state(state['backend'])
+    self._restore_backend(state.get('backend'))
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._order):

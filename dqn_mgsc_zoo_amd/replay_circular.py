@@ -276,13 +276,15 @@ class _SlotStorage:
     self._device = device
     self._backend = None
 
+  def _make(self, use_device):
+    if use_device:
+      return replay_lib._DeviceStorage(  # pylint: disable=protected-access
+          self._capacity, self._mode, None, self._device)
+    return replay_lib._HostStorage(None, None)  # pylint: disable=protected-access
+
   def put(self, slot, item, oldest_live_slot=None):
     if self._backend is None:
-      if replay_lib.is_frame_transition(item):
-        self._backend = replay_lib._DeviceStorage(  # pylint: disable=protected-access
-            self._capacity, self._mode, None, self._device)
-      else:
-        self._backend = replay_lib._HostStorage(None, None)  # pylint: disable=protected-access
+      self._backend = self._make(replay_lib.is_frame_transition(item))
     self._backend.put(slot, item, oldest_live_slot)
 
   def drop(self, slot):
@@ -308,6 +310,8 @@ class _SlotStorage:
 
   def set_state(self, state):
     if state is not None:
+      if self._backend is None:
+        self._backend = self._make(state.get('kind') == 'device')
       self._backend.set_state(state)
 
 
