@@ -64,6 +64,21 @@ class DqzLearnerConfig(ctypes.Structure):
   ]
 
 
+class DqzMetaConfig(ctypes.Structure):
+  _fields_ = [
+      ('meta_batch', ctypes.c_int),
+      ('num_actions', ctypes.c_int),
+      ('learning_rate', ctypes.c_float),
+      ('decay', ctypes.c_float),
+      ('eps', ctypes.c_float),
+      ('grad_error_bound', ctypes.c_float),
+      ('meta_learning_rate', ctypes.c_float),
+      ('b1', ctypes.c_float),
+      ('b2', ctypes.c_float),
+      ('meta_eps', ctypes.c_float),
+  ]
+
+
 # name -> (restype, argtypes); must match include/dqz.h exactly.
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -82,6 +97,11 @@ SIGNATURES = {
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
          _vp],
+    ),
+    'dqz_learner_grad': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
+         _vp, _vp],
     ),
     'dqz_learner_outputs': (_int, [_vp, _vp, _vp, _vp, _vp]),
     'dqz_learner_profile': (
@@ -108,6 +128,14 @@ SIGNATURES = {
         _int,
         [_vp, _i64, _i64, _i64, _i64, _int, ctypes.c_double, ctypes.c_double,
          _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
+    'dqz_meta_create': (
+        _int, [ctypes.POINTER(DqzMetaConfig), ctypes.POINTER(_vp)]),
+    'dqz_meta_destroy': (_int, [_vp]),
+    'dqz_meta_update': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp,
+         ctypes.POINTER(DqzStore), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'dqz_meta_outputs': (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

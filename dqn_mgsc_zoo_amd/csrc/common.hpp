@@ -70,9 +70,16 @@ struct NetZ {
 // optax 0.1.2 scale_by_stddev + scale(-lr) (dqn/run_atari.py:208-213):
 //   mu = (1-decay) g + decay mu ; nu = (1-decay) g^2 + decay nu
 //   theta += -lr * g * rsqrt(nu - mu^2 + eps)
+// Centered RMSProp on one parameter, or — when `gout` is set (gradient-output
+// mode, used by the MGSC meta-update) — store the gradient at gout[i] instead.
 struct Rms {
   float lr, decay, c1, eps;
+  float* gout;
   __device__ __forceinline__ void apply(float* th, float* mu, float* nu, int64_t i, float g) const {
+    if (gout) {
+      gout[i] = g;
+      return;
+    }
     const float m = c1 * g + decay * mu[i];
     const float v = c1 * (g * g) + decay * nu[i];
     mu[i] = m;

@@ -78,6 +78,7 @@ struct Conv1FwdArgs {
   NetZ nz;
   int64_t w_off, b_off;
   int B;
+  int linear;  // 1: write the pre-activation (no ReLU)
   float* out;  // y1 [Z][B][400][32]
 };
 
@@ -114,7 +115,10 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int pos = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (pos < C1_POS) out[pos * C1CO + i] = relu(acc[r] + bias);
+    if (pos < C1_POS) {
+      const float v = acc[r] + bias;
+      out[pos * C1CO + i] = a.linear ? v : relu(v);
+    }
   }
 }
 

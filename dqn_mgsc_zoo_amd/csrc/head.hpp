@@ -17,6 +17,7 @@ struct HeadArgs {
   const float* reward;
   const float* discount;
   const float* weights;  // PER importance weights or null
+  const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
   float bound;           // grad_error_bound
   float* q;              // [Z][B][A]
   float* td;             // [B]
@@ -43,13 +44,14 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   const int A = h.A, B = h.B;
   // Issue the per-sample batch loads early (their latency overlaps the fc1 sums).
   int a_tm1 = 0;
-  float r = 0.f, d = 0.f, w = 1.f;
+  float r = 0.f, d = 0.f, w = 1.f, pm = 0.f;
   if (!h.fwd_only && n == 0) {
     const int slot = h.slots[b];
     a_tm1 = h.action[slot];
     r = h.reward[slot];
     d = h.discount[slot];
     if (h.weights) w = h.weights[b];
+    if (h.meta_p) pm = h.meta_p[b];
   }
   float h0 = 0.f;
   for (int z = 0; z < h.Z; ++z) {
@@ -95,8 +97,15 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
       v = s_q[1][am];
     }
     const float td = (r + d * v) - s_q[0][a_tm1];
-    float g = w * td / (float)B;  // d mean(l2(td) * w) / d td
-    g = fminf(fmaxf(g, -h.bound), h.bound);
+    float g;
+    if (h.meta_p) {
+      // meta mode: p_b * grad of loss_fn on the single transition b
+      // (dqn_mgsc_batched/agent.py:152-158): batch of one, clip, then weight.
+      g = pm * fminf(fmaxf(td, -h.bound), h.bound);
+    } else {
+      g = w * td / (float)B;  // d mean(l2(td) * w) / d td
+      g = fminf(fmaxf(g, -h.bound), h.bound);
+    }
     h.td[b] = td;
     h.loss_part[b] = 0.5f * td * td * w;
     h.gq[b] = -g;

@@ -19,6 +19,7 @@
 #include "conv1.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
+#include "meta.hpp"
 #include "sampling.hpp"
 
 namespace dqz {
@@ -54,6 +55,7 @@ struct ConvFwd : Shape {
   static constexpr bool kAFastK = true, kBFastK = false;
   const float* in;  // [Z][B][IH][IH][CI]
   int B;
+  int linear;  // 1: pre-activation output (no ReLU)
   NetZ nz;
   int64_t w_off, b_off;
   float* out;  // [Z][B*OH*OH][CO]
@@ -65,7 +67,8 @@ struct ConvFwd : Shape {
   __device__ float4 a4(const TileCoord& tc, int m, int k) const { return ld4(a_ptr(tc, m, k)); }
   __device__ float4 b4(const TileCoord& tc, int k, int n) const { return ld4(nz.p[tc.z] + w_off + k * CO + n); }
   __device__ void store(const TileCoord& tc, int m, int n, float v) const {
-    out[((int64_t)tc.z * M + m) * CO + n] = relu(v + nz.p[tc.z][b_off + n]);
+    const float y = v + nz.p[tc.z][b_off + n];
+    out[((int64_t)tc.z * M + m) * CO + n] = linear ? y : relu(y);
   }
 };
 using Conv2Fwd = ConvFwd<C1O, C1CO, C2K, C2S, C2CO, C2O>;
@@ -334,6 +337,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.w_off = L->off[0];
   c1.b_off = L->off[1];
   c1.B = B;
+  c1.linear = 0;
   c1.out = L->y1;
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(C1_BLOCKS, B, Z), dim3(256), kConv1FwdSmem, st, c1);
   DQZ_HIP(hipGetLastError());
@@ -343,6 +347,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   static_cast<Shape&>(c2) = make_shape<CfgConv>(Z, B * C2M, C2CO, C2KK, 1);
   c2.in = L->y1;
   c2.B = B;
+  c2.linear = 0;
   c2.nz = nz;
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
@@ -354,6 +359,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   static_cast<Shape&>(c3) = make_shape<CfgConv>(Z, B * C3M, C3CO, C3KK, 1);
   c3.in = L->y2;
   c3.B = B;
+  c3.linear = 0;
   c3.nz = nz;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
@@ -391,10 +397,15 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
   return h;
 }
 
+// One learner step.  gout == null: centered RMSProp on P->online/mu/nu.
+// gout != null: gradient-output mode — the full gradient is written to gout
+// (dqz parameter layout) and P->online/mu/nu are left untouched.
+// meta_p != null: per-sample cotangents p_b * (-clip(td_b)) (MGSC meta mode).
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
-                     const float* is_weights, void* stream, PhaseEvents pe) {
-  if (!L || !P || !P->online || !P->target || !P->mu || !P->nu || !slots)
-    return fail(DQZ_ERR_INVALID, "null argument");
+                     const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
+                     const float* meta_p = nullptr) {
+  if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
+  if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
   if (L->cfg.algo == DQZ_ALGO_PER && !is_weights) return fail(DQZ_ERR_INVALID, "PER step needs is_weights");
   hipStream_t st = (hipStream_t)stream;
@@ -414,6 +425,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   rms.decay = L->cfg.decay;
   rms.c1 = (float)(1.0 - (double)L->cfg.decay);
   rms.eps = L->cfg.eps;
+  rms.gout = gout;
 
   HeadArgs h = make_head(L, nz, Z, B);
   h.fwd_only = 0;
@@ -422,6 +434,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.reward = S->reward;
   h.discount = S->discount;
   h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
+  h.meta_p = meta_p;
   h.bound = L->cfg.grad_error_bound;
   h.td = L->td;
   h.loss_part = L->loss_part;
@@ -521,6 +534,12 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
 int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream) {
   return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr});
+}
+
+int dqz_learner_grad(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                     const float* is_weights, float* grad_out, void* stream) {
+  if (!grad_out) return fail(DQZ_ERR_INVALID, "null grad_out");
+  return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr}, grad_out);
 }
 
 int dqz_learner_profile(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
@@ -747,6 +766,227 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
 int dqz_target_copy(float* target, const float* online, int64_t total, void* stream) {
   if (!target || !online || total < 0) return fail(DQZ_ERR_INVALID, "bad argument");
   DQZ_HIP(hipMemcpyAsync(target, online, total * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return DQZ_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// MGSC meta-update (meta.hpp)
+
+struct dqz_meta {
+  dqz_meta_config cfg;
+  dqz_learner* lm;   // meta batch learner (B = M)
+  dqz_learner* l1;   // one-transition learner (B = 1)
+  int64_t total;
+  float *G, *thp, *mu1, *nu1, *J;  // [total] each; G also holds g', thp also holds v
+  float *zv1, *zv2, *zv3, *zvp;    // tangent forward outputs
+  float *x, *p, *s, *dl, *loss, *loss_part;
+  int nparts;
+  void* block;
+};
+
+extern "C" {
+
+int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
+  if (!cfg || !out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (cfg->meta_batch < 1 || cfg->meta_batch > MAXB)
+    return fail(DQZ_ERR_UNSUPPORTED, "meta_batch must be in [1, %d]", MAXB);
+  dqz_learner_config lc;
+  lc.batch = cfg->meta_batch;
+  lc.num_actions = cfg->num_actions;
+  lc.algo = DQZ_ALGO_DQN;
+  lc.learning_rate = cfg->learning_rate;
+  lc.decay = cfg->decay;
+  lc.eps = cfg->eps;
+  lc.grad_error_bound = cfg->grad_error_bound;
+  dqz_meta* H = new dqz_meta();
+  H->cfg = *cfg;
+  if (int rc = dqz_learner_create(&lc, &H->lm)) {
+    delete H;
+    return rc;
+  }
+  lc.batch = 1;
+  if (int rc = dqz_learner_create(&lc, &H->l1)) {
+    dqz_learner_destroy(H->lm);
+    delete H;
+    return rc;
+  }
+  const int M = cfg->meta_batch;
+  H->total = H->lm->total;
+  H->nparts = (int)((H->total / 4 + 255) / 256);
+  const int64_t sizes[] = {H->total, H->total, H->total, H->total, H->total,
+                           (int64_t)M * C1M * C1CO, (int64_t)M * C2M * C2CO, (int64_t)M * FLAT,
+                           (int64_t)H->lm->S_fc1 * M * HID,
+                           M, M, M, M, 1, H->nparts};
+  float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
+                    &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part};
+  int64_t tot = 0;
+  for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
+  if (hipMalloc(&H->block, tot * sizeof(float)) != hipSuccess || hipMemset(H->block, 0, tot * sizeof(float)) != hipSuccess) {
+    if (H->block) (void)hipFree(H->block);
+    dqz_learner_destroy(H->lm);
+    dqz_learner_destroy(H->l1);
+    delete H;
+    return fail(DQZ_ERR_HIP, "hipMalloc of %lld bytes of meta scratch failed", (long long)(tot * 4));
+  }
+  float* q = (float*)H->block;
+  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
+    *ptrs[i] = q;
+    q += (sizes[i] + 63) / 64 * 64;
+  }
+  *out = H;
+  return DQZ_OK;
+}
+
+int dqz_meta_destroy(dqz_meta* H) {
+  if (!H) return DQZ_OK;
+  dqz_learner_destroy(H->lm);
+  dqz_learner_destroy(H->l1);
+  if (H->block) (void)hipFree(H->block);
+  delete H;
+  return DQZ_OK;
+}
+
+int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                    const dqz_store* S1, const int32_t* online_slot, float* logits, const int32_t* pos,
+                    float* adam_mu, float* adam_nu, int32_t* adam_count, void* stream) {
+  if (!H || !P || !P->online || !P->target || !P->mu || !P->nu || !slots || !online_slot || !logits || !pos ||
+      !adam_mu || !adam_nu || !adam_count)
+    return fail(DQZ_ERR_INVALID, "null argument");
+  if (int rc = check_store(S)) return rc;
+  if (int rc = check_store(S1)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  dqz_learner* L = H->lm;
+  const int M = H->cfg.meta_batch, A = H->cfg.num_actions;
+
+  // p = softmax(logits[pos])
+  hipLaunchKernelGGL(meta_softmax_kernel, dim3(1), dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p);
+  DQZ_HIP(hipGetLastError());
+
+  // G = sum_i p_i g_i: one batched backward with p-weighted cotangents.
+  if (int rc = step_impl(L, P, S, slots, nullptr, stream, PhaseEvents{nullptr}, H->G, H->p)) return rc;
+
+  MetaRmsArgs ra;
+  ra.lr = H->cfg.learning_rate;
+  ra.decay = H->cfg.decay;
+  ra.c1 = (float)(1.0 - (double)H->cfg.decay);
+  ra.eps = H->cfg.eps;
+  ra.n4 = H->total / 4;
+  const dim3 eg((unsigned)((ra.n4 + 255) / 256));
+  hipLaunchKernelGGL(meta_rms1_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)P->online,
+                     (const float4*)P->mu, (const float4*)P->nu, (float4*)H->thp, (float4*)H->mu1,
+                     (float4*)H->nu1, (float4*)H->J);
+  DQZ_HIP(hipGetLastError());
+
+  // g' = grad loss_fn(theta', target = theta, online transition) -> G buffer.
+  dqz_params P1;
+  P1.online = H->thp;
+  P1.target = P->online;
+  P1.mu = nullptr;
+  P1.nu = nullptr;
+  if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, PhaseEvents{nullptr}, H->G)) return rc;
+
+  // v = -2 u' du/dG -> thp buffer; partial sums of u'^2.
+  hipLaunchKernelGGL(meta_rms2_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)H->mu1,
+                     (const float4*)H->nu1, (const float4*)H->J, (float4*)H->thp, H->loss_part);
+  DQZ_HIP(hipGetLastError());
+  const float* v = H->thp;
+
+  // Tangent forward over the stored online activations: V * y + vb per layer.
+  NetZ nv;
+  nv.p[0] = nv.p[1] = nv.p[2] = v;
+  nv.which[0] = nv.which[1] = nv.which[2] = 0;
+  Conv1FwdArgs c1;
+  c1.src = Conv1Src{S->frames, S->fidx, slots, nullptr};
+  c1.nz = nv;
+  c1.w_off = L->off[0];
+  c1.b_off = L->off[1];
+  c1.B = M;
+  c1.linear = 1;
+  c1.out = H->zv1;
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(C1_BLOCKS, M, 1), dim3(256), kConv1FwdSmem, st, c1);
+  DQZ_HIP(hipGetLastError());
+  Conv2Fwd c2;
+  static_cast<Shape&>(c2) = make_shape<CfgConv>(1, M * C2M, C2CO, C2KK, 1);
+  c2.in = L->y1;
+  c2.B = M;
+  c2.linear = 1;
+  c2.nz = nv;
+  c2.w_off = L->off[2];
+  c2.b_off = L->off[3];
+  c2.out = H->zv2;
+  Conv3Fwd c3;
+  static_cast<Shape&>(c3) = make_shape<CfgConv>(1, M * C3M, C3CO, C3KK, 1);
+  c3.in = L->y2;
+  c3.B = M;
+  c3.linear = 1;
+  c3.nz = nv;
+  c3.w_off = L->off[4];
+  c3.b_off = L->off[5];
+  c3.out = H->zv3;
+  Fc1Fwd f1;
+  static_cast<Shape&>(f1) = make_shape<CfgFc1>(1, M, HID, FLAT, L->S_fc1);
+  f1.in = L->y3;
+  f1.nz = nv;
+  f1.w_off = L->off[6];
+  f1.part = H->zvp;
+  DQZ_HIP((launch_gemm<CfgConv>(st, c2, c3, f1)));
+
+  MetaDotArgs md;
+  md.dy1 = L->dy1;
+  md.dy2 = L->dy2;
+  md.dy3 = L->dy3;
+  md.dz1 = L->dz1;
+  md.gq = L->gq;
+  md.ga = L->ga;
+  md.zv1 = H->zv1;
+  md.zv2 = H->zv2;
+  md.zv3 = H->zv3;
+  md.zvp = H->zvp;
+  md.S = f1.g.S;
+  md.M = M;
+  md.A = A;
+  md.v = v;
+  md.b1_off = L->off[7];
+  md.w2_off = L->off[8];
+  md.b2_off = L->off[9];
+  md.h1 = L->h1;
+  md.s_out = H->s;
+  hipLaunchKernelGGL(meta_dot_kernel, dim3(M), dim3(512), 0, st, md);
+  DQZ_HIP(hipGetLastError());
+
+  MetaAdamArgs ad;
+  ad.x = H->x;
+  ad.p = H->p;
+  ad.s = H->s;
+  ad.M = M;
+  ad.logits = logits;
+  ad.pos = pos;
+  ad.m = adam_mu;
+  ad.v = adam_nu;
+  ad.count = adam_count;
+  ad.lr = H->cfg.meta_learning_rate;
+  ad.b1 = H->cfg.b1;
+  ad.b2 = H->cfg.b2;
+  ad.eps = H->cfg.meta_eps;
+  ad.loss_part = H->loss_part;
+  ad.nparts = H->nparts;
+  ad.loss = H->loss;
+  ad.dlogits = H->dl;
+  hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_meta_outputs(dqz_meta* H, float* probs, float* dlogits, float* td, float* loss, void* stream) {
+  if (!H) return fail(DQZ_ERR_INVALID, "null meta handle");
+  hipStream_t st = (hipStream_t)stream;
+  const int M = H->cfg.meta_batch;
+  if (probs) DQZ_HIP(hipMemcpyAsync(probs, H->p, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
+  if (dlogits) DQZ_HIP(hipMemcpyAsync(dlogits, H->dl, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
+  if (td) DQZ_HIP(hipMemcpyAsync(td, H->lm->td, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
+  if (loss) DQZ_HIP(hipMemcpyAsync(loss, H->loss, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }
 

@@ -1,0 +1,242 @@
+// meta.hpp — MGSC meta-update kernels (dqn_mgsc_batched/agent.py:104-220).
+//
+// The reference differentiates meta_loss_fn w.r.t. the M meta-batch logits
+// with per-transition gradients materialised by vmap (M x 6.75 MB).  Here
+// nothing per-example is stored:
+//   G  = sum_i p_i g_i is ONE batched backward whose per-sample cotangent at
+//        q_i[a_i] is -p_i clip(td_i)   (head meta mode + gradient-output mode);
+//   v  = dL/dG = -2 u' * du/dG          (elementwise, meta_rms1/2_kernel);
+//   p_i dL/dp_i = p_i v.g_i = sum_layers <dz_i^(p), V * y_i + vb>, where
+//        dz^(p) are the p-weighted pre-activation gradients the batched
+//        backward already produced (they are linear in the cotangent) and
+//        V * y is a forward of the stored activations with the tangent v as
+//        weights (meta_dot_kernel);
+//   dL/dx_j = p_j dL/dp_j - p_j sum_i p_i dL/dp_i (softmax backward), then
+//        optax.adam on the logits (meta_adam_kernel).
+#pragma once
+#include "common.hpp"
+
+namespace dqz {
+
+constexpr int META_THREADS = 256;
+
+__device__ __forceinline__ float block_sum_f32(float v, float* sbuf) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) sbuf[wave] = v;
+  __syncthreads();
+  float r = sbuf[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r += sbuf[w];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ float block_max_f32(float v, float* sbuf) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if (lane == 0) sbuf[wave] = v;
+  __syncthreads();
+  float r = sbuf[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, sbuf[w]);
+  __syncthreads();
+  return r;
+}
+
+// p = exp(x - (c + log(sum exp(x - c)))), c = max x  (JNPprobabilities_from_logits,
+// replay_circular.py:79-86).  One block; x gathered from logits[pos].
+__global__ __launch_bounds__(META_THREADS) void meta_softmax_kernel(const float* __restrict__ logits,
+                                                                    const int32_t* __restrict__ pos, int M,
+                                                                    float* __restrict__ x_out,
+                                                                    float* __restrict__ p_out) {
+  __shared__ float sbuf[META_THREADS / 64];
+  const int i = threadIdx.x;
+  const float x = i < M ? logits[pos[i]] : -INFINITY;
+  const float c = block_max_f32(x, sbuf);
+  const float s = block_sum_f32(i < M ? expf(x - c) : 0.f, sbuf);
+  const float lse = c + logf(s);
+  if (i < M) {
+    x_out[i] = x;
+    p_out[i] = expf(x - lse);
+  }
+}
+
+struct MetaRmsArgs {
+  float lr, decay, c1, eps;
+  int64_t n4;  // total / 4 (float4 granules)
+};
+
+// theta' = theta + u(G; mu, nu); keeps mu', nu' and J = du/dG
+//   = -lr D^{-3/2} (D - c1 G (G - mu')),  D = nu' - mu'^2 + eps.
+__global__ __launch_bounds__(256) void meta_rms1_kernel(MetaRmsArgs a, const float4* __restrict__ G,
+                                                        const float4* __restrict__ th,
+                                                        const float4* __restrict__ mu,
+                                                        const float4* __restrict__ nu, float4* __restrict__ thp,
+                                                        float4* __restrict__ mu1, float4* __restrict__ nu1,
+                                                        float4* __restrict__ J) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n4) return;
+  const float4 g4 = G[i], t4 = th[i], m4 = mu[i], v4 = nu[i];
+  float4 o_t, o_m, o_v, o_j;
+  auto one = [&](float g, float t, float m0, float v0, float& ot, float& om, float& ov, float& oj) {
+    const float m = a.c1 * g + a.decay * m0;
+    const float v = a.c1 * (g * g) + a.decay * v0;
+    const float d = v - m * m + a.eps;
+    const float rs = rsqrtf(d);
+    ot = t + (-a.lr) * (g * rs);
+    om = m;
+    ov = v;
+    oj = -a.lr * (d - a.c1 * g * (g - m)) * (rs * rs * rs);
+  };
+  one(g4.x, t4.x, m4.x, v4.x, o_t.x, o_m.x, o_v.x, o_j.x);
+  one(g4.y, t4.y, m4.y, v4.y, o_t.y, o_m.y, o_v.y, o_j.y);
+  one(g4.z, t4.z, m4.z, v4.z, o_t.z, o_m.z, o_v.z, o_j.z);
+  one(g4.w, t4.w, m4.w, v4.w, o_t.w, o_m.w, o_v.w, o_j.w);
+  thp[i] = o_t;
+  mu1[i] = o_m;
+  nu1[i] = o_v;
+  J[i] = o_j;
+}
+
+// u' = u(g'; mu', nu') (theta'' - theta'), v = dL/dG = -2 u' J, and per-block
+// partial sums of u'^2 (the meta loss).
+__global__ __launch_bounds__(256) void meta_rms2_kernel(MetaRmsArgs a, const float4* __restrict__ g2,
+                                                        const float4* __restrict__ mu1,
+                                                        const float4* __restrict__ nu1,
+                                                        const float4* __restrict__ J, float4* __restrict__ v_out,
+                                                        float* __restrict__ loss_part) {
+  __shared__ float sbuf[4];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float sq = 0.f;
+  if (i < a.n4) {
+    const float4 g4 = g2[i], m4 = mu1[i], n4 = nu1[i], j4 = J[i];
+    float4 o;
+    auto one = [&](float g, float m0, float v0, float j, float& ov) {
+      const float m = a.c1 * g + a.decay * m0;
+      const float v = a.c1 * (g * g) + a.decay * v0;
+      const float u = (-a.lr) * (g * rsqrtf(v - m * m + a.eps));
+      ov = -2.f * u * j;
+      sq += u * u;
+    };
+    one(g4.x, m4.x, n4.x, j4.x, o.x);
+    one(g4.y, m4.y, n4.y, j4.y, o.y);
+    one(g4.z, m4.z, n4.z, j4.z, o.z);
+    one(g4.w, m4.w, n4.w, j4.w, o.w);
+    v_out[i] = o;
+  }
+  sq = block_sum_f32(sq, sbuf);
+  if (threadIdx.x == 0) loss_part[blockIdx.x] = sq;
+}
+
+struct MetaDotArgs {
+  const float* dy1;  // [M][400][32] p-weighted conv1 pre-activation grads
+  const float* dy2;  // [M][81][64]
+  const float* dy3;  // [M][3136]
+  const float* dz1;  // [M][512]
+  const float* gq;   // [M] cotangent at q[a] (= -p clip(td))
+  const int32_t* ga; // [M] a_tm1
+  const float* zv1;  // [M][400][32] V1 * x + vb1
+  const float* zv2;  // [M][81][64]
+  const float* zv3;  // [M][3136]
+  const float* zvp;  // fc1 split-K partials of V_fc1 y3 [S][M][512]
+  int S, M, A;
+  const float* v;    // tangent (param layout)
+  int64_t b1_off, w2_off, b2_off;
+  const float* h1;   // [M][512] online fc1 output (z = 0)
+  float* s_out;      // [M]  p_i dL/dp_i
+};
+
+// One block (512 threads) per meta-batch sample.
+__global__ __launch_bounds__(512) void meta_dot_kernel(MetaDotArgs a) {
+  __shared__ float sbuf[8];
+  __shared__ float s_fc2[8];
+  const int b = blockIdx.x, t = threadIdx.x;
+  float acc = 0.f;
+  {
+    const float4* d = reinterpret_cast<const float4*>(a.dy1 + (int64_t)b * C1M * C1CO);
+    const float4* z = reinterpret_cast<const float4*>(a.zv1 + (int64_t)b * C1M * C1CO);
+    for (int i = t; i < C1M * C1CO / 4; i += 512) {
+      const float4 x = d[i], y = z[i];
+      acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+  }
+  {
+    const float4* d = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * C2M * C2CO);
+    const float4* z = reinterpret_cast<const float4*>(a.zv2 + (int64_t)b * C2M * C2CO);
+    for (int i = t; i < C2M * C2CO / 4; i += 512) {
+      const float4 x = d[i], y = z[i];
+      acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+  }
+  {
+    const float4* d = reinterpret_cast<const float4*>(a.dy3 + (int64_t)b * FLAT);
+    const float4* z = reinterpret_cast<const float4*>(a.zv3 + (int64_t)b * FLAT);
+    for (int i = t; i < FLAT / 4; i += 512) {
+      const float4 x = d[i], y = z[i];
+      acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+  }
+  // fc1: dz1 . (vb1 + sum_s partial)
+  float zf = a.v[a.b1_off + t];
+  for (int s = 0; s < a.S; ++s) zf += a.zvp[((int64_t)s * a.M + b) * HID + t];
+  acc += a.dz1[(int64_t)b * HID + t] * zf;
+  // fc2: gq . (h1 . V2[:, a] + vb2[a])
+  const int act = a.ga[b];
+  float f2 = wave_sum(a.h1[(int64_t)b * HID + t] * a.v[a.w2_off + t * a.A + act]);
+  if ((t & 63) == 0) s_fc2[t >> 6] = f2;
+  __syncthreads();
+  if (t == 0) {
+    float z2 = a.v[a.b2_off + act];
+    for (int w = 0; w < 8; ++w) z2 += s_fc2[w];
+    acc += a.gq[b] * z2;
+  }
+  acc = block_sum_f32(acc, sbuf);
+  if (t == 0) a.s_out[b] = acc;
+}
+
+struct MetaAdamArgs {
+  const float* x;   // [M] gathered logits
+  const float* p;   // [M]
+  const float* s;   // [M] p_i dL/dp_i
+  int M;
+  float* logits;
+  const int32_t* pos;
+  float *m, *v;
+  int32_t* count;
+  float lr, b1, b2, eps;
+  const float* loss_part;
+  int nparts;
+  float* loss;
+  float* dlogits;   // [M]
+};
+
+// softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
+// new logits scattered back.  One block.
+__global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) {
+  __shared__ float sbuf[META_THREADS / 64];
+  const int i = threadIdx.x;
+  const float si = i < a.M ? a.s[i] : 0.f;
+  const float tot = block_sum_f32(si, sbuf);
+  float lp = 0.f;
+  for (int j = i; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+  lp = block_sum_f32(lp, sbuf);
+  const int32_t cnt = *a.count + 1;
+  __syncthreads();
+  if (i < a.M) {
+    const float g = si - a.p[i] * tot;
+    const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
+    const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
+    const float mh = m / (1.f - powf(a.b1, (float)cnt));
+    const float vh = v / (1.f - powf(a.b2, (float)cnt));
+    a.m[i] = m;
+    a.v[i] = v;
+    a.dlogits[i] = g;
+    a.logits[a.pos[i]] = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+  }
+  if (i == 0) {
+    *a.count = cnt;
+    *a.loss = lp;
+  }
+}
+
+}  // namespace dqz

@@ -52,6 +52,7 @@ class Learner:
     self.algo = algo
     self.batch_size = int(batch_size)
     self.optimizer = optimizer
+    self.grad_error_bound = float(grad_error_bound)
     self.device = torch.device(device)
     self.offsets, self.sizes, self.total = network.layout()
     self.online = torch.zeros((self.total,), dtype=torch.float32, device=self.device)
@@ -116,6 +117,17 @@ class Learner:
     _native.check(_native.lib().dqz_learner_step(
         self._h, ctypes.byref(self._params_c), store.c_ref(),
         _native.ptr(slots), _native.ptr(weights), _native.stream_handle(stream)))
+
+  def grad(self, store, slots, weights=None, out=None, stream=None):
+    """jax.grad(loss_fn) of the same step into a flat tensor (no update)."""
+    if slots.dtype != torch.int32 or slots.numel() != self.batch_size:
+      raise ValueError('slots must be a device int32 tensor of batch size')
+    out = torch.zeros_like(self.online) if out is None else out
+    _native.check(_native.lib().dqz_learner_grad(
+        self._h, ctypes.byref(self._params_c), store.c_ref(),
+        _native.ptr(slots), _native.ptr(weights), _native.ptr(out),
+        _native.stream_handle(stream)))
+    return out
 
   def profile(self, store, slots, weights=None, iters=20, stream=None):
     """Average ms per phase (HIP events on the launch stream), dict."""
@@ -185,3 +197,119 @@ def sample_uniform(base, size, capacity, n, seed, counter, out, stream=None):
       int(base), int(size), int(capacity), int(n), int(seed) & (2**64 - 1),
       _native.ptr(counter), _native.ptr(out), _native.stream_handle(stream)))
   return out
+
+
+class AdamConfig:
+  """optax.adam(learning_rate, b1, b2, eps) stand-in (eps_root = 0)."""
+
+  def __init__(self, learning_rate, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0):
+    if eps_root != 0.0:
+      raise NotImplementedError('eps_root is not used by the reference')
+    self.learning_rate = float(learning_rate)
+    self.b1 = float(b1)
+    self.b2 = float(b2)
+    self.eps = float(eps)
+
+
+def adam(learning_rate, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0):
+  return AdamConfig(learning_rate, b1, b2, eps, eps_root)
+
+
+class MetaLearner:
+  """MGSC meta-update on device (dqn_mgsc_batched/agent.py:104-220, 302-334).
+
+  Holds the meta optimizer state (optax ScaleByAdamState(count, mu, nu) over
+  the M meta-batch logits, shared across calls exactly as the reference's
+  `self._meta_opt_state`) and a one-slot frame store for the newest
+  transition.  `update` reads the learner's online/target params and RMSProp
+  state, never modifies them, and writes the Adam-updated logits back into
+  the replay's device logit buffer at the meta batch's positions
+  (replay.update_priorities(indices, new_meta_params)).
+  """
+
+  def __init__(self, learner: Learner, meta_batch_size, meta_optimizer=None):
+    from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
+    if learner.algo != 'dqn':
+      raise ValueError('the MGSC agents use q_learning on dqn_atari_network')
+    meta_optimizer = meta_optimizer or adam(2.5e-4)
+    self.learner = learner
+    self.meta_batch_size = int(meta_batch_size)
+    self.meta_optimizer = meta_optimizer
+    dev = learner.device
+    m = self.meta_batch_size
+    self.adam_mu = torch.zeros((m,), dtype=torch.float32, device=dev)
+    self.adam_nu = torch.zeros((m,), dtype=torch.float32, device=dev)
+    self.adam_count = torch.zeros((1,), dtype=torch.int32, device=dev)
+    self.probs = torch.zeros((m,), dtype=torch.float32, device=dev)
+    self.dlogits = torch.zeros((m,), dtype=torch.float32, device=dev)
+    self.td = torch.zeros((m,), dtype=torch.float32, device=dev)
+    self.loss = torch.zeros((1,), dtype=torch.float32, device=dev)
+    self.online_store = store_lib.FrameStore(1, 8, device=dev)
+    self.online_store.fidx[0].copy_(torch.arange(8, dtype=torch.int32))
+    self.online_slot = torch.zeros((1,), dtype=torch.int32, device=dev)
+    opt = learner.optimizer
+    cfg = _native.DqzMetaConfig(
+        m, learner.network.num_actions, opt.learning_rate, opt.decay, opt.eps,
+        learner.grad_error_bound, meta_optimizer.learning_rate,
+        meta_optimizer.b1, meta_optimizer.b2, meta_optimizer.eps)
+    handle = ctypes.c_void_p()
+    _native.check(_native.lib().dqz_meta_create(ctypes.byref(cfg),
+                                                ctypes.byref(handle)))
+    self._h = handle
+
+  def __del__(self):
+    h = getattr(self, '_h', None)
+    if h is not None and h.value and _native._lib is not None:  # pylint: disable=protected-access
+      _native.lib().dqz_meta_destroy(h)
+      self._h = None
+
+  def set_online_transition(self, transition):
+    """Uploads the newest host transition (uint8 [84,84,4] stacks)."""
+    s_tm1 = np.asarray(transition.s_tm1, np.uint8)
+    s_t = np.asarray(transition.s_t, np.uint8)
+    frames = np.concatenate([np.moveaxis(s_tm1, -1, 0),
+                             np.moveaxis(s_t, -1, 0)]).reshape(8, -1)
+    st = self.online_store
+    st.frames.copy_(torch.from_numpy(np.ascontiguousarray(frames)))
+    meta = torch.tensor([float(transition.r_t), float(transition.discount_t)],
+                        dtype=torch.float32)
+    st.action[0] = int(transition.a_tm1)
+    st.reward.copy_(meta[:1])
+    st.discount.copy_(meta[1:])
+
+  def update(self, store, slots, logits, positions, stream=None):
+    """One meta_update on replay `slots` (device int32 [M]); logits updated
+    in place at `positions` (device int32 [M], distinct)."""
+    m = self.meta_batch_size
+    if slots.dtype != torch.int32 or slots.numel() != m:
+      raise ValueError('slots must be a device int32 tensor of meta batch size')
+    if positions.dtype != torch.int32 or positions.numel() != m:
+      raise ValueError('positions must be a device int32 tensor [M]')
+    if logits.dtype != torch.float32:
+      raise ValueError('logits must be float32')
+    lrn = self.learner
+    _native.check(_native.lib().dqz_meta_update(
+        self._h, ctypes.byref(lrn._params_c), store.c_ref(),  # pylint: disable=protected-access
+        _native.ptr(slots), self.online_store.c_ref(),
+        _native.ptr(self.online_slot), _native.ptr(logits),
+        _native.ptr(positions), _native.ptr(self.adam_mu),
+        _native.ptr(self.adam_nu), _native.ptr(self.adam_count),
+        _native.stream_handle(stream)))
+
+  def fetch_outputs(self, stream=None):
+    """(probs [M], dL/dlogits [M], meta-batch td [M], meta loss [1])."""
+    _native.check(_native.lib().dqz_meta_outputs(
+        self._h, _native.ptr(self.probs), _native.ptr(self.dlogits),
+        _native.ptr(self.td), _native.ptr(self.loss),
+        _native.stream_handle(stream)))
+    return self.probs, self.dlogits, self.td, self.loss
+
+  def get_state(self):
+    """optax ScaleByAdamState(count, mu, nu) as host arrays."""
+    return {'count': int(self.adam_count.item()),
+            'mu': self.adam_mu.cpu().numpy(), 'nu': self.adam_nu.cpu().numpy()}
+
+  def set_state(self, state):
+    self.adam_count.fill_(int(state['count']))
+    self.adam_mu.copy_(torch.as_tensor(np.asarray(state['mu'], np.float32)))
+    self.adam_nu.copy_(torch.as_tensor(np.asarray(state['nu'], np.float32)))

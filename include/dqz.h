@@ -115,6 +115,13 @@ int dqz_learner_destroy(dqz_learner* learner);
 int dqz_learner_step(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
                      const int32_t* slots, const float* is_weights, void* stream);
 
+/* Gradient only: d loss / d params of the same step into grad_out (device
+ * f32, dqz_param_layout order, padding untouched); params->online / mu / nu
+ * are not modified and mu / nu may be NULL.  = jax.grad(loss_fn) at
+ * dqn/agent.py:112-116. */
+int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                     const int32_t* slots, const float* is_weights, float* grad_out, void* stream);
+
 /* Phases of one learner step, in launch order (dqz_learner_profile):
  *  0 conv1 fwd (frame gather fused)   1 conv2 fwd   2 conv3 fwd
  *  3 fc1 fwd (split-K)
@@ -209,6 +216,49 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
 
 /* Target sync: target <- online (dqn/agent.py:155-156; hard copy, not Polyak). */
 int dqz_target_copy(float* target, const float* online, int64_t total, void* stream);
+
+/* ---- MGSC meta-update (dqn_mgsc_batched/agent.py:104-220) -------------- */
+
+typedef struct dqz_meta_config {
+  int meta_batch;          /* M (meta_batch_size, run_atari.py:101), 1..256 */
+  int num_actions;         /* A; the network is dqn_atari_network (per-action bias) */
+  float learning_rate;     /* inner optax.rmsprop(centered) lr, run_atari.py:218-223 */
+  float decay;             /* 0.95 */
+  float eps;               /* optimizer_epsilon */
+  float grad_error_bound;  /* rlax.clip_gradient bound */
+  float meta_learning_rate; /* optax.adam lr, run_atari.py:241-243 */
+  float b1, b2, meta_eps;  /* optax.adam defaults 0.9, 0.999, 1e-8 */
+} dqz_meta_config;
+
+typedef struct dqz_meta dqz_meta;
+
+int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out);
+int dqz_meta_destroy(dqz_meta* meta);
+
+/* One jitted `meta_update` + `replay.update_priorities` (agent.py:211-220,
+ * 302-334) for the stop-gradient (FIFO) variant:
+ *   p = softmax(logits[pos]) (replay_circular.py:79-86); G = sum_i p_i g_i
+ *   (per-transition grads of loss_fn, agent.py:152-172); theta' = theta +
+ *   RMSProp(G; mu, nu); g' = grad loss_fn(theta', target=theta, online
+ *   transition); theta'' = stop_grad(theta' + RMSProp(g'; mu', nu'));
+ *   L = sum |theta' - theta''|^2; Adam on the M logits, written back to
+ *   logits[pos[i]].
+ * params: online / target / mu / nu are read only (the agent's opt_state is
+ * not advanced by meta_update).  slots: device int32 [M] meta-batch replay
+ * slots in `store`.  online_store/online_slot: the newest transition (device
+ * int32 [1]).  logits: the replay's device logit buffer; pos: device int32
+ * [M] absolute positions (distinct).  adam_mu/adam_nu: device f32 [M];
+ * adam_count: device int32 [1] (ScaleByAdamState). */
+int dqz_meta_update(dqz_meta* meta, const dqz_params* params, const dqz_store* store,
+                    const int32_t* slots, const dqz_store* online_store, const int32_t* online_slot,
+                    float* logits, const int32_t* pos, float* adam_mu, float* adam_nu,
+                    int32_t* adam_count, void* stream);
+
+/* Device copies of the last meta-update's intermediates (any may be NULL):
+ * probs [M], dlogits [M] (d L / d logits), td [M] meta-batch TD errors,
+ * loss [1] = sum |theta' - theta''|^2. */
+int dqz_meta_outputs(dqz_meta* meta, float* probs, float* dlogits, float* td, float* loss,
+                     void* stream);
 
 #ifdef __cplusplus
 }

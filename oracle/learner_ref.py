@@ -207,3 +207,90 @@ def learner_step(online, target, mu, nu, s_tm1, a_tm1, r_t, discount_t, s_t,
 def zeros_like_tree(tree):
   return {m: {n: np.zeros_like(np.asarray(v, np.float64)) for n, v in d.items()}
           for m, d in tree.items()}
+
+
+def _tree_map(f, *trees):
+  return {m: {n: f(*(t[m][n] for t in trees)) for n in trees[0][m]}
+          for m in trees[0]}
+
+
+def _tree_dot(a, b):
+  return sum(float(np.sum(np.asarray(a[m][n], np.float64) *
+                          np.asarray(b[m][n], np.float64)))
+             for m in a for n in a[m])
+
+
+def softmax_logsumexp(logits):
+  """replay_circular.JNPprobabilities_from_logits (replay_circular.py:79-86)."""
+  x = np.asarray(logits, np.float64)
+  c = x.max()
+  return np.exp(x - (c + np.log(np.sum(np.exp(x - c)))))
+
+
+def rmsprop_update_jacobian(g, mu, nu, lr, decay, eps):
+  """d u / d g of the centered RMSProp update u = -lr g rsqrt(D) (diagonal).
+
+  mu' = d mu + c g, nu' = d nu + c g^2, D = nu' - mu'^2 + eps (c = 1 - d):
+  du/dg = -lr D^{-3/2} (D - c g (g - mu')).
+  """
+  c = 1.0 - decay
+  m = c * g + decay * mu
+  v = c * g * g + decay * nu
+  dd = v - m * m + eps
+  return -lr * (dd - c * g * (g - m)) / dd**1.5
+
+
+def meta_update(online, target, mu, nu, meta, logits, online_transition,
+                adam_m, adam_v, adam_count, lr=2.5e-4, decay=0.95,
+                eps=0.01 / 32**2, grad_error_bound=1.0 / 32, meta_lr=2.5e-4):
+  """MGSCDqn.meta_update (dqn_mgsc_batched/agent.py:104-220), fp64.
+
+  meta: dict(s_tm1 [M,84,84,4], a_tm1, r_t, discount_t, s_t) — the meta batch.
+  online_transition: the same keys for one transition (no batch axis).
+  Follows the reference literally: per-example gradients g_i of
+  loss_fn on a single transition (:152-158), G = sum_i p_i g_i (:171-172),
+  theta' = theta + RMSProp(G; s) (:178-179), g' = grad loss_fn(theta',
+  target=theta, online transition) (:183-185), theta'' =
+  stop_gradient(theta' + RMSProp(g'; s')) (:189-191), loss =
+  sum ||theta' - theta''||^2 (:104-110, :195).  The gradient w.r.t. the
+  logits is taken analytically: dL/dtheta' = -2 u', dtheta'/dG = diag(du/dG),
+  dL/dp_i = v . g_i with v = dL/dG; softmax backward; optax adam.
+  Returns dict(probs, td, G, theta_p, g_p, loss, v, dlogits, new_logits,
+  adam_m, adam_v, adam_count).
+  """
+  s_tm1 = np.asarray(meta['s_tm1'])
+  m_size = s_tm1.shape[0]
+  p = softmax_logsumexp(logits)
+  q_tm1, _ = forward(online, s_tm1)
+  q_t, _ = forward(target, np.asarray(meta['s_t']))
+  td, _, _ = td_loss(q_tm1, meta['a_tm1'], meta['r_t'], meta['discount_t'], q_t,
+                     None, None, grad_error_bound)
+  per_example = []
+  for i in range(m_size):
+    qi, cache = forward(online, s_tm1[i:i + 1])
+    _, _, dq = td_loss(qi, np.asarray(meta['a_tm1'])[i:i + 1],
+                       np.asarray(meta['r_t'])[i:i + 1],
+                       np.asarray(meta['discount_t'])[i:i + 1],
+                       q_t[i:i + 1], None, None, grad_error_bound)
+    per_example.append(backward(online, cache, dq))
+  big_g = _tree_map(lambda *gs: sum(pi * g for pi, g in zip(p, gs)),
+                    *per_example)
+  theta_p, mu_p, nu_p = rmsprop_centered(online, big_g, mu, nu, lr, decay, eps)
+  ot = {k: np.asarray(v)[None, ...] for k, v in online_transition.items()}
+  step2 = learner_step(theta_p, online, mu_p, nu_p, ot['s_tm1'], ot['a_tm1'],
+                       ot['r_t'], ot['discount_t'], ot['s_t'], lr=lr,
+                       decay=decay, eps=eps, grad_error_bound=grad_error_bound)
+  theta_pp = step2['params']
+  u_p = _tree_map(lambda a, b: a - b, theta_pp, theta_p)
+  loss = _tree_dot(u_p, u_p)
+  jac = _tree_map(lambda g, m, n: rmsprop_update_jacobian(g, m, n, lr, decay,
+                                                          eps),
+                  big_g, _tree_map(np.asarray, mu), _tree_map(np.asarray, nu))
+  v = _tree_map(lambda u, j: -2.0 * u * j, u_p, jac)
+  dp = np.array([_tree_dot(v, g) for g in per_example])
+  dlogits = p * (dp - np.dot(p, dp))
+  new_logits, m, vv, count = adam(np.asarray(logits, np.float64), dlogits,
+                                  adam_m, adam_v, adam_count, meta_lr)
+  return dict(probs=p, td=td, G=big_g, theta_p=theta_p, g_p=step2['grads'],
+              loss=loss, v=v, dp=dp, dlogits=dlogits, new_logits=new_logits,
+              adam_m=m, adam_v=vv, adam_count=count)

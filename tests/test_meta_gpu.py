@@ -1,0 +1,136 @@
+"""GPU parity: learner gradients and the MGSC meta-update vs the fp64 oracle.
+
+Tolerances: gradients atol 1e-6 + rtol 1e-3 of the leaf's max |g|; meta
+probabilities rtol 1e-6; d meta-loss / d logits within 2e-3 of max |dlogits|
+(f32 sums over 1.7M parameters against fp64); updated logits atol 1e-6 (the
+Adam step is lr-scaled); meta loss rtol 2e-3.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner_ref
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _store(capacity, num_frames, num_actions, seed, device):
+  from dqn_mgsc_zoo_amd import store as store_lib
+  frames, fidx, action, reward, discount = helpers.random_store_contents(
+      capacity, num_frames, num_actions, seed)
+  st = store_lib.FrameStore(capacity, num_frames)
+  for name, arr in (('frames', frames), ('fidx', fidx), ('action', action),
+                    ('reward', reward), ('discount', discount)):
+    getattr(st, name).copy_(torch.from_numpy(arr))
+  host = dict(frames=frames, fidx=fidx, action=action, reward=reward,
+              discount=discount)
+  return st, host
+
+
+def _rand_opt_state(tree, seed):
+  rng = np.random.default_rng(seed)
+  mu = {m: {n: (1e-3 * rng.standard_normal(np.shape(v))).astype(np.float32)
+            for n, v in d.items()} for m, d in tree.items()}
+  nu = {m: {n: (mu[m][n].astype(np.float64)**2 +
+                1e-6 * rng.random(np.shape(v))).astype(np.float32)
+            for n, v in d.items()} for m, d in mu.items()}
+  return mu, nu
+
+
+def _f64(tree):
+  return {m: {n: np.asarray(v, np.float64) for n, v in d.items()}
+          for m, d in tree.items()}
+
+
+@pytest.mark.parametrize('algo', ['dqn', 'double'])
+def test_learner_grad_matches_oracle(device, algo):
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  net = (networks.dqn_atari_network(6) if algo == 'dqn' else
+         networks.double_dqn_atari_network(6))
+  online = net.init(5)
+  target = helpers.perturbed_tree(online, 6)
+  lrn = learner_lib.Learner(net, 32, algo=algo)
+  lrn.set_params(online, target)
+  st, host = _store(128, 320, 6, 7, device)
+  slots = np.random.default_rng(8).integers(0, 128, 32).astype(np.int32)
+  s_tm1 = helpers.stacks_from(host['frames'], host['fidx'], slots, 0)
+  s_t = helpers.stacks_from(host['frames'], host['fidx'], slots, 1)
+  z = learner_ref.zeros_like_tree(online)
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1,
+                                 host['action'][slots], host['reward'][slots],
+                                 host['discount'][slots], s_t, algo=algo)
+  before = lrn.online.clone()
+  g = lrn.grad(st, torch.from_numpy(slots).to(device))
+  assert torch.equal(before, lrn.online)  # gradient mode leaves params alone
+  got = net.unflatten(g.cpu().numpy())
+  for m in ref['grads']:
+    for n in ref['grads'][m]:
+      want = ref['grads'][m][n]
+      np.testing.assert_allclose(got[m][n], want,
+                                 atol=1e-6 + 1e-3 * np.abs(want).max(),
+                                 err_msg='%s/%s' % (m, n))
+
+
+@pytest.mark.parametrize('meta_batch', [8, 100])
+def test_meta_update_matches_oracle(device, meta_batch):
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  a = 6
+  net = networks.dqn_atari_network(a)
+  online = net.init(21)
+  target = helpers.perturbed_tree(online, 22)
+  mu, nu = _rand_opt_state(online, 23)
+  lrn = learner_lib.Learner(net, 32, algo='dqn')
+  lrn.set_params(online, target)
+  lrn.set_opt_state(mu, nu)
+  meta = learner_lib.MetaLearner(lrn, meta_batch, learner_lib.adam(2.5e-4))
+  rng = np.random.default_rng(24)
+  am = (1e-3 * rng.standard_normal(meta_batch)).astype(np.float32)
+  av = (1e-6 * rng.random(meta_batch)).astype(np.float32)
+  meta.set_state({'count': 2, 'mu': am, 'nu': av})
+
+  capacity = 256
+  st, host = _store(capacity, 640, a, 25, device)
+  slots = rng.choice(capacity, meta_batch, replace=False).astype(np.int32)
+  cap_logits = 1000
+  logits = rng.standard_normal(cap_logits).astype(np.float32)
+  pos = rng.choice(cap_logits, meta_batch, replace=False).astype(np.int32)
+  ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot_t[..., 3] = 0  # trailing zero padding
+  ot = replay_lib.Transition(ot_tm1, 3, -1.0, 0.99, ot_t)
+
+  mb = dict(s_tm1=helpers.stacks_from(host['frames'], host['fidx'], slots, 0),
+            a_tm1=host['action'][slots], r_t=host['reward'][slots],
+            discount_t=host['discount'][slots],
+            s_t=helpers.stacks_from(host['frames'], host['fidx'], slots, 1))
+  ref = learner_ref.meta_update(
+      _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
+      dict(s_tm1=ot_tm1, a_tm1=3, r_t=-1.0, discount_t=0.99, s_t=ot_t),
+      am, av, 2)
+
+  meta.set_online_transition(ot)
+  logits_d = torch.from_numpy(logits).to(device)
+  p0 = [t.clone() for t in (lrn.online, lrn.target, lrn.mu, lrn.nu)]
+  meta.update(st, torch.from_numpy(slots).to(device), logits_d,
+              torch.from_numpy(pos).to(device))
+  probs, dlogits, td, loss = [t.cpu().numpy() for t in meta.fetch_outputs()]
+  for before, after in zip(p0, (lrn.online, lrn.target, lrn.mu, lrn.nu)):
+    assert torch.equal(before, after)  # meta_update leaves theta / opt_state
+  np.testing.assert_allclose(probs, ref['probs'], rtol=1e-5)
+  np.testing.assert_allclose(td, ref['td'], atol=1e-4)
+  np.testing.assert_allclose(loss[0], ref['loss'], rtol=2e-3)
+  scale = np.abs(ref['dlogits']).max()
+  assert scale > 0
+  np.testing.assert_allclose(dlogits, ref['dlogits'], atol=2e-3 * scale)
+  new = logits_d.cpu().numpy()
+  np.testing.assert_allclose(new[pos], ref['new_logits'], atol=1e-6)
+  untouched = np.setdiff1d(np.arange(cap_logits), pos)
+  np.testing.assert_array_equal(new[untouched], logits[untouched])
+  state = meta.get_state()
+  assert state['count'] == 3
+  np.testing.assert_allclose(state['mu'], ref['adam_m'], atol=2e-3 * scale)

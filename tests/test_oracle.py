@@ -126,3 +126,90 @@ def test_rmsprop_and_adam_formulas():
   # first bias-corrected Adam step moves by lr * g/|g| (up to eps)
   np.testing.assert_allclose(x, [-0.01, 0.01], rtol=1e-6)
   assert c == 1
+
+
+def _torch_rms(p, g, mu, nu, lr, decay, eps):
+  m = (1 - decay) * g + decay * mu
+  v = (1 - decay) * g * g + decay * nu
+  return p - lr * g * torch.rsqrt(v - m * m + eps), m, v
+
+
+def test_oracle_meta_update_matches_torch_autograd():
+  """MGSC meta_loss_fn (dqn_mgsc_batched/agent.py:160-199) restated in torch
+  and differentiated by autograd w.r.t. the logits, vs the oracle's analytic
+  chain (per-example dot products + softmax backward)."""
+  a, m_size = 6, 4
+  online = _init(a, False, 11)
+  target = helpers.perturbed_tree(online, 12)
+  rng = np.random.default_rng(13)
+  meta = dict(s_tm1=rng.integers(0, 256, (m_size, 84, 84, 4), dtype=np.uint8),
+              a_tm1=rng.integers(0, a, m_size),
+              r_t=np.array([1.0, 0.0, -1.0, 0.0]),
+              discount_t=np.array([0.99, 0.0, 0.99, 0.99]),
+              s_t=rng.integers(0, 256, (m_size, 84, 84, 4), dtype=np.uint8))
+  ot = dict(s_tm1=rng.integers(0, 256, (84, 84, 4), dtype=np.uint8), a_tm1=2,
+            r_t=1.0, discount_t=0.99,
+            s_t=rng.integers(0, 256, (84, 84, 4), dtype=np.uint8))
+  mu = {m: {n: 1e-3 * rng.standard_normal(np.shape(v)) for n, v in d.items()}
+        for m, d in online.items()}
+  nu = {m: {n: mu[m][n]**2 + 1e-6 * rng.random(np.shape(v))
+            for n, v in d.items()} for m, d in mu.items()}
+  logits = rng.standard_normal(m_size).astype(np.float32)
+  am, av = 0.1 * rng.standard_normal(m_size), 0.01 * rng.random(m_size)
+  lr, decay, eps, bound = 2.5e-4, 0.95, 0.01 / 32**2, 0.05
+  ref = learner_ref.meta_update(online, target, mu, nu, meta, logits, ot, am,
+                                av, 3, lr=lr, decay=decay, eps=eps,
+                                grad_error_bound=bound)
+
+  keys = [(m, n) for m in online for n in online[m]]
+  th = {k: torch.tensor(online[k[0]][k[1]], dtype=torch.float64) for k in keys}
+
+  def tree(flat):
+    out = {}
+    for (m, n), v in flat.items():
+      out.setdefault(m, {})[n] = v
+    return out
+
+  def single_grad(params, target_params, s_tm1, act, r, d, s_t):
+    p = {k: v.detach().requires_grad_(True) for k, v in params.items()}
+    q = _torch_q(tree(p), s_tm1[None], False)
+    with torch.no_grad():
+      v = _torch_q(tree(target_params), s_t[None], False).max(dim=1).values
+    td = (r + d * v) - q[0, act]
+    loss = (0.5 * _ClipGrad.apply(td, -bound, bound)**2).mean()
+    gs = torch.autograd.grad(loss, [p[k] for k in keys])
+    return dict(zip(keys, gs))
+
+  x = torch.tensor(logits, dtype=torch.float64, requires_grad=True)
+  c = x.max()
+  probs = torch.exp(x - (c + torch.log(torch.sum(torch.exp(x - c)))))
+  tt = {k: torch.tensor(target[k[0]][k[1]], dtype=torch.float64) for k in keys}
+  per = [single_grad(th, tt, meta['s_tm1'][i], meta['a_tm1'][i], meta['r_t'][i],
+                     meta['discount_t'][i], meta['s_t'][i]) for i in range(m_size)]
+  big_g = {k: sum(probs[i] * per[i][k] for i in range(m_size)) for k in keys}
+  tmu = {k: torch.tensor(mu[k[0]][k[1]]) for k in keys}
+  tnu = {k: torch.tensor(nu[k[0]][k[1]]) for k in keys}
+  th_p, mu_p, nu_p = {}, {}, {}
+  for k in keys:
+    th_p[k], mu_p[k], nu_p[k] = _torch_rms(th[k], big_g[k], tmu[k], tnu[k], lr,
+                                           decay, eps)
+  g2 = single_grad(th_p, th, ot['s_tm1'], ot['a_tm1'], ot['r_t'],
+                   ot['discount_t'], ot['s_t'])
+  loss = 0.0
+  for k in keys:
+    th_pp, _, _ = _torch_rms(th_p[k].detach(), g2[k], mu_p[k].detach(),
+                             nu_p[k].detach(), lr, decay, eps)
+    loss = loss + torch.sum((th_p[k] - th_pp.detach())**2)
+  loss.backward()
+  np.testing.assert_allclose(ref['probs'], probs.detach().numpy(), rtol=1e-12)
+  np.testing.assert_allclose(ref['loss'], loss.item(), rtol=1e-9)
+  np.testing.assert_allclose(ref['dlogits'], x.grad.numpy(), rtol=1e-6,
+                             atol=1e-6 * np.abs(x.grad.numpy()).max())
+  assert np.abs(ref['dlogits']).max() > 0
+  # adam on the logits, optax 0.1.2 bias-corrected, count 3 -> 4
+  b1, b2 = 0.9, 0.999
+  mm = b1 * am + (1 - b1) * ref['dlogits']
+  vv = b2 * av + (1 - b2) * ref['dlogits']**2
+  want = logits - 2.5e-4 * (mm / (1 - b1**4)) / (np.sqrt(vv / (1 - b2**4)) + 1e-8)
+  np.testing.assert_allclose(ref['new_logits'], want, rtol=1e-12)
+  assert ref['adam_count'] == 4
