@@ -22,6 +22,10 @@ from dqn_mgsc_zoo_amd import replay as replay_lib
 
 Transition = replay_lib.Transition
 ReservoirTransitionReplay = replay_lib.ReservoirTransitionReplay
+TransitionAccumulator = replay_lib.TransitionAccumulator  # :1432-1466
+SumTree = replay_lib.SumTree
+importance_sampling_weights = replay_lib.importance_sampling_weights
+_power = replay_lib._power  # pylint: disable=protected-access
 
 
 def TransitionReplay(capacity, structure, random_state, encoder=None,  # pylint: disable=invalid-name
