@@ -105,16 +105,12 @@ def main():
   ap.add_argument('--cpu-seconds', type=float, default=15.0)
   args = ap.parse_args()
 
-  world = int(os.environ.get('WORLD_SIZE', '1'))
-  rank = int(os.environ.get('RANK', '0'))
+  from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-  dist = None
-  if world > 1:
-    import torch.distributed as dist  # pylint: disable=g-import-not-at-top
-    torch.cuda.set_device(local_rank)
-    dist.init_process_group('nccl')
+  torch.cuda.set_device(local_rank)
+  reps = replicas_lib.Replicas('nccl')  # RCCL; replicas only, no grad exchange
+  world, rank = reps.world, reps.rank
   dev = torch.device('cuda', local_rank)
-  torch.cuda.set_device(dev)
 
   from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
   from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
@@ -172,8 +168,7 @@ def main():
 
   done = run(args.warmup, 0)
   steps = (args.steps // g) * g if graph is not None else args.steps
-  if dist is not None:
-    dist.barrier()
+  reps.barrier()
   torch.cuda.synchronize(dev)
   ev0 = torch.cuda.Event(enable_timing=True)
   ev1 = torch.cuda.Event(enable_timing=True)
@@ -183,22 +178,11 @@ def main():
   ev1.record()
   torch.cuda.synchronize(dev)
   elapsed = time.perf_counter() - t0
-  if dist is not None:
-    dist.barrier()
+  reps.barrier()
   gpu_ms = ev0.elapsed_time(ev1)
-  elapsed_max = elapsed
-  stats = torch.tensor([steps / elapsed, elapsed, gpu_ms / 1e3],
-                       dtype=torch.float64, device=dev)
-  if dist is not None:
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
-    gathered = torch.zeros((world, stats.numel()), dtype=torch.float64,
-                           device=dev)
-    dist.all_gather_into_tensor(gathered, stats)  # RCCL stats gather only
-    per_rank = gathered.cpu().numpy()
-  else:
-    per_rank = stats.cpu().numpy()[None, :]
+  elapsed_max = reps.max_over_ranks(elapsed, device=dev)
+  per_rank = reps.gather_stats([steps / elapsed, elapsed, gpu_ms / 1e3],
+                               device=dev)
 
   # Per-phase device time (HIP events on the launch stream) for the roofline.
   phases = lrn.profile(store, slots, iters=args.profile_iters)
@@ -207,8 +191,7 @@ def main():
   finite = bool(torch.isfinite(lrn.online).all().item())
 
   if rank != 0:
-    if dist is not None:
-      dist.destroy_process_group()
+    reps.close()
     return
 
   value = world * steps / elapsed_max
@@ -268,8 +251,7 @@ def main():
   else:
     out['cpu_baseline'] = None
   print(json.dumps(out), flush=True)
-  if dist is not None:
-    dist.destroy_process_group()
+  reps.close()
 
 
 if __name__ == '__main__':

@@ -1,0 +1,67 @@
+"""CPU: libdqz.so loads and exports every function include/dqz.h declares,
+and the ctypes binding table matches the header (no compute calls)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'dqz.h')
+
+
+def _declared():
+  text = open(HEADER).read()
+  text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+  return sorted(set(re.findall(r'\b(dqz_\w+)\s*\(', text)))
+
+
+@pytest.fixture(scope='module')
+def libdqz():
+  from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+  if not os.path.exists(_native.LIB_PATH):
+    import __graft_entry__  # pylint: disable=g-import-not-at-top
+    __graft_entry__._compile_lib()  # pylint: disable=protected-access
+  return ctypes.CDLL(_native.LIB_PATH)
+
+
+def test_header_declares_the_abi():
+  names = _declared()
+  assert 'dqz_learner_step' in names and 'dqz_meta_update' in names
+  assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol(libdqz):
+  missing = [n for n in _declared() if not hasattr(libdqz, n)]
+  assert not missing, missing
+
+
+def test_binding_table_matches_header(libdqz):
+  from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+  assert sorted(_native.SIGNATURES) == _declared()
+  _native.lib()  # binds restype/argtypes of every symbol
+
+
+def test_error_paths_without_a_gpu(libdqz):
+  """Argument validation runs before any HIP call."""
+  from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+  lib = _native.lib()
+  offs = (ctypes.c_int64 * 10)()
+  sizes = (ctypes.c_int64 * 10)()
+  total = ctypes.c_int64()
+  assert lib.dqz_param_layout(6, 0, offs, sizes, ctypes.byref(total)) == 0
+  assert sum(sizes) == 1687206 and total.value % 64 == 0
+  assert lib.dqz_param_layout(6, 1, offs, sizes, ctypes.byref(total)) == 0
+  assert sum(sizes) == 1687201
+  assert lib.dqz_param_layout(0, 0, offs, sizes, ctypes.byref(total)) == -1
+  assert b'num_actions' in lib.dqz_last_error()
+  cfg = _native.DqzLearnerConfig(0, 6, 0, 2.5e-4, 0.95, 1e-5, 1 / 32)
+  h = ctypes.c_void_p()
+  assert lib.dqz_learner_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
+  assert b'batch' in lib.dqz_last_error()
+  mcfg = _native.DqzMetaConfig(100000, 6, 2.5e-4, 0.95, 1e-5, 1 / 32, 2.5e-4,
+                               0.9, 0.999, 1e-8)
+  assert lib.dqz_meta_create(ctypes.byref(mcfg), ctypes.byref(h)) == -3
+  with pytest.raises(_native.NativeLibraryError, match='meta_batch'):
+    _native.check(lib.dqz_meta_create(ctypes.byref(mcfg), ctypes.byref(h)))
