@@ -56,18 +56,31 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
       }
     }
   } else {
+    // slot -> 4 frame ids -> 504 16-byte pieces (2 per thread), all loads in
+    // flight before the first LDS store.
     const int slot = src.slots[b];
-    for (int i = threadIdx.x; i < FC * QPC; i += blockDim.x) {
-      const int ci = i / QPC, j = i % QPC;
-      const int f = src.fidx[(int64_t)slot * 8 + which * 4 + ci];
-      float* dst = s_in + ci * C1_PLANE + j * 16;
-      if (f < 0) {
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int32_t* fr = src.fidx + (int64_t)slot * 8 + which * 4;
+    const int f0 = fr[0], f1 = fr[1], f2 = fr[2], f3 = fr[3];
+    constexpr int NP = FC * QPC;  // 504
+    uint4 v[2];
+    int fq[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(dst + 4 * q) = z;
-      } else {
-        const uint4* g = reinterpret_cast<const uint4*>(src.frames + (int64_t)f * FB + row0 * FW);
-        store_bytes_as_f32(dst, g[j]);
+    for (int q = 0; q < 2; ++q) {
+      const int i = min((int)threadIdx.x + 256 * q, NP - 1);
+      const int ci = i / QPC, j = i % QPC;
+      const int f = ci == 0 ? f0 : ci == 1 ? f1 : ci == 2 ? f2 : f3;
+      fq[q] = f;
+      const uint4* g = reinterpret_cast<const uint4*>(src.frames + (int64_t)max(f, 0) * FB + row0 * FW);
+      v[q] = g[j];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = (int)threadIdx.x + 256 * q;
+      if (i < NP) {
+        const int ci = i / QPC, j = i % QPC;
+        float* dst = s_in + ci * C1_PLANE + j * 16;
+        if (fq[q] < 0) v[q] = make_uint4(0u, 0u, 0u, 0u);  // trailing zero padding
+        store_bytes_as_f32(dst, v[q]);
       }
     }
   }
@@ -89,10 +102,13 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   float* s_in = smem;                  // 8064
   float* s_w = smem + C1_IN_FLOATS;    // 256 x 32
   const int rb = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
-  const float* w = a.nz.p[z] + a.w_off;
-  for (int i = threadIdx.x; i < C1KK * C1CO / 4; i += blockDim.x)
-    reinterpret_cast<float4*>(s_w)[i] = reinterpret_cast<const float4*>(w)[i];
+  const float4* w4 = reinterpret_cast<const float4*>(a.nz.p[z] + a.w_off);
+  float4 wv[8];  // 256 x 32 weights = 8 float4 per thread, issued together
+#pragma unroll
+  for (int q = 0; q < 8; ++q) wv[q] = w4[threadIdx.x + 256 * q];
   stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) reinterpret_cast<float4*>(s_w)[threadIdx.x + 256 * q] = wv[q];
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -137,10 +153,15 @@ __global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
   float* s_in = smem;                 // 8064
   float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
   const int rb = blockIdx.x, b = blockIdx.y;
-  const float* dy = a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO;
-  for (int i = threadIdx.x; i < C1_POS * C1CO / 4; i += blockDim.x)
-    reinterpret_cast<float4*>(s_dy)[i] = reinterpret_cast<const float4*>(dy)[i];
+  const float4* dy4 = reinterpret_cast<const float4*>(a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO);
+  constexpr int ND4 = C1_POS * C1CO / 4;  // 800
+  float4 dv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dv[q] = dy4[min((int)threadIdx.x + 256 * q, ND4 - 1)];
   stage_conv1_input(s_in, a.src, b, a.which, rb);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if ((int)threadIdx.x + 256 * q < ND4) reinterpret_cast<float4*>(s_dy)[threadIdx.x + 256 * q] = dv[q];
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -1,0 +1,225 @@
+// fwd.hpp — conv2 / conv3 / fc1 forward as per-sample LDS-window kernels.
+//
+// B = 32 makes every layer a tiny GEMM (M = 32 x 81 rows at most), so a
+// generic tiled GEMM leaves most of the 256 CUs idle and spends its time on
+// im2col address arithmetic.  These kernels instead give each workgroup one
+// sample (one network copy z) and one 16-channel quarter of the outputs:
+//   * the sample's whole input window is staged once into LDS with padded
+//     pixel / row strides chosen so that the A-operand reads of a
+//     v_mfma_f32_16x16x4_f32 (16 consecutive output positions x 2 k lanes
+//     per 32-lane group) hit 32 distinct banks;
+//   * each wave owns a quarter of K and keeps its weight slice (the B
+//     operand) in registers, loaded once with plain global loads;
+//   * the inner loop is fully unrolled: ds_read_b32 at immediate offsets +
+//     MFMA, no VALU address math;
+//   * the four K-quarter partial tiles are summed through LDS in a fixed
+//     order (deterministic), then bias + ReLU (or the linear tangent mode of
+//     the MGSC meta-update) and a coalesced store.
+// Work per launch: Z x B x 4 workgroups (256 at B = 32, Z = 2).
+#pragma once
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace dqz {
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct LayerFwdArgs {
+  const float* in;  // [Z][B][...] layer input (NHWC)
+  NetZ nz;
+  int64_t w_off, b_off;
+  int B;
+  int linear;  // 1: pre-activation output, no ReLU (tangent forward)
+  float* out;  // [Z][B][...]
+};
+
+// ---- conv2: 20x20x32 -> 9x9x64, 4x4 stride 2 -------------------------------
+// LDS image: element (ih, iw, ci) at ih*C2L_RS + iw*C2L_S + ci.  Bank of the
+// A read for position p = 9 oh + ow: 2*oh*RS + 2*ow*S = 2p (mod 32).
+constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
+
+__global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
+  __shared__ float s_in[C2L_WIN];
+  const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
+  const int n = lane & 15, kq = lane >> 4;
+  const float* W = a.nz.p[z] + a.w_off;  // [512][64], k = kh*128 + kw*32 + ci
+  float wr[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) wr[kk] = W[(w * 128 + 4 * kk + kq) * C2CO + 16 * nq + n];
+  const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C1M * C1CO));
+  constexpr int NQ4 = C1M * C1CO / 4;  // 3200
+  float4 r[13];
+#pragma unroll
+  for (int q = 0; q < 13; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+#pragma unroll
+  for (int q = 0; q < 13; ++q) {
+    const int i = t + 256 * q;
+    if (i < NQ4) {
+      const int pix = i >> 3, ci = (i & 7) * 4;  // 8 float4 per pixel
+      float* d = s_in + (pix / C1O) * C2L_RS + (pix % C1O) * C2L_S + ci;
+      d[0] = r[q].x;
+      d[1] = r[q].y;
+      d[2] = r[q].z;
+      d[3] = r[q].w;
+    }
+  }
+  __syncthreads();
+  int base[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int p = min(16 * m + n, C2M - 1);
+    base[m] = (2 * (p / C2O) + w) * C2L_RS + 2 * (p % C2O) * C2L_S + kq;
+  }
+  f32x4 acc[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    const int off = (kk >> 3) * C2L_S + 4 * (kk & 7);  // kw, ci block
+#pragma unroll
+    for (int m = 0; m < 6; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+  }
+  __syncthreads();
+  float* s_red = s_in;  // [4][96][16]
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 1536 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  __syncthreads();
+  const float* bias = a.nz.p[z] + a.b_off + 16 * nq;
+  float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
+  for (int i = t; i < C2M * 16; i += 256) {
+    const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bias[i & 15];
+    out[(i >> 4) * C2CO + (i & 15)] = a.linear ? v : relu(v);
+  }
+}
+
+// ---- conv3: 9x9x64 -> 7x7x64, 3x3 stride 1 ---------------------------------
+// Wave w owns input channels [16w, 16w + 16) of every tap.  Bank of the A read
+// for p = 7 oh + ow: oh*RS + ow*S = 14 oh + 2 ow = 2p (mod 32).
+constexpr int C3L_S = 66, C3L_RS = 622, C3L_WIN = 9 * C3L_RS;  // 5598 floats
+
+__global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
+  __shared__ float s_in[C3L_WIN];
+  const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  const float* W = a.nz.p[z] + a.w_off;  // [576][64], k = (kh*3 + kw)*64 + ci
+  float wr[36];
+#pragma unroll
+  for (int kk = 0; kk < 36; ++kk)
+    wr[kk] = W[((kk >> 2) * C3CI + 16 * w + 4 * (kk & 3) + kq) * C3CO + 16 * nq + n];
+  const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C2M * C2CO));
+  constexpr int NQ4 = C2M * C2CO / 4;  // 1296
+  float4 r[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NQ4) {
+      const int pix = i >> 4, ci = (i & 15) * 4;
+      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + ci;
+      d[0] = r[q].x;
+      d[1] = r[q].y;
+      d[2] = r[q].z;
+      d[3] = r[q].w;
+    }
+  }
+  __syncthreads();
+  int base[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int p = min(16 * m + n, C3M - 1);
+    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + 16 * w + kq;
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 36; ++kk) {
+    const int tap = kk >> 2;
+    const int off = (tap / 3) * C3L_RS + (tap % 3) * C3L_S + 4 * (kk & 3);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+  }
+  __syncthreads();
+  float* s_red = s_in;  // [4][64][16]
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 1024 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  __syncthreads();
+  const float* bias = a.nz.p[z] + a.b_off + 16 * nq;
+  float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
+  for (int i = t; i < C3M * 16; i += 256) {
+    const float v = ((s_red[i] + s_red[1024 + i]) + (s_red[2048 + i] + s_red[3072 + i])) + bias[i & 15];
+    out[(i >> 4) * C3CO + (i & 15)] = a.linear ? v : relu(v);
+  }
+}
+
+// ---- fc1: [B][3136] x [3136][512] split-K partials ------------------------
+// grid (32 column tiles of 16, FC1_S K-splits of 448, Z * ceil(B/32)); wave w
+// owns k in [448 s + 112 w, +112).  K is permuted inside each 16-block so a
+// lane's four k for steps e = 0..3 are contiguous: one float4 A load per
+// (row tile, 16-block).  Partials [Z][FC1_S][B][512] are reduced by the head.
+constexpr int FC1_S = 7, FC1_KS = FLAT / FC1_S, FC1_KW = FC1_KS / 4;  // 448, 112
+
+struct Fc1FwdArgs {
+  const float* in;  // [Z][B][3136]
+  NetZ nz;
+  int64_t w_off;
+  int B, MG;        // MG = ceil(B / 32) row groups
+  float* part;      // [Z][FC1_S][B][512]
+};
+
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
+  __shared__ float s_red[4][2][256];
+  const int nt = blockIdx.x, s = blockIdx.y, z = blockIdx.z / a.MG, mg = blockIdx.z % a.MG;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  const int k0 = s * FC1_KS + w * FC1_KW;
+  const float* W = a.nz.p[z] + a.w_off + 16 * nt + n;  // [3136][512]
+  constexpr int J = FC1_KW / 16;                        // 7
+  float wr[J][4];
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[j][e] = W[(int64_t)(k0 + 16 * j + 4 * kq + e) * HID];
+  float4 av[2][J];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int row = min(32 * mg + 16 * mt + n, a.B - 1);
+    const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0 + 4 * kq;
+#pragma unroll
+    for (int j = 0; j < J; ++j) av[mt][j] = *reinterpret_cast<const float4*>(x + 16 * j);
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      acc[mt] = mfma4(av[mt][j].x, wr[j][0], acc[mt]);
+      acc[mt] = mfma4(av[mt][j].y, wr[j][1], acc[mt]);
+      acc[mt] = mfma4(av[mt][j].z, wr[j][2], acc[mt]);
+      acc[mt] = mfma4(av[mt][j].w, wr[j][3], acc[mt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w][mt][(4 * kq + rr) * 16 + n] = acc[mt][rr];
+  __syncthreads();
+  // 512 outputs (32 rows x 16 cols), 2 per thread
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 32 * mg + 16 * h + (t >> 4);
+    const float v = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
+    if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
+  }
+}
+
+}  // namespace dqz

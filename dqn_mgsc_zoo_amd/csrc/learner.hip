@@ -18,6 +18,8 @@
 #include "common.hpp"
 #include "conv1.hpp"
 #include "gemm.hpp"
+#include "fwd.hpp"
+#include "bwd.hpp"
 #include "head.hpp"
 #include "meta.hpp"
 #include "sampling.hpp"
@@ -271,9 +273,9 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   L->shared_bias = cfg->algo == DQZ_ALGO_DQN ? 0 : 1;
   param_layout(cfg->num_actions, L->shared_bias, L->off, L->sz, &L->total);
   const int B = cfg->batch, Z = L->Z, A = cfg->num_actions;
-  L->S_fc1 = make_shape<CfgFc1>(Z, B, HID, FLAT, 14).g.S;
+  L->S_fc1 = FC1_S;
   L->S2 = make_shape<CfgBwd3>(1, C2KK + 1, C2CO, B * C2M, std::max(1, (B * C2M + 287) / 288)).g.S;
-  L->S3 = make_shape<CfgBwd2>(1, C3KK + 1, C3CO, B * C3M, std::max(1, (B * C3M + 223) / 224)).g.S;
+  L->S3 = B;  // per-sample conv3 dW partials (conv3_bwd_kernel)
   const int64_t n_y1 = (int64_t)Z * B * C1M * C1CO, n_y2 = (int64_t)Z * B * C2M * C2CO, n_y3 = (int64_t)Z * B * FLAT;
   const int64_t n_fc1p = (int64_t)Z * L->S_fc1 * B * HID, n_h1 = (int64_t)Z * B * HID, n_q = (int64_t)Z * B * A;
   const int64_t n_dz1 = (int64_t)B * HID, n_dy3 = (int64_t)B * FLAT, n_dy2 = (int64_t)B * C2M * C2CO,
@@ -343,37 +345,36 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   DQZ_HIP(hipGetLastError());
   pe.mark(1, st);
 
-  Conv2Fwd c2;
-  static_cast<Shape&>(c2) = make_shape<CfgConv>(Z, B * C2M, C2CO, C2KK, 1);
+  LayerFwdArgs c2;
   c2.in = L->y1;
-  c2.B = B;
-  c2.linear = 0;
   c2.nz = nz;
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
+  c2.B = B;
+  c2.linear = 0;
   c2.out = L->y2;
-  DQZ_HIP((launch_gemm<CfgConv>(st, c2)));
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(4, B, Z), dim3(256), 0, st, c2);
+  DQZ_HIP(hipGetLastError());
   pe.mark(2, st);
 
-  Conv3Fwd c3;
-  static_cast<Shape&>(c3) = make_shape<CfgConv>(Z, B * C3M, C3CO, C3KK, 1);
+  LayerFwdArgs c3 = c2;
   c3.in = L->y2;
-  c3.B = B;
-  c3.linear = 0;
-  c3.nz = nz;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  DQZ_HIP((launch_gemm<CfgConv>(st, c3)));
+  hipLaunchKernelGGL(conv3_fwd_kernel, dim3(4, B, Z), dim3(256), 0, st, c3);
+  DQZ_HIP(hipGetLastError());
   pe.mark(3, st);
 
-  Fc1Fwd f1;
-  static_cast<Shape&>(f1) = make_shape<CfgFc1>(Z, B, HID, FLAT, L->S_fc1);
+  Fc1FwdArgs f1;
   f1.in = L->y3;
   f1.nz = nz;
   f1.w_off = L->off[6];
+  f1.B = B;
+  f1.MG = (B + 31) / 32;
   f1.part = L->fc1p;
-  DQZ_HIP((launch_gemm<CfgFc1>(st, f1)));
+  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
+  DQZ_HIP(hipGetLastError());
   pe.mark(4, st);
   return DQZ_OK;
 }
@@ -445,36 +446,29 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   DQZ_HIP(hipGetLastError());
   pe.mark(5, st);
 
-  Fc1Dx fdx;
-  static_cast<Shape&>(fdx) = make_shape<CfgFc1Dx>(1, B, FLAT, HID, 1);
-  fdx.dz1 = L->dz1;
-  fdx.w1 = P->online + L->off[6];
-  fdx.y3 = L->y3;
-  fdx.dy3 = L->dy3;
-  DQZ_HIP((launch_gemm<CfgFc1Dx>(st, fdx)));
+  Fc1BwdArgs fb;
+  fb.dz1 = L->dz1;
+  fb.y3 = L->y3;
+  fb.th = P->online;
+  fb.mu = P->mu;
+  fb.nu = P->nu;
+  fb.w_off = L->off[6];
+  fb.rms = rms;
+  fb.B = B;
+  fb.dy3 = L->dy3;
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+  DQZ_HIP(hipGetLastError());
   pe.mark(6, st);
 
-  Conv3Dx c3dx;
-  static_cast<Shape&>(c3dx) = make_shape<CfgBwd2>(1, B * C2M, C3CI, C3KK, 1);
-  c3dx.dy3 = L->dy3;
-  c3dx.w3 = P->online + L->off[4];
-  c3dx.y2 = L->y2;
-  c3dx.dy2 = L->dy2;
-  Conv3Dw c3dw;
-  static_cast<Shape&>(c3dw) = make_shape<CfgBwd2>(1, C3KK + 1, C3CO, B * C3M, L->S3);
-  c3dw.in = L->y2;
-  c3dw.dy = L->dy3;
-  c3dw.part = L->p3;
-  Fc1DwRms f1dw;
-  static_cast<Shape&>(f1dw) = make_shape<CfgBwd2>(1, FLAT, HID, B, 1);
-  f1dw.y3 = L->y3;
-  f1dw.dz1 = L->dz1;
-  f1dw.th = P->online;
-  f1dw.mu = P->mu;
-  f1dw.nu = P->nu;
-  f1dw.w_off = L->off[6];
-  f1dw.rms = rms;
-  DQZ_HIP((launch_gemm<CfgBwd2>(st, c3dx, c3dw, f1dw)));
+  Conv3BwdArgs c3b;
+  c3b.dy3 = L->dy3;
+  c3b.y2 = L->y2;
+  c3b.w3 = P->online + L->off[4];
+  c3b.dy2 = L->dy2;
+  c3b.part = L->p3;
+  c3b.B = B;
+  hipLaunchKernelGGL(conv3_bwd_kernel, dim3(12, B), dim3(256), 0, st, c3b);
+  DQZ_HIP(hipGetLastError());
   pe.mark(7, st);
 
   Conv2DxPhased c2dx;
@@ -513,7 +507,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.p3 = L->p3;
   u.S1 = B * C1_BLOCKS;
   u.S2 = c2dw.g.S;
-  u.S3 = c3dw.g.S;
+  u.S3 = B;
   u.h1 = L->h1;
   u.dz1 = L->dz1;
   u.gq = L->gq;
@@ -907,31 +901,32 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   c1.out = H->zv1;
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(C1_BLOCKS, M, 1), dim3(256), kConv1FwdSmem, st, c1);
   DQZ_HIP(hipGetLastError());
-  Conv2Fwd c2;
-  static_cast<Shape&>(c2) = make_shape<CfgConv>(1, M * C2M, C2CO, C2KK, 1);
+  LayerFwdArgs c2;
   c2.in = L->y1;
-  c2.B = M;
-  c2.linear = 1;
   c2.nz = nv;
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
+  c2.B = M;
+  c2.linear = 1;
   c2.out = H->zv2;
-  Conv3Fwd c3;
-  static_cast<Shape&>(c3) = make_shape<CfgConv>(1, M * C3M, C3CO, C3KK, 1);
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(4, M, 1), dim3(256), 0, st, c2);
+  DQZ_HIP(hipGetLastError());
+  LayerFwdArgs c3 = c2;
   c3.in = L->y2;
-  c3.B = M;
-  c3.linear = 1;
-  c3.nz = nv;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = H->zv3;
-  Fc1Fwd f1;
-  static_cast<Shape&>(f1) = make_shape<CfgFc1>(1, M, HID, FLAT, L->S_fc1);
+  hipLaunchKernelGGL(conv3_fwd_kernel, dim3(4, M, 1), dim3(256), 0, st, c3);
+  DQZ_HIP(hipGetLastError());
+  Fc1FwdArgs f1;
   f1.in = L->y3;
   f1.nz = nv;
   f1.w_off = L->off[6];
+  f1.B = M;
+  f1.MG = (M + 31) / 32;
   f1.part = H->zvp;
-  DQZ_HIP((launch_gemm<CfgConv>(st, c2, c3, f1)));
+  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, f1.MG), dim3(256), 0, st, f1);
+  DQZ_HIP(hipGetLastError());
 
   MetaDotArgs md;
   md.dy1 = L->dy1;
@@ -944,7 +939,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   md.zv2 = H->zv2;
   md.zv3 = H->zv3;
   md.zvp = H->zvp;
-  md.S = f1.g.S;
+  md.S = FC1_S;
   md.M = M;
   md.A = A;
   md.v = v;

@@ -126,8 +126,9 @@ int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_s
  *  0 conv1 fwd (frame gather fused)   1 conv2 fwd   2 conv3 fwd
  *  3 fc1 fwd (split-K)
  *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample)
- *  5 fc1 dX                           6 {conv3 dX, conv3 dW, fc1 dW+RMSProp}
- *  7 {conv2 dX, conv2 dW}             8 conv1 dW (frame gather fused)
+ *  5 fc1 backward: dX + dW + RMSProp of fc1/w in one pass over W1
+ *  6 {conv3 dX, conv3 dW}             7 {conv2 dX, conv2 dW}
+ *  8 conv1 dW (frame gather fused)
  *  9 gradient reductions + RMSProp (all leaves but fc1/w) */
 #define DQZ_NUM_PHASES 10
 
