@@ -10,7 +10,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libdqz.so')
+LIB_PATH = os.environ.get('DQZ_LIB') or os.path.join(_HERE, 'libdqz.so')
 
 DQZ_OK = 0
 ALGO_DQN = 0

@@ -27,6 +27,7 @@ struct Fc1BwdArgs {
 };
 
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
+  DQZ_STAMP(5, 0);
   __shared__ float s_red[4][2][256];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -100,6 +101,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
     }
     __syncthreads();
   }
+  DQZ_STAMP(5, 2);
   const Rms& R = a.rms;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
@@ -117,6 +119,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
         a.th[i] = o_th[4 * q + r] + (-R.lr) * (g * rsqrtf(v - m * m + R.eps));
       }
     }
+  DQZ_STAMP(5, 3);
 }
 
 // ---- conv3 backward: dX and per-sample dW partials -----------------------
@@ -265,12 +268,166 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
 }
 
 __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
+  DQZ_STAMP(6, 0);
   __shared__ float s_win[C3X_WIN];
   const int job = blockIdx.x, b = blockIdx.y;
   if (job < 8)
     conv3_bwd_dx(a, s_win, b, job & 3, job >> 2);
   else
     conv3_bwd_dw(a, s_win, b, job - 8);
+  DQZ_STAMP(6, 3);
+}
+
+// ---- conv2 backward: dX by stride phase and per-sample dW partials --------
+// grid (12, B).  Jobs 0..7: dX of stride phase (ph, pw) = (job & 3) >> 1,
+// job & 1 for input-channel half job >> 2: output pixels (2a + ph, 2c + pw),
+// a, c in [0, 10), are a 2x2-tap correlation of dy2 zero-padded by 1 with
+// W2[ph + 2(1 - u)][pw + 2(1 - v)] (K = 4 taps x 64 co), masked by relu'(y1).
+// Jobs 8..11: dW partial of output-channel quarter (job - 8):
+// part[b][(kh*4 + kw)*32 + ci][co] = sum_p y1[b][2oh+kh][2ow+kw][ci] dy2[b][p][co]
+// (bias row 512 = sum_p dy2).  Wave w of a dW job owns kh = w.
+constexpr int C2X_S = 66, C2X_RS = 756, C2X_WIN = 11 * C2X_RS;  // padded dy2 window, 8316 floats
+constexpr int C2W_S = 40, C2W_RS = 808, C2W_WIN = 20 * C2W_RS;  // y1 window for dW, 16160 floats
+
+struct Conv2BwdArgs {
+  const float* dy2;  // [B][81][64]
+  const float* y1;   // [B][400][32] online
+  const float* w2;   // online W2 [4][4][32][64]
+  float* dy1;        // [B][400][32]
+  float* part;       // [B][513][64]
+  int B;
+};
+
+__device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  float wr[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int tp = kk >> 2, u = tp >> 1, v = tp & 1;
+    const int kh = ph + 2 * (1 - u), kw = pw + 2 * (1 - v);
+    wr[kk] = a.w2[((kh * C2K + kw) * C2CI + 16 * hh + n) * C2CO + 16 * w + 4 * (kk & 3) + kq];
+  }
+  const float4* src = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * (C2M * C2CO));
+  constexpr int NW4 = 121 * 16;  // 1936
+  float4 r[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int i = min(t + 256 * q, NW4 - 1);
+    const int pix = i >> 4, oh = pix / 11 - 1, ow = pix % 11 - 1;
+    const bool in = oh >= 0 && oh < C2O && ow >= 0 && ow < C2O;
+    const float4 v = src[(in ? oh * C2O + ow : 0) * 16 + (i & 15)];
+    r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int i = t + 256 * q;
+    if (i < NW4) {
+      const int pix = i >> 4;
+      float* d = s_win + (pix / 11) * C2X_RS + (pix % 11) * C2X_S + (i & 15) * 4;
+      d[0] = r[q].x;
+      d[1] = r[q].y;
+      d[2] = r[q].z;
+      d[3] = r[q].w;
+    }
+  }
+  __syncthreads();
+  int base[7];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    const int p = min(16 * m + n, 99);  // p = 10 a + c
+    base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + 16 * w + kq;
+  }
+  f32x4 acc[7];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int tp = kk >> 2;  // (u', v') = (tp >> 1, tp & 1)
+    const int off = (tp >> 1) * C2X_RS + (tp & 1) * C2X_S + 4 * (kk & 3);
+#pragma unroll
+    for (int m = 0; m < 7; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
+  }
+  __syncthreads();
+  float* s_red = s_win;  // [4][112][16]
+#pragma unroll
+  for (int m = 0; m < 7; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  __syncthreads();
+  for (int i = t; i < 1600; i += 256) {
+    const int p = i >> 4, ah = p / 10, cw = p % 10;
+    const float v = (s_red[i] + s_red[1792 + i]) + (s_red[3584 + i] + s_red[5376 + i]);
+    const int64_t o = ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15);
+    a.dy1[o] = a.y1[o] > 0.f ? v : 0.f;
+  }
+}
+
+__device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win, int b, int nq) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
+  const int n = lane & 15, kq = lane >> 4;
+  float dr[21];
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk) {
+    const int p = 4 * kk + kq;
+    const float v = a.dy2[((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 16 * nq + n];
+    dr[kk] = p < C2M ? v : 0.f;
+  }
+  const float4* src = reinterpret_cast<const float4*>(a.y1 + (int64_t)b * (C1M * C1CO));
+  constexpr int NQ4 = C1M * C1CO / 4;  // 3200
+  float4 r[13];
+#pragma unroll
+  for (int q = 0; q < 13; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+#pragma unroll
+  for (int q = 0; q < 13; ++q) {
+    const int i = t + 256 * q;
+    if (i < NQ4) {
+      const int pix = i >> 3;
+      *reinterpret_cast<float4*>(s_win + (pix / C1O) * C2W_RS + (pix % C1O) * C2W_S + (i & 7) * 4) = r[q];
+    }
+  }
+  __syncthreads();
+  int pb[21];
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk) {
+    const int p = min(4 * kk + kq, C2M - 1);
+    pb[kk] = (2 * (p / C2O) + w) * C2W_RS + 2 * (p % C2O) * C2W_S + n;
+  }
+  f32x4 acc[8];  // tile = (kw, ci half)
+#pragma unroll
+  for (int m = 0; m < 8; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int off = (m >> 1) * C2W_S + 16 * (m & 1);
+      acc[m] = mfma4(s_win[pb[kk] + off], dr[kk], acc[m]);
+    }
+  float* part = a.part + (int64_t)b * (C2KK + 1) * C2CO + 16 * nq + n;
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      part[((w * C2K + (m >> 1)) * C2CI + 16 * (m & 1) + 4 * kq + rr) * C2CO] = acc[m][rr];
+  if (w == 0) {
+    float sb = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 21; ++kk) sb += dr[kk];
+    sb += __shfl_xor(sb, 16, 64);
+    sb += __shfl_xor(sb, 32, 64);
+    if (kq == 0) part[C2KK * C2CO] = sb;
+  }
+}
+
+__global__ __launch_bounds__(256) void conv2_bwd_kernel(Conv2BwdArgs a) {
+  DQZ_STAMP(7, 0);
+  __shared__ float s_win[C2W_WIN];
+  const int job = blockIdx.x, b = blockIdx.y;
+  if (job < 8)
+    conv2_bwd_dx(a, s_win, b, (job & 3) >> 1, job & 1, job >> 2);
+  else
+    conv2_bwd_dw(a, s_win, b, job - 8);
+  DQZ_STAMP(7, 3);
 }
 
 }  // namespace dqz

@@ -88,10 +88,44 @@ struct Rms {
   }
 };
 
+// In-kernel timeline stamps (diagnostic builds only: -DDQZ_TRACE).  Wave 0 of
+// every workgroup records s_memrealtime (100 MHz, chip-wide) at named points;
+// tools/trace_step.py reads them back with dqz_debug_trace().
+#ifdef DQZ_TRACE
+constexpr int TRACE_KERNELS = 16, TRACE_BLOCKS = 1024, TRACE_SLOTS = 4;
+__device__ unsigned long long g_dqz_trace[TRACE_KERNELS * TRACE_BLOCKS * TRACE_SLOTS];
+#define DQZ_STAMP(kid, slot)                                                                              \
+  do {                                                                                                    \
+    if (threadIdx.x == 0) {                                                                               \
+      const unsigned bl_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                \
+      if (bl_ < (unsigned)dqz::TRACE_BLOCKS)                                                              \
+        dqz::g_dqz_trace[((kid) * dqz::TRACE_BLOCKS + bl_) * dqz::TRACE_SLOTS + (slot)] =                \
+            __builtin_amdgcn_s_memrealtime();                                                             \
+    }                                                                                                     \
+  } while (0)
+#else
+#define DQZ_STAMP(kid, slot) \
+  do {                       \
+  } while (0)
+#endif
+
+// Wave64 sum with DPP (VALU-only cross-lane moves; __shfl_xor lowers to
+// ds_bpermute, an LDS round trip per step): row_shr 1/2/4/8 leaves each
+// 16-lane row's sum in its lane 15, row_bcast 15 / 31 fold the rows into lane
+// 63, readlane broadcasts it.  Masked-off lanes read 0 (update_dpp old = 0).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0x111>(v);
+  v += dpp_f<0x112>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  v += dpp_f<0x142, 0xa>(v);
+  v += dpp_f<0x143, 0xc>(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // Philox4x32-10 (Salmon et al., SC'11).

@@ -98,10 +98,12 @@ struct Conv1FwdArgs {
 // grid (4 row blocks, B, Z); 256 threads; each wave owns 32 positions x 32
 // channels (the 4th wave's tile is 4/32 live).
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
+  DQZ_STAMP(0, 0);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                  // 8064
   float* s_w = smem + C1_IN_FLOATS;    // 256 x 32
   const int rb = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const float bias = a.nz.p[z][a.b_off + (threadIdx.x & 31)];  // epilogue operand, loaded early
   const float4* w4 = reinterpret_cast<const float4*>(a.nz.p[z] + a.w_off);
   float4 wv[8];  // 256 x 32 weights = 8 float4 per thread, issued together
 #pragma unroll
@@ -109,6 +111,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb);
 #pragma unroll
   for (int q = 0; q < 8; ++q) reinterpret_cast<float4*>(s_w)[threadIdx.x + 256 * q] = wv[q];
+  DQZ_STAMP(0, 1);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -125,8 +128,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
     const float bv = pb[64 * j];
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
   }
+  DQZ_STAMP(0, 2);
   // C/D map of 32x32x2: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h
-  const float bias = a.nz.p[z][a.b_off + i];
   float* out = a.out + (((int64_t)z * a.B + b) * C1M + rb * C1_POS) * C1CO;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -136,6 +139,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
       out[pos * C1CO + i] = a.linear ? v : relu(v);
     }
   }
+  DQZ_STAMP(0, 3);
 }
 
 struct Conv1DwArgs {
@@ -149,6 +153,7 @@ struct Conv1DwArgs {
 // grid (4 row blocks, B); wave w owns kernel rows [64w, 64w+64) (two 32-row
 // MFMA tiles; row = kh*32 + kw*4 + ci), K' = 100 positions.
 __global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
+  DQZ_STAMP(8, 0);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                 // 8064
   float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
@@ -193,6 +198,7 @@ __global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
       part[(kh * 32 + row) * C1CO + i] = acc[r];
     }
   }
+  DQZ_STAMP(8, 3);
 }
 
 constexpr size_t kConv1FwdSmem = (C1_IN_FLOATS + C1KK * C1CO) * sizeof(float);

@@ -41,11 +41,13 @@ struct LayerFwdArgs {
 constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
 
 __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
+  DQZ_STAMP(1, 0);
   __shared__ float s_in[C2L_WIN];
   const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
   const int n = lane & 15, kq = lane >> 4;
   const float* W = a.nz.p[z] + a.w_off;  // [512][64], k = kh*128 + kw*32 + ci
+  const float bv = a.nz.p[z][a.b_off + 16 * nq + (t & 15)];  // epilogue bias, loaded early
   float wr[32];
 #pragma unroll
   for (int kk = 0; kk < 32; ++kk) wr[kk] = W[(w * 128 + 4 * kk + kq) * C2CO + 16 * nq + n];
@@ -66,6 +68,7 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
       d[3] = r[q].w;
     }
   }
+  DQZ_STAMP(1, 1);
   __syncthreads();
   int base[6];
 #pragma unroll
@@ -82,6 +85,7 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
 #pragma unroll
     for (int m = 0; m < 6; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
   }
+  DQZ_STAMP(1, 2);
   __syncthreads();
   float* s_red = s_in;  // [4][96][16]
 #pragma unroll
@@ -89,12 +93,12 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1536 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
-  const float* bias = a.nz.p[z] + a.b_off + 16 * nq;
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   for (int i = t; i < C2M * 16; i += 256) {
-    const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bias[i & 15];
+    const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bv;
     out[(i >> 4) * C2CO + (i & 15)] = a.linear ? v : relu(v);
   }
+  DQZ_STAMP(1, 3);
 }
 
 // ---- conv3: 9x9x64 -> 7x7x64, 3x3 stride 1 ---------------------------------
@@ -103,11 +107,13 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
 constexpr int C3L_S = 66, C3L_RS = 622, C3L_WIN = 9 * C3L_RS;  // 5598 floats
 
 __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
+  DQZ_STAMP(2, 0);
   __shared__ float s_in[C3L_WIN];
   const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const float* W = a.nz.p[z] + a.w_off;  // [576][64], k = (kh*3 + kw)*64 + ci
+  const float bv = a.nz.p[z][a.b_off + 16 * nq + (t & 15)];  // epilogue bias, loaded early
   float wr[36];
 #pragma unroll
   for (int kk = 0; kk < 36; ++kk)
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
       d[3] = r[q].w;
     }
   }
+  DQZ_STAMP(2, 1);
   __syncthreads();
   int base[4];
 #pragma unroll
@@ -146,6 +153,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
   }
+  DQZ_STAMP(2, 2);
   __syncthreads();
   float* s_red = s_in;  // [4][64][16]
 #pragma unroll
@@ -153,12 +161,12 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1024 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
-  const float* bias = a.nz.p[z] + a.b_off + 16 * nq;
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
   for (int i = t; i < C3M * 16; i += 256) {
-    const float v = ((s_red[i] + s_red[1024 + i]) + (s_red[2048 + i] + s_red[3072 + i])) + bias[i & 15];
+    const float v = ((s_red[i] + s_red[1024 + i]) + (s_red[2048 + i] + s_red[3072 + i])) + bv;
     out[(i >> 4) * C3CO + (i & 15)] = a.linear ? v : relu(v);
   }
+  DQZ_STAMP(2, 3);
 }
 
 // ---- fc1: [B][3136] x [3136][512] split-K partials ------------------------
@@ -177,6 +185,7 @@ struct Fc1FwdArgs {
 };
 
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
+  DQZ_STAMP(3, 0);
   __shared__ float s_red[4][2][256];
   const int nt = blockIdx.x, s = blockIdx.y, z = blockIdx.z / a.MG, mg = blockIdx.z % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -212,6 +221,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w][mt][(4 * kq + rr) * 16 + n] = acc[mt][rr];
+  DQZ_STAMP(3, 2);
   __syncthreads();
   // 512 outputs (32 rows x 16 cols), 2 per thread
 #pragma unroll
@@ -220,6 +230,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
     const float v = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
     if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
   }
+  DQZ_STAMP(3, 3);
 }
 
 }  // namespace dqz

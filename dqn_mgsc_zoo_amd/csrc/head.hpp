@@ -35,14 +35,18 @@ struct HeadArgs {
 //   the cotangent at td is clip(w td / B, +-bound) because rlax.clip_gradient
 //   clips the incoming gradient; dq[b, a_b] = -that; dz1 = dq W2[:, a_b] relu'.
 // Cross-sample sums (fc2/fc1-bias grads, mean loss) happen in update_kernel.
+template <int AMAX, int SMAX>
 __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
-  __shared__ float s_red[8][MAXA];
-  __shared__ float s_q[3][MAXA];
+  DQZ_STAMP(4, 0);
+  __shared__ float s_red[8][3 * AMAX];
+  __shared__ float s_q[3][AMAX];
   __shared__ float s_g;
   __shared__ int s_a;
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = n >> 6;
-  const int A = h.A, B = h.B;
-  // Issue the per-sample batch loads early (their latency overlaps the fc1 sums).
+  const int A = h.A, B = h.B, Z = h.Z, S = h.S;
+  // Every global load is issued up front: the batch record chain
+  // (slot -> action/reward/discount), the Z x S fc1 partials, fc1 biases and
+  // the W2 rows; nothing below waits on more than one round trip.
   int a_tm1 = 0;
   float r = 0.f, d = 0.f, w = 1.f, pm = 0.f;
   if (!h.fwd_only && n == 0) {
@@ -53,38 +57,50 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
     if (h.weights) w = h.weights[b];
     if (h.meta_p) pm = h.meta_p[b];
   }
+  float pv[3][SMAX], b1v[3], w2v[3][AMAX];
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+    const int zc = min(z, Z - 1);
+    const float* part = h.fc1p + ((int64_t)zc * S * B + b) * HID + n;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) pv[z][s] = part[(int64_t)min(s, S - 1) * B * HID];
+    b1v[z] = h.nz.p[zc][h.b1_off + n];
+    const float* w2 = h.nz.p[zc] + h.w2_off + n * A;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) w2v[z][a] = w2[min(a, A - 1)];
+  }
   float h0 = 0.f;
-  for (int z = 0; z < h.Z; ++z) {
-    const float* part = h.fc1p + ((int64_t)z * h.S * B + b) * HID + n;
-    float acc0 = h.nz.p[z][h.b1_off + n], acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    int s = 0;
-    for (; s + 4 <= h.S; s += 4) {
-      acc0 += part[(int64_t)(s + 0) * B * HID];
-      acc1 += part[(int64_t)(s + 1) * B * HID];
-      acc2 += part[(int64_t)(s + 2) * B * HID];
-      acc3 += part[(int64_t)(s + 3) * B * HID];
+  DQZ_STAMP(4, 1);
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+    if (z < Z) {
+      float acc = b1v[z];
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) acc += s < S ? pv[z][s] : 0.f;
+      const float hv = relu(acc);
+      h.h1[((int64_t)z * B + b) * HID + n] = hv;
+      if (z == 0) h0 = hv;
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a) {
+        const float sa = wave_sum(hv * w2v[z][a]);
+        if (lane == 0) s_red[wave][z * AMAX + a] = sa;
+      }
     }
-    for (; s < h.S; ++s) acc0 += part[(int64_t)s * B * HID];
-    const float hv = relu((acc0 + acc1) + (acc2 + acc3));
-    h.h1[((int64_t)z * B + b) * HID + n] = hv;
-    if (z == 0) h0 = hv;
-    const float* w2 = h.nz.p[z] + h.w2_off + n * A;
-    for (int a = 0; a < A; ++a) {
-      const float sa = wave_sum(hv * w2[a]);
-      if (lane == 0) s_red[wave][a] = sa;
-    }
-    __syncthreads();
-    if (n < A) {
+  }
+  __syncthreads();
+  if (n < 3 * AMAX) {
+    const int z = n / AMAX, a = n % AMAX;
+    if (z < Z && a < A) {
       float sa = 0.f;
 #pragma unroll
       for (int ww = 0; ww < 8; ++ww) sa += s_red[ww][n];
-      const float qv = sa + h.nz.p[z][h.b2_off + (h.shared_bias ? 0 : n)];
-      s_q[z][n] = qv;
-      h.q[((int64_t)z * B + b) * A + n] = qv;
+      const float qv = sa + h.nz.p[z][h.b2_off + (h.shared_bias ? 0 : a)];
+      s_q[z][a] = qv;
+      h.q[((int64_t)z * B + b) * A + a] = qv;
     }
-    __syncthreads();
   }
   if (h.fwd_only) return;
+  __syncthreads();
   if (n == 0) {
     float v;
     if (h.algo == DQZ_ALGO_DQN) {
@@ -114,8 +130,22 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
     s_a = a_tm1;
   }
   __syncthreads();
-  const float wv = h.nz.p[0][h.w2_off + n * A + s_a];
+  float wv = w2v[0][0];
+#pragma unroll
+  for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
+  DQZ_STAMP(4, 2);
   h.dz1[(int64_t)b * HID + n] = h0 > 0.f ? s_g * wv : 0.f;
+  DQZ_STAMP(4, 3);
+}
+
+// Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.
+inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
+  if (h.S > 7) return hipErrorInvalidValue;
+  if (h.A <= 8)
+    hipLaunchKernelGGL((head_kernel<8, 7>), dim3(grid), dim3(HID), 0, st, h);
+  else
+    hipLaunchKernelGGL((head_kernel<MAXA, 7>), dim3(grid), dim3(HID), 0, st, h);
+  return hipGetLastError();
 }
 
 struct UpdArgs {
@@ -136,25 +166,31 @@ struct UpdArgs {
   Rms rms;
 };
 
-constexpr int UPD_PARAMS = 64;  // parameters per workgroup
-constexpr int UPD_GROUPS = 4;   // threads sharing one parameter's reduction
+constexpr int UPD_PARAMS = 32;  // parameters per workgroup
+constexpr int UPD_GROUPS = 8;   // threads sharing one parameter's reduction
 
-// Sum of p[s * stride + i] over s = g, g + G, g + 2G, ... < S.
+// Sum of p[s * stride + i] over s = g, g + G, g + 2G, ... < S, eight loads in
+// flight per iteration (the slabs are written by the previous kernel, so every
+// load is a cache miss; one dependent chain per slab would be latency-bound).
 __device__ __forceinline__ float sum_split(const float* p, int S, int64_t stride, int64_t i, int g) {
-  float a0 = 0.f, a1 = 0.f;
+  constexpr int G = UPD_GROUPS;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int s = g;
-  for (; s + UPD_GROUPS < S; s += 2 * UPD_GROUPS) {
-    a0 += p[s * stride + i];
-    a1 += p[(s + UPD_GROUPS) * stride + i];
+  for (; s + 7 * G < S; s += 8 * G) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[(int64_t)(s + u * G) * stride + i];
   }
-  if (s < S) a0 += p[s * stride + i];
-  return a0 + a1;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (s + u * G < S) a[u] += p[(int64_t)(s + u * G) * stride + i];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // Reduces every gradient that crosses samples or split-K chunks and applies
 // centered RMSProp to every leaf except fc1/w (fused into its dW epilogue).
-// 256 threads = 64 parameters x 4 reduction groups, combined through LDS.
+// 256 threads = 32 parameters x 8 reduction groups, combined through LDS.
 __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
+  DQZ_STAMP(9, 0);
   __shared__ float s_part[UPD_GROUPS][UPD_PARAMS];
   const int pl = threadIdx.x % UPD_PARAMS, grp = threadIdx.x / UPD_PARAMS;
   const int64_t i = (int64_t)blockIdx.x * UPD_PARAMS + pl;
@@ -197,13 +233,16 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
   s_part[grp][pl] = g;
   __syncthreads();
   if (grp == 0 && dst >= 0) {
-    const float gs = (s_part[0][pl] + s_part[1][pl]) + (s_part[2][pl] + s_part[3][pl]);
+    const float gs = ((s_part[0][pl] + s_part[1][pl]) + (s_part[2][pl] + s_part[3][pl])) +
+                     ((s_part[4][pl] + s_part[5][pl]) + (s_part[6][pl] + s_part[7][pl]));
     u.rms.apply(u.th, u.mu, u.nu, dst, gs);
   }
+  DQZ_STAMP(9, 3);
 }
 
 __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
                                       uint64_t* counter, int32_t* out) {
+  DQZ_STAMP(10, 0);
   const uint64_t ctr = *counter;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x5EED5u),
@@ -214,6 +253,7 @@ __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capaci
   }
   __syncthreads();
   if (threadIdx.x == 0) *counter = ctr + 1;
+  DQZ_STAMP(10, 3);
 }
 
 __global__ void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx, const int32_t* slots, int n,

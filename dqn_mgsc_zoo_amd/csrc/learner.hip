@@ -274,7 +274,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   param_layout(cfg->num_actions, L->shared_bias, L->off, L->sz, &L->total);
   const int B = cfg->batch, Z = L->Z, A = cfg->num_actions;
   L->S_fc1 = FC1_S;
-  L->S2 = make_shape<CfgBwd3>(1, C2KK + 1, C2CO, B * C2M, std::max(1, (B * C2M + 287) / 288)).g.S;
+  L->S2 = B;  // per-sample conv2 dW partials (conv2_bwd_kernel)
   L->S3 = B;  // per-sample conv3 dW partials (conv3_bwd_kernel)
   const int64_t n_y1 = (int64_t)Z * B * C1M * C1CO, n_y2 = (int64_t)Z * B * C2M * C2CO, n_y3 = (int64_t)Z * B * FLAT;
   const int64_t n_fc1p = (int64_t)Z * L->S_fc1 * B * HID, n_h1 = (int64_t)Z * B * HID, n_q = (int64_t)Z * B * A;
@@ -442,8 +442,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.gq = L->gq;
   h.ga = L->ga;
   h.dz1 = L->dz1;
-  hipLaunchKernelGGL(head_kernel, dim3(B), dim3(HID), 0, st, h);
-  DQZ_HIP(hipGetLastError());
+  DQZ_HIP(launch_head(h, B, st));
   pe.mark(5, st);
 
   Fc1BwdArgs fb;
@@ -471,18 +470,15 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   DQZ_HIP(hipGetLastError());
   pe.mark(7, st);
 
-  Conv2DxPhased c2dx;
-  static_cast<Shape&>(c2dx) = make_shape<CfgBwd3>(4, B * 100, C2CI, 4 * C2CO, 1);
-  c2dx.dy2 = L->dy2;
-  c2dx.w2 = P->online + L->off[2];
-  c2dx.y1 = L->y1;
-  c2dx.dy1 = L->dy1;
-  Conv2Dw c2dw;
-  static_cast<Shape&>(c2dw) = make_shape<CfgBwd3>(1, C2KK + 1, C2CO, B * C2M, L->S2);
-  c2dw.in = L->y1;
-  c2dw.dy = L->dy2;
-  c2dw.part = L->p2;
-  DQZ_HIP((launch_gemm<CfgBwd3>(st, c2dx, c2dw)));
+  Conv2BwdArgs c2b;
+  c2b.dy2 = L->dy2;
+  c2b.y1 = L->y1;
+  c2b.w2 = P->online + L->off[2];
+  c2b.dy1 = L->dy1;
+  c2b.part = L->p2;
+  c2b.B = B;
+  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(12, B), dim3(256), 0, st, c2b);
+  DQZ_HIP(hipGetLastError());
   pe.mark(8, st);
 
   Conv1DwArgs c1dw;
@@ -506,7 +502,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.p2 = L->p2;
   u.p3 = L->p3;
   u.S1 = B * C1_BLOCKS;
-  u.S2 = c2dw.g.S;
+  u.S2 = B;
   u.S3 = B;
   u.h1 = L->h1;
   u.dz1 = L->dz1;
@@ -579,7 +575,7 @@ static int forward_q(dqz_learner* L, const float* params, const Conv1Src& src, i
   HeadArgs h = make_head(L, nz, 1, n);
   h.fwd_only = 1;
   h.q = q_out;
-  hipLaunchKernelGGL(head_kernel, dim3(n), dim3(HID), 0, st, h);
+  DQZ_HIP(launch_head(h, n, st));
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -986,3 +982,19 @@ int dqz_meta_outputs(dqz_meta* H, float* probs, float* dlogits, float* td, float
 }
 
 }  // extern "C"
+
+#ifdef DQZ_TRACE
+// Diagnostic builds only (not part of include/dqz.h): copy / clear the
+// in-kernel timeline stamps (common.hpp DQZ_STAMP).
+extern "C" int dqz_debug_trace(unsigned long long* host_out, int clear) {
+  const size_t bytes = sizeof(unsigned long long) * TRACE_KERNELS * TRACE_BLOCKS * TRACE_SLOTS;
+  if (host_out) DQZ_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dqz_trace), bytes));
+  if (clear) {
+    void* p = nullptr;
+    DQZ_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_dqz_trace)));
+    DQZ_HIP(hipMemset(p, 0, bytes));
+  }
+  return DQZ_OK;
+}
+#endif
+

@@ -77,7 +77,7 @@ class Learner:
 
   def __del__(self):
     h = getattr(self, '_h', None)
-    if h is not None and h.value and _native._lib is not None:  # pylint: disable=protected-access
+    if h is not None and h.value and _native is not None and _native._lib is not None:  # pylint: disable=protected-access
       _native.lib().dqz_learner_destroy(h)
       self._h = None
 
@@ -259,7 +259,7 @@ class MetaLearner:
 
   def __del__(self):
     h = getattr(self, '_h', None)
-    if h is not None and h.value and _native._lib is not None:  # pylint: disable=protected-access
+    if h is not None and h.value and _native is not None and _native._lib is not None:  # pylint: disable=protected-access
       _native.lib().dqz_meta_destroy(h)
       self._h = None
 

@@ -1,0 +1,85 @@
+"""Per-kernel timeline of one learner step from in-kernel s_memrealtime stamps.
+
+usage (GPU box): python tools/trace_step.py   (builds libdqz_trace.so first)
+Prints, per kernel in launch order: first-block start relative to the previous
+kernel's last-block end (the boundary), kernel span, median block lifetime and
+the median of the named intervals between stamps (10 ns ticks -> us).
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')
+subprocess.check_call(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC',
+                       '-DDQZ_TRACE', '-I' + os.path.join(ROOT, 'include'), '-o', LIB,
+                       os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'csrc', 'learner.hip')])
+os.environ['DQZ_LIB'] = LIB
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
+
+NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_bwd',
+         6: 'conv3_bwd', 7: 'conv2_bwd', 8: 'conv1_dw', 9: 'update'}
+ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9]
+K, NB, NS = 16, 1024, 4
+
+dev = torch.device('cuda:0')
+net = networks.dqn_atari_network(6)
+lrn = learner_lib.Learner(net, 32, algo='dqn', device=dev)
+lrn.set_params(net.init(0))
+cap = int(os.environ.get('CAP', '200000'))
+store = synthetic.fill_episodic(cap, 6, seed=0, device=dev)
+slots = torch.zeros((32,), dtype=torch.int32, device=dev)
+counter = torch.zeros((1,), dtype=torch.int64, device=dev)
+
+
+def step():
+  learner_lib.sample_uniform(0, cap, cap, 32, 1, counter, slots)
+  lrn.step(store, slots)
+
+
+lib = _native.lib()
+fn = lib.dqz_debug_trace
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros(K * NB * NS, np.uint64)
+side = torch.cuda.Stream(dev)
+side.wait_stream(torch.cuda.current_stream(dev))
+with torch.cuda.stream(side):
+  for _ in range(3):
+    step()
+torch.cuda.current_stream(dev).wait_stream(side)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+  for _ in range(20):
+    step()
+for _ in range(5):
+  g.replay()
+torch.cuda.synchronize()
+fn(None, 1)
+g.replay()
+torch.cuda.synchronize()
+fn(buf.ctypes.data, 0)
+t = buf.reshape(K, NB, NS).astype(np.int64)
+prev_end = None
+print('%-10s %8s %8s %8s | %8s %8s %8s %8s  (us; 100 MHz ticks)' % (
+    'kernel', 'gap', 'span', 'blk_med', 's0-s1', 's1-s2', 's2-s3', 'nblk'))
+for k in ORDER:
+  s0 = t[k, :, 0]
+  live = s0 > 0
+  if not live.any():
+    continue
+  s0 = s0[live]
+  s3 = t[k, live, 3]
+  start, end = s0.min(), s3.max()
+  gap = (start - prev_end) / 100 if prev_end is not None else 0
+  def med(a, b):
+    x = t[k, live, b] - t[k, live, a]
+    ok = (t[k, live, a] > 0) & (t[k, live, b] > 0)
+    return np.median(x[ok]) / 100 if ok.any() else float('nan')
+  print('%-10s %8.2f %8.2f %8.2f | %8.2f %8.2f %8.2f %8d' % (
+      NAMES[k], gap, (end - start) / 100, np.median(s3 - s0) / 100, med(0, 1), med(1, 2), med(2, 3), live.sum()))
+  prev_end = end
