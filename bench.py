@@ -131,10 +131,10 @@ def main():
   seed = 1 + rank
 
   def one_step():
-    # FIFO replay full: live ids [t - size, t) = slots [0, capacity).
-    learner_lib.sample_uniform(0, args.capacity, args.capacity, BATCH, seed,
-                               counter, slots)
-    lrn.step(store, slots)
+    # FIFO replay full: live ids [t - size, t) = slots [0, capacity).  The
+    # uniform draw is fused into the step's conv1 kernel.
+    lrn.step_uniform(store, 0, args.capacity, args.capacity, seed, counter,
+                     slots)
 
   g = args.graph_steps if args.graph else 1
   graph = None

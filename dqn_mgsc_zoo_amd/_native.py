@@ -98,6 +98,11 @@ SIGNATURES = {
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
          _vp],
     ),
+    'dqz_learner_step_uniform': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _i64, _i64,
+         _i64, ctypes.c_uint64, _vp, _vp, _vp],
+    ),
     'dqz_learner_grad': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,

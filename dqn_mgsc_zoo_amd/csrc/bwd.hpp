@@ -26,99 +26,132 @@ struct Fc1BwdArgs {
   float* dy3;  // [B][3136]
 };
 
+constexpr int FC1B_LD = 528;  // LDS row stride of the dz1 chunk: 528 = 16 (mod 32) banks apart
+
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
   DQZ_STAMP(5, 0);
+  __shared__ __attribute__((aligned(16))) float s_dz[32 * FC1B_LD];  // dz1 chunk, later the dW block
   __shared__ float s_red[4][2][256];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = 16 * blockIdx.x;
   const float* W1 = a.th + a.w_off;
-  float4 wv[8];  // W1[k0 + n][128 w + 16 j + 4 kq + e]
+  float4 wv[8];  // dX B operand: W1[k0 + n][128 w + 16 j + 4 kq + e]
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
-  // The RMSProp operands of this lane's 32 dW entries, loaded up front so
-  // their latency hides under the GEMMs.  Entry (q, r): row k0 + 4 kq + r,
-  // column 128 w + 16 q + n (the C layout of the dW tiles).
-  const int64_t e0 = a.w_off + (int64_t)(k0 + 4 * kq) * HID + 128 * w + n;
-  float o_th[32], o_mu[32], o_nu[32];
-  if (!a.rms.gout) {
+  // RMSProp operands of this thread's 32 parameters of the 16 x 512 block, as
+  // float4 f = t + 256 i: row f / 128, columns 4 (f % 128) .. +3.
+  const bool upd = a.rms.gout == nullptr;
+  float4 o_th[8], o_mu[8], o_nu[8];
+  if (upd) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t i = e0 + r * HID + 16 * q;
-        o_th[4 * q + r] = a.th[i];
-        o_mu[4 * q + r] = a.mu[i];
-        o_nu[4 * q + r] = a.nu[i];
-      }
+    for (int i = 0; i < 8; ++i) {
+      const int f = t + 256 * i;
+      const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
+      o_th[i] = *reinterpret_cast<const float4*>(a.th + e);
+      o_mu[i] = *reinterpret_cast<const float4*>(a.mu + e);
+      o_nu[i] = *reinterpret_cast<const float4*>(a.nu + e);
+    }
   }
   f32x4 gacc[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) gacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int c = 0; c < a.B; c += 32) {
-    // dX rows of samples [c, c + 32)
-    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    // stage dz1 rows [c, c + 32) (rows past B are zero)
+    {
+      float4 v[16];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int row = min(c + 16 * mt + n, a.B - 1);
-      const float* d = a.dz1 + (int64_t)row * HID + 128 * w + 4 * kq;
-      float4 av[8];
+      for (int i = 0; i < 16; ++i) {
+        const int f = t + 256 * i, row = f >> 7;
+        const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + 4 * (f & 127));
+        v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      float ym[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) av[j] = *reinterpret_cast<const float4*>(d + 16 * j);
+      for (int h = 0; h < 2; ++h)
+        ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
+      float yv[8];  // dW A operand: y3[c + 4 kk + kq][k0 + n]
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xacc[mt] = mfma4(av[j].x, wv[j].x, xacc[mt]);
-        xacc[mt] = mfma4(av[j].y, wv[j].y, xacc[mt]);
-        xacc[mt] = mfma4(av[j].z, wv[j].z, xacc[mt]);
-        xacc[mt] = mfma4(av[j].w, wv[j].w, xacc[mt]);
+      for (int kk = 0; kk < 8; ++kk) {
+        const int bb = c + 4 * kk + kq;
+        const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
+        yv[kk] = bb < a.B ? y : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int f = t + 256 * i;
+        *reinterpret_cast<float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127)) = v[i];
+      }
+      __syncthreads();
+      // dX: rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
+      f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const float* d = s_dz + (16 * mt + n) * FC1B_LD + 128 * w + 4 * kq;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
+          xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
+          xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
+          xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
+          xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
+        }
+      }
+      // dW over the chunk: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const float* d = s_dz + (4 * kk + kq) * FC1B_LD + 128 * w + n;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) gacc[q] = mfma4(yv[kk], d[16 * q], gacc[q]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s_red[w][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int sample = c + 16 * h + (t >> 4);
+        const float v2 = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
+        if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
       }
     }
-    // dW over the chunk's samples: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int b = c + 4 * kk + kq;
-      const int bb = min(b, a.B - 1);
-      const float yv = a.y3[(int64_t)bb * FLAT + k0 + n];
-      const float av = b < a.B ? yv : 0.f;
-      const float* d = a.dz1 + (int64_t)bb * HID + 128 * w + n;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) gacc[q] = mfma4(av, d[16 * q], gacc[q]);
-    }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s_red[w][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int sample = c + 16 * h + (t >> 4);
-      const float v = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
-      if (sample < a.B) {
-        const int64_t i = (int64_t)sample * FLAT + k0 + (t & 15);
-        a.dy3[i] = a.y3[i] > 0.f ? v : 0.f;
-      }
-    }
-    __syncthreads();
   }
   DQZ_STAMP(5, 2);
-  const Rms& R = a.rms;
+  // dW block through LDS into the float4 layout of the RMSProp operands.
+  __syncthreads();
 #pragma unroll
   for (int q = 0; q < 8; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t i = e0 + r * HID + 16 * q;
-      const float g = gacc[q][r];
-      if (R.gout) {
-        R.gout[i] = g;
-      } else {
-        const float m = R.c1 * g + R.decay * o_mu[4 * q + r];
-        const float v = R.c1 * (g * g) + R.decay * o_nu[4 * q + r];
-        a.mu[i] = m;
-        a.nu[i] = v;
-        a.th[i] = o_th[4 * q + r] + (-R.lr) * (g * rsqrtf(v - m * m + R.eps));
-      }
+    for (int r = 0; r < 4; ++r) s_dz[(4 * kq + r) * FC1B_LD + 128 * w + 16 * q + n] = gacc[q][r];
+  __syncthreads();
+  const Rms& R = a.rms;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = t + 256 * i;
+    const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
+    const float4 g = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127));
+    if (!upd) {
+      *reinterpret_cast<float4*>(R.gout + e) = g;
+    } else {
+      float4 th4 = o_th[i], mu4 = o_mu[i], nu4 = o_nu[i];
+      auto one = [&](float gg, float& th, float& mu, float& nu) {
+        const float m = R.c1 * gg + R.decay * mu;
+        const float v = R.c1 * (gg * gg) + R.decay * nu;
+        mu = m;
+        nu = v;
+        th = th + (-R.lr) * (gg * rsqrtf(v - m * m + R.eps));
+      };
+      one(g.x, th4.x, mu4.x, nu4.x);
+      one(g.y, th4.y, mu4.y, nu4.y);
+      one(g.z, th4.z, mu4.z, nu4.z);
+      one(g.w, th4.w, mu4.w, nu4.w);
+      *reinterpret_cast<float4*>(a.th + e) = th4;
+      *reinterpret_cast<float4*>(a.mu + e) = mu4;
+      *reinterpret_cast<float4*>(a.nu + e) = nu4;
     }
+  }
   DQZ_STAMP(5, 3);
 }
 
@@ -150,6 +183,13 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
   for (int kk = 0; kk < 36; ++kk) {
     const int tap = 8 - (kk >> 2);  // (2 - kh')*3 + (2 - kw')
     wr[kk] = a.w3[(tap * C3CI + 16 * nq + n) * C3CO + 16 * w + 4 * (kk & 3) + kq];
+  }
+  float ym[3];  // relu'(y2) operands of the epilogue, loaded early
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = t + 256 * k;
+    const int p = min(48 * mh + (i >> 4), C2M - 1);
+    ym[k] = a.y2[((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15)];
   }
   // padded dy3 window: (ph, pw) in 11 x 11, interior [2, 9)
   const float4* src = reinterpret_cast<const float4*>(a.dy3 + (int64_t)b * FLAT);
@@ -199,12 +239,13 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 768 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
-  for (int i = t; i < 768; i += 256) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = t + 256 * k;
     const int p = 48 * mh + (i >> 4);
     if (p < C2M) {
       const float v = (s_red[i] + s_red[768 + i]) + (s_red[1536 + i] + s_red[2304 + i]);
-      const int64_t o = ((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15);
-      a.dy2[o] = a.y2[o] > 0.f ? v : 0.f;
+      a.dy2[((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15)] = ym[k] > 0.f ? v : 0.f;
     }
   }
 }
@@ -270,7 +311,9 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
 __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
   DQZ_STAMP(6, 0);
   __shared__ float s_win[C3X_WIN];
-  const int job = blockIdx.x, b = blockIdx.y;
+  const SampleJob sj = xcd_sample_job(12, a.B);
+  if (!sj.valid) return;
+  const int job = sj.job, b = sj.s;
   if (job < 8)
     conv3_bwd_dx(a, s_win, b, job & 3, job >> 2);
   else
@@ -307,6 +350,12 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     const int tp = kk >> 2, u = tp >> 1, v = tp & 1;
     const int kh = ph + 2 * (1 - u), kw = pw + 2 * (1 - v);
     wr[kk] = a.w2[((kh * C2K + kw) * C2CI + 16 * hh + n) * C2CO + 16 * w + 4 * (kk & 3) + kq];
+  }
+  float ym[7];  // relu'(y1) operands of the epilogue, loaded early
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int p = min((t + 256 * k) >> 4, 99), ah = p / 10, cw = p % 10;
+    ym[k] = a.y1[((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (t & 15)];
   }
   const float4* src = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * (C2M * C2CO));
   constexpr int NW4 = 121 * 16;  // 1936
@@ -355,11 +404,15 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
-  for (int i = t; i < 1600; i += 256) {
-    const int p = i >> 4, ah = p / 10, cw = p % 10;
-    const float v = (s_red[i] + s_red[1792 + i]) + (s_red[3584 + i] + s_red[5376 + i]);
-    const int64_t o = ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15);
-    a.dy1[o] = a.y1[o] > 0.f ? v : 0.f;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int i = t + 256 * k;
+    if (i < 1600) {
+      const int p = i >> 4, ah = p / 10, cw = p % 10;
+      const float v = (s_red[i] + s_red[1792 + i]) + (s_red[3584 + i] + s_red[5376 + i]);
+      a.dy1[((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15)] =
+          ym[k] > 0.f ? v : 0.f;
+    }
   }
 }
 
@@ -422,7 +475,9 @@ __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win
 __global__ __launch_bounds__(256) void conv2_bwd_kernel(Conv2BwdArgs a) {
   DQZ_STAMP(7, 0);
   __shared__ float s_win[C2W_WIN];
-  const int job = blockIdx.x, b = blockIdx.y;
+  const SampleJob sj = xcd_sample_job(12, a.B);
+  if (!sj.valid) return;
+  const int job = sj.job, b = sj.s;
   if (job < 8)
     conv2_bwd_dx(a, s_win, b, (job & 3) >> 1, job & 1, job >> 2);
   else

@@ -141,4 +141,40 @@ __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
   return c;
 }
 
+// XCD-aware decode of a 1-D grid for per-sample kernels.  Workgroups are
+// dispatched round-robin over the 8 XCDs (block i -> XCD i % 8), each with its
+// own L2.  Sending every job of sample s to XCD s % 8 in every kernel keeps a
+// sample's activations in one L2 from the kernel that writes them to the
+// kernel that reads them.  Grid = J * ceil8(nsamp) blocks; padding blocks exit.
+struct SampleJob {
+  int s, job;
+  bool valid;
+};
+
+__device__ __forceinline__ SampleJob xcd_sample_job(int J, int nsamp) {
+  const int i = blockIdx.x, x = i & 7, slot = i >> 3;
+  const int s = 8 * (slot / J) + x;
+  return SampleJob{s, slot % J, s < nsamp};
+}
+
+inline dim3 xcd_grid(int J, int nsamp) { return dim3((unsigned)(J * ((nsamp + 7) / 8) * 8)); }
+
+// Uniform replay draw of the device sampler (replay.py:119-125 distribution):
+// draw i of step `ctr` -> live slot (base + floor(u * size)) mod capacity,
+// u from Philox(counter = (ctr, i), key = seed).
+struct UniformDraw {
+  int64_t base, size, capacity;
+  uint64_t seed;
+  uint64_t* counter;  // device step counter (read by the sampling kernel, advanced later)
+  int32_t* slots_out;
+};
+
+__device__ __forceinline__ int32_t uniform_slot(uint64_t ctr, int i, const UniformDraw& d) {
+  const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x5EED5u),
+                             make_uint2((unsigned)d.seed, (unsigned)(d.seed >> 32)));
+  const uint64_t u = ((uint64_t)r.x << 32) | r.y;
+  const int64_t j = (int64_t)__umul64hi(u, (uint64_t)d.size);  // uniform in [0, size)
+  return (int32_t)((d.base + j) % d.capacity);
+}
+
 }  // namespace dqz

@@ -19,6 +19,8 @@ struct Conv1Src {
   const int32_t* fidx;    // [capacity][8]
   const int32_t* slots;   // [B]
   const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
+  int fused;              // 1: slots come from the fused uniform sampler `draw`
+  UniformDraw draw;
 };
 
 __device__ __forceinline__ void store_bytes_as_f32(float* dst, uint4 v) {
@@ -36,7 +38,8 @@ __device__ __forceinline__ void store_bytes_as_f32(float* dst, uint4 v) {
 
 // Stages input rows [20*rb, 20*rb + 24) of sample b, stack `which`, as
 // s_in[ci][row][col] = pixel / 255.
-__device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& src, int b, int which, int rb) {
+__device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& src, int b, int which, int rb,
+                                                  int z = 0) {
   const int row0 = rb * C1S * C1_ROWS;
   constexpr int QPC = C1_PLANE / 16;  // 126 16-byte pieces per channel
   if (src.states) {
@@ -58,7 +61,13 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
   } else {
     // slot -> 4 frame ids -> 504 16-byte pieces (2 per thread), all loads in
     // flight before the first LDS store.
-    const int slot = src.slots[b];
+    int slot;
+    if (src.fused) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
+      slot = uniform_slot(*src.draw.counter, b, src.draw);
+      if (threadIdx.x == 0 && rb == 0 && z == 0) src.draw.slots_out[b] = slot;
+    } else {
+      slot = src.slots[b];
+    }
     const int32_t* fr = src.fidx + (int64_t)slot * 8 + which * 4;
     const int f0 = fr[0], f1 = fr[1], f2 = fr[2], f3 = fr[3];
     constexpr int NP = FC * QPC;  // 504
@@ -90,7 +99,7 @@ struct Conv1FwdArgs {
   Conv1Src src;
   NetZ nz;
   int64_t w_off, b_off;
-  int B;
+  int B, Z;
   int linear;  // 1: write the pre-activation (no ReLU)
   float* out;  // y1 [Z][B][400][32]
 };
@@ -102,13 +111,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                  // 8064
   float* s_w = smem + C1_IN_FLOATS;    // 256 x 32
-  const int rb = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.Z * a.B);
+  if (!sj.valid) return;
+  const int rb = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const float bias = a.nz.p[z][a.b_off + (threadIdx.x & 31)];  // epilogue operand, loaded early
   const float4* w4 = reinterpret_cast<const float4*>(a.nz.p[z] + a.w_off);
   float4 wv[8];  // 256 x 32 weights = 8 float4 per thread, issued together
 #pragma unroll
   for (int q = 0; q < 8; ++q) wv[q] = w4[threadIdx.x + 256 * q];
-  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb);
+  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb, z);
 #pragma unroll
   for (int q = 0; q < 8; ++q) reinterpret_cast<float4*>(s_w)[threadIdx.x + 256 * q] = wv[q];
   DQZ_STAMP(0, 1);
@@ -144,7 +155,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
 
 struct Conv1DwArgs {
   Conv1Src src;
-  int which;
+  int which, B;
   const float* dy1;  // [B][400][32] (online copy)
   float* part;       // [B*4][257][32]: dW rows 0..255 (HWIO order), db row 256
 };
@@ -157,7 +168,9 @@ __global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                 // 8064
   float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
-  const int rb = blockIdx.x, b = blockIdx.y;
+  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.B);
+  if (!sj.valid) return;
+  const int rb = sj.job, b = sj.s;
   const float4* dy4 = reinterpret_cast<const float4*>(a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO);
   constexpr int ND4 = C1_POS * C1CO / 4;  // 800
   float4 dv[4];

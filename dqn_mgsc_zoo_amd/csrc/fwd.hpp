@@ -30,7 +30,7 @@ struct LayerFwdArgs {
   const float* in;  // [Z][B][...] layer input (NHWC)
   NetZ nz;
   int64_t w_off, b_off;
-  int B;
+  int B, Z;
   int linear;  // 1: pre-activation output, no ReLU (tangent forward)
   float* out;  // [Z][B][...]
 };
@@ -43,7 +43,9 @@ constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
 __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
   DQZ_STAMP(1, 0);
   __shared__ float s_in[C2L_WIN];
-  const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
+  if (!sj.valid) return;
+  const int nq = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
   const int n = lane & 15, kq = lane >> 4;
   const float* W = a.nz.p[z] + a.w_off;  // [512][64], k = kh*128 + kw*32 + ci
@@ -109,7 +111,9 @@ constexpr int C3L_S = 66, C3L_RS = 622, C3L_WIN = 9 * C3L_RS;  // 5598 floats
 __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
   DQZ_STAMP(2, 0);
   __shared__ float s_in[C3L_WIN];
-  const int nq = blockIdx.x, b = blockIdx.y, z = blockIdx.z;
+  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
+  if (!sj.valid) return;
+  const int nq = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const float* W = a.nz.p[z] + a.w_off;  // [576][64], k = (kh*3 + kw)*64 + ci

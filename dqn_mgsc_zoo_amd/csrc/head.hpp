@@ -18,6 +18,7 @@ struct HeadArgs {
   const float* discount;
   const float* weights;  // PER importance weights or null
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
+  uint64_t* advance;     // fused sampler's step counter, advanced once here (or null)
   float bound;           // grad_error_bound
   float* q;              // [Z][B][A]
   float* td;             // [B]
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   // the W2 rows; nothing below waits on more than one round trip.
   int a_tm1 = 0;
   float r = 0.f, d = 0.f, w = 1.f, pm = 0.f;
+  if (h.advance && b == 0 && n == 0) *h.advance += 1;  // every conv1 block has read it
   if (!h.fwd_only && n == 0) {
     const int slot = h.slots[b];
     a_tm1 = h.action[slot];
@@ -233,8 +235,9 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
   s_part[grp][pl] = g;
   __syncthreads();
   if (grp == 0 && dst >= 0) {
-    const float gs = ((s_part[0][pl] + s_part[1][pl]) + (s_part[2][pl] + s_part[3][pl])) +
-                     ((s_part[4][pl] + s_part[5][pl]) + (s_part[6][pl] + s_part[7][pl]));
+    float gs = 0.f;
+#pragma unroll
+    for (int gi = 0; gi < UPD_GROUPS; ++gi) gs += s_part[gi][pl];
     u.rms.apply(u.th, u.mu, u.nu, dst, gs);
   }
   DQZ_STAMP(9, 3);
@@ -244,13 +247,8 @@ __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capaci
                                       uint64_t* counter, int32_t* out) {
   DQZ_STAMP(10, 0);
   const uint64_t ctr = *counter;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x5EED5u),
-                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-    const uint64_t u = ((uint64_t)r.x << 32) | r.y;
-    const int64_t j = (int64_t)__umul64hi(u, (uint64_t)size);  // uniform in [0, size)
-    out[i] = (int32_t)((base + j) % capacity);
-  }
+  const UniformDraw d{base, size, capacity, seed, counter, out};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = uniform_slot(ctr, i, d);
   __syncthreads();
   if (threadIdx.x == 0) *counter = ctr + 1;
   DQZ_STAMP(10, 3);

@@ -339,9 +339,10 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.w_off = L->off[0];
   c1.b_off = L->off[1];
   c1.B = B;
+  c1.Z = Z;
   c1.linear = 0;
   c1.out = L->y1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(C1_BLOCKS, B, Z), dim3(256), kConv1FwdSmem, st, c1);
+  hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
   DQZ_HIP(hipGetLastError());
   pe.mark(1, st);
 
@@ -351,9 +352,10 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
   c2.B = B;
+  c2.Z = Z;
   c2.linear = 0;
   c2.out = L->y2;
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(4, B, Z), dim3(256), 0, st, c2);
+  hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
   DQZ_HIP(hipGetLastError());
   pe.mark(2, st);
 
@@ -362,7 +364,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  hipLaunchKernelGGL(conv3_fwd_kernel, dim3(4, B, Z), dim3(256), 0, st, c3);
+  hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
   DQZ_HIP(hipGetLastError());
   pe.mark(3, st);
 
@@ -404,7 +406,7 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 // meta_p != null: per-sample cotangents p_b * (-clip(td_b)) (MGSC meta mode).
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
-                     const float* meta_p = nullptr) {
+                     const float* meta_p = nullptr, const UniformDraw* draw = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -418,8 +420,15 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   nz.which[0] = 0;
   nz.which[1] = 1;
   nz.which[2] = 1;
-  Conv1Src src{S->frames, S->fidx, slots, nullptr};
-  if (int rc = forward_impl(L, nz, Z, B, src, st, pe)) return rc;
+  Conv1Src src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
+  if (draw) {  // conv1 draws the batch itself; later kernels read the published slots
+    Conv1Src fsrc = src;
+    fsrc.fused = 1;
+    fsrc.draw = *draw;
+    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe)) return rc;
+  } else {
+    if (int rc = forward_impl(L, nz, Z, B, src, st, pe)) return rc;
+  }
 
   Rms rms;
   rms.lr = L->cfg.learning_rate;
@@ -436,6 +445,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.discount = S->discount;
   h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
   h.meta_p = meta_p;
+  h.advance = draw ? draw->counter : nullptr;
   h.bound = L->cfg.grad_error_bound;
   h.td = L->td;
   h.loss_part = L->loss_part;
@@ -466,7 +476,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
   c3b.B = B;
-  hipLaunchKernelGGL(conv3_bwd_kernel, dim3(12, B), dim3(256), 0, st, c3b);
+  hipLaunchKernelGGL(conv3_bwd_kernel, xcd_grid(12, B), dim3(256), 0, st, c3b);
   DQZ_HIP(hipGetLastError());
   pe.mark(7, st);
 
@@ -477,16 +487,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
   c2b.B = B;
-  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(12, B), dim3(256), 0, st, c2b);
+  hipLaunchKernelGGL(conv2_bwd_kernel, xcd_grid(12, B), dim3(256), 0, st, c2b);
   DQZ_HIP(hipGetLastError());
   pe.mark(8, st);
 
   Conv1DwArgs c1dw;
   c1dw.src = src;
   c1dw.which = 0;
+  c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  hipLaunchKernelGGL(conv1_dw_kernel, dim3(C1_BLOCKS, B), dim3(256), kConv1DwSmem, st, c1dw);
+  hipLaunchKernelGGL(conv1_dw_kernel, xcd_grid(C1_BLOCKS, B), dim3(256), kConv1DwSmem, st, c1dw);
   DQZ_HIP(hipGetLastError());
   pe.mark(9, st);
 
@@ -524,6 +535,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
 int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream) {
   return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr});
+}
+
+int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_store* S, int64_t base, int64_t size,
+                             int64_t capacity, uint64_t seed, uint64_t* counter_dev, int32_t* slots_out,
+                             void* stream) {
+  if (!counter_dev || !slots_out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (size < 1) return fail(DQZ_ERR_INVALID, "cannot sample from an empty replay (size=%lld)", (long long)size);
+  if (capacity < size || base < 0) return fail(DQZ_ERR_INVALID, "bad replay geometry");
+  if (L && L->cfg.algo == DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "PER samples by priority, not uniformly");
+  const UniformDraw d{base, size, capacity, seed, counter_dev, slots_out};
+  return step_impl(L, P, S, slots_out, nullptr, stream, PhaseEvents{nullptr}, nullptr, nullptr, &d);
 }
 
 int dqz_learner_grad(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
@@ -584,7 +606,7 @@ int dqz_forward(dqz_learner* L, const float* params, const uint8_t* states, int 
   if (!L || !params || !states || !q_out) return fail(DQZ_ERR_INVALID, "null argument");
   if (n < 1 || n > L->cfg.batch) return fail(DQZ_ERR_INVALID, "n must be in [1, %d]", L->cfg.batch);
   if (reinterpret_cast<uintptr_t>(states) % 16) return fail(DQZ_ERR_INVALID, "states must be 16-byte aligned");
-  Conv1Src src{nullptr, nullptr, nullptr, states};
+  Conv1Src src{nullptr, nullptr, nullptr, states, 0, UniformDraw{}};
   return forward_q(L, params, src, 0, n, q_out, (hipStream_t)stream);
 }
 
@@ -594,7 +616,7 @@ int dqz_forward_slots(dqz_learner* L, const float* params, const dqz_store* S, c
   if (int rc = check_store(S)) return rc;
   if (n < 1 || n > L->cfg.batch) return fail(DQZ_ERR_INVALID, "n must be in [1, %d]", L->cfg.batch);
   if (which != 0 && which != 1) return fail(DQZ_ERR_INVALID, "which must be 0 (s_tm1) or 1 (s_t)");
-  Conv1Src src{S->frames, S->fidx, slots, nullptr};
+  Conv1Src src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
   return forward_q(L, params, src, which, n, q_out, (hipStream_t)stream);
 }
 
@@ -888,14 +910,15 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   nv.p[0] = nv.p[1] = nv.p[2] = v;
   nv.which[0] = nv.which[1] = nv.which[2] = 0;
   Conv1FwdArgs c1;
-  c1.src = Conv1Src{S->frames, S->fidx, slots, nullptr};
+  c1.src = Conv1Src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
   c1.nz = nv;
   c1.w_off = L->off[0];
   c1.b_off = L->off[1];
   c1.B = M;
+  c1.Z = 1;
   c1.linear = 1;
   c1.out = H->zv1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(C1_BLOCKS, M, 1), dim3(256), kConv1FwdSmem, st, c1);
+  hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, M), dim3(256), kConv1FwdSmem, st, c1);
   DQZ_HIP(hipGetLastError());
   LayerFwdArgs c2;
   c2.in = L->y1;
@@ -903,16 +926,17 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
   c2.B = M;
+  c2.Z = 1;
   c2.linear = 1;
   c2.out = H->zv2;
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(4, M, 1), dim3(256), 0, st, c2);
+  hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, M), dim3(256), 0, st, c2);
   DQZ_HIP(hipGetLastError());
   LayerFwdArgs c3 = c2;
   c3.in = L->y2;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = H->zv3;
-  hipLaunchKernelGGL(conv3_fwd_kernel, dim3(4, M, 1), dim3(256), 0, st, c3);
+  hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, M), dim3(256), 0, st, c3);
   DQZ_HIP(hipGetLastError());
   Fc1FwdArgs f1;
   f1.in = L->y3;

@@ -118,6 +118,20 @@ class Learner:
         self._h, ctypes.byref(self._params_c), store.c_ref(),
         _native.ptr(slots), _native.ptr(weights), _native.stream_handle(stream)))
 
+  def step_uniform(self, store, base, size, capacity, seed, counter, slots_out,
+                   stream=None):
+    """Uniform sample + learner step in one pass (sampler fused into conv1).
+
+    Draws exactly what `sample_uniform(base, size, capacity, B, seed,
+    counter, ...)` would, writes them to `slots_out` and advances `counter`.
+    """
+    if slots_out.dtype != torch.int32 or slots_out.numel() != self.batch_size:
+      raise ValueError('slots_out must be a device int32 tensor of batch size')
+    _native.check(_native.lib().dqz_learner_step_uniform(
+        self._h, ctypes.byref(self._params_c), store.c_ref(), int(base),
+        int(size), int(capacity), int(seed) & (2**64 - 1), _native.ptr(counter),
+        _native.ptr(slots_out), _native.stream_handle(stream)))
+
   def grad(self, store, slots, weights=None, out=None, stream=None):
     """jax.grad(loss_fn) of the same step into a flat tensor (no update)."""
     if slots.dtype != torch.int32 or slots.numel() != self.batch_size:

@@ -115,6 +115,16 @@ int dqz_learner_destroy(dqz_learner* learner);
 int dqz_learner_step(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
                      const int32_t* slots, const float* is_weights, void* stream);
 
+/* Sampling fused into the step: the batch is `size` uniform draws
+ * (base + floor(u * size)) mod capacity with Philox(counter, i; seed), as
+ * dqz_sample_uniform would draw them, computed inside the conv1 kernel (no
+ * separate sampler launch); the drawn slots are written to slots_out (device
+ * int32 [B]) and *counter_dev advances by one.  Uniform FIFO / reservoir
+ * replays (replay.py:119-125, 246-296). */
+int dqz_learner_step_uniform(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                             int64_t base, int64_t size, int64_t capacity, uint64_t seed,
+                             uint64_t* counter_dev, int32_t* slots_out, void* stream);
+
 /* Gradient only: d loss / d params of the same step into grad_out (device
  * f32, dqz_param_layout order, padding untouched); params->online / mu / nu
  * are not modified and mu / nu may be NULL.  = jax.grad(loss_fn) at

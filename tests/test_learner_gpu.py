@@ -161,3 +161,24 @@ def test_sample_uniform_device(device):
   expected = counts.sum() / size
   # chi-square-ish bound on the per-slot counts
   assert np.abs(counts[live] - expected).max() < 6 * np.sqrt(expected)
+
+
+def test_fused_uniform_step_matches_sample_then_step(device):
+  """dqz_learner_step_uniform == dqz_sample_uniform + dqz_learner_step, bit for bit."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  batch = 32
+  net, lrn, st, host, online, target, mu, nu = _setup('dqn', batch, seed=13)
+  _, lrn2, _, _, _, _, _, _ = _setup('dqn', batch, seed=13)
+  c1 = torch.zeros((1,), dtype=torch.int64, device=device)
+  c2 = torch.zeros((1,), dtype=torch.int64, device=device)
+  s1 = torch.zeros((batch,), dtype=torch.int32, device=device)
+  s2 = torch.zeros((batch,), dtype=torch.int32, device=device)
+  for _ in range(3):
+    learner_lib.sample_uniform(5, 200, st.capacity, batch, 77, c1, s1)
+    lrn.step(st, s1)
+    lrn2.step_uniform(st, 5, 200, st.capacity, 77, c2, s2)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s2)
+  assert int(c1.item()) == int(c2.item()) == 3
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(lrn, which), getattr(lrn2, which))

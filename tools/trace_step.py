@@ -38,8 +38,7 @@ counter = torch.zeros((1,), dtype=torch.int64, device=dev)
 
 
 def step():
-  learner_lib.sample_uniform(0, cap, cap, 32, 1, counter, slots)
-  lrn.step(store, slots)
+  lrn.step_uniform(store, 0, cap, cap, 1, counter, slots)
 
 
 lib = _native.lib()
