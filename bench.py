@@ -50,10 +50,10 @@ def phase_flops(algo, batch):
       'conv3_fwd': 2 * z * b * MAC['conv3'],
       'fc1_fwd': 2 * z * b * MAC['fc1'],
       'head': 2 * z * b * MAC['fc2'],
-      'fc1_bwd': 2 * b * 2 * MAC['fc1'],
-      'bwd_conv3': 2 * b * 2 * MAC['conv3'],
-      'bwd_conv2': 2 * b * 2 * MAC['conv2'],
-      'conv1_dw': 2 * b * MAC['conv1'],
+      'fc1_dx': 2 * b * MAC['fc1'],
+      'conv3_dx+fc1_dw': 2 * b * (MAC['conv3'] + MAC['fc1']),
+      'conv2_dx+conv3_dw': 2 * b * (MAC['conv2'] + MAC['conv3']),
+      'conv1_dw+conv2_dw': 2 * b * (MAC['conv1'] + MAC['conv2']),
       'update': 0,
   }
 

@@ -19,8 +19,8 @@ ALGO_PER = 2
 NUM_LEAVES = 10
 NUM_PHASES = 10
 PHASE_NAMES = (
-    'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_bwd',
-    'bwd_conv3', 'bwd_conv2', 'conv1_dw', 'update')
+    'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_dx',
+    'conv3_dx+fc1_dw', 'conv2_dx+conv3_dw', 'conv1_dw+conv2_dw', 'update')
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4

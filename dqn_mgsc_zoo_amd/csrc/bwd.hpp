@@ -1,6 +1,7 @@
 // bwd.hpp — backward kernels specialised for the NatureQNetwork at small B.
 #pragma once
 #include "common.hpp"
+#include "conv1.hpp"
 #include "fwd.hpp"
 
 namespace dqz {
@@ -28,36 +29,33 @@ struct Fc1BwdArgs {
 
 constexpr int FC1B_LD = 528;  // LDS row stride of the dz1 chunk: 528 = 16 (mod 32) banks apart
 
-__global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
-  DQZ_STAMP(5, 0);
-  __shared__ __attribute__((aligned(16))) float s_dz[32 * FC1B_LD];  // dz1 chunk, later the dW block
-  __shared__ float s_red[4][2][256];
+// DX: dy3 = (dz1 @ W1^T) relu'(y3) (the critical path: conv3 backward waits on
+// it).  DW: dW1 + RMSProp, which only has to finish before the next step and
+// runs on the learner's side stream beside the conv backward kernels.  DW
+// must start after DX: it overwrites the W1 rows DX reads.
+constexpr int FC1B_SMEM = 32 * FC1B_LD + 4 * 2 * 256;  // floats: dz1 chunk (later the dW block) + dX partials
+
+template <bool DX, bool DW>
+__device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, int blk) {
+  DQZ_STAMP(DW ? 11 : 5, 0);
+  float* s_dz = smem;
+  float(*s_red)[2][256] = reinterpret_cast<float(*)[2][256]>(smem + 32 * FC1B_LD);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
-  const int k0 = 16 * blockIdx.x;
+  const int k0 = 16 * blk;
   const float* W1 = a.th + a.w_off;
   float4 wv[8];  // dX B operand: W1[k0 + n][128 w + 16 j + 4 kq + e]
+  if constexpr (DX) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
-  // RMSProp operands of this thread's 32 parameters of the 16 x 512 block, as
-  // float4 f = t + 256 i: row f / 128, columns 4 (f % 128) .. +3.
-  const bool upd = a.rms.gout == nullptr;
-  float4 o_th[8], o_mu[8], o_nu[8];
-  if (upd) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = t + 256 * i;
-      const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
-      o_th[i] = *reinterpret_cast<const float4*>(a.th + e);
-      o_mu[i] = *reinterpret_cast<const float4*>(a.mu + e);
-      o_nu[i] = *reinterpret_cast<const float4*>(a.nu + e);
-    }
+    for (int j = 0; j < 8; ++j)
+      wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
   }
+  const bool upd = DW && a.rms.gout == nullptr;
   f32x4 gacc[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) gacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int c = 0; c < a.B; c += 32) {
+    if (c > 0) __syncthreads();  // previous chunk's s_dz / s_red readers are done
     // stage dz1 rows [c, c + 32) (rows past B are zero)
     {
       float4 v[16];
@@ -68,15 +66,19 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
         v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       float ym[2];
+      if constexpr (DX) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-        ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
+        for (int h = 0; h < 2; ++h)
+          ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
+      }
       float yv[8];  // dW A operand: y3[c + 4 kk + kq][k0 + n]
+      if constexpr (DW) {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int bb = c + 4 * kk + kq;
-        const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
-        yv[kk] = bb < a.B ? y : 0.f;
+        for (int kk = 0; kk < 8; ++kk) {
+          const int bb = c + 4 * kk + kq;
+          const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
+          yv[kk] = bb < a.B ? y : 0.f;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -84,6 +86,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
         *reinterpret_cast<float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127)) = v[i];
       }
       __syncthreads();
+      if constexpr (DX) {
       // dX: rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
       f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -98,6 +101,12 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
           xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
         }
       }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s_red[w][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
+      }
+      if constexpr (DW) {
       // dW over the chunk: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
@@ -105,20 +114,23 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) gacc[q] = mfma4(yv[kk], d[16 * q], gacc[q]);
       }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[w][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
+      }
       __syncthreads();
+      if constexpr (DX) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int sample = c + 16 * h + (t >> 4);
         const float v2 = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
         if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
       }
+      }
     }
   }
-  DQZ_STAMP(5, 2);
+  if constexpr (!DW) {
+    DQZ_STAMP(5, 3);
+    return;
+  }
+  DQZ_STAMP(11, 2);
   // dW block through LDS into the float4 layout of the RMSProp operands.
   __syncthreads();
 #pragma unroll
@@ -126,12 +138,27 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) s_dz[(4 * kq + r) * FC1B_LD + 128 * w + 16 * q + n] = gacc[q][r];
   __syncthreads();
+  // RMSProp on this thread's 32 parameters of the 16 x 512 block, as float4
+  // f = t + 256 i: row f / 128, columns 4 (f % 128) .. +3; every operand load
+  // is issued before the first update.
   const Rms& R = a.rms;
+  float4 gv[8], o_th[8], o_mu[8], o_nu[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int f = t + 256 * i;
     const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
-    const float4 g = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127));
+    gv[i] = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127));
+    if (upd) {
+      o_th[i] = *reinterpret_cast<const float4*>(a.th + e);
+      o_mu[i] = *reinterpret_cast<const float4*>(a.mu + e);
+      o_nu[i] = *reinterpret_cast<const float4*>(a.nu + e);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = t + 256 * i;
+    const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
+    const float4 g = gv[i];
     if (!upd) {
       *reinterpret_cast<float4*>(R.gout + e) = g;
     } else {
@@ -152,7 +179,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(Fc1BwdArgs a) {
       *reinterpret_cast<float4*>(a.nu + e) = nu4;
     }
   }
-  DQZ_STAMP(5, 3);
+  DQZ_STAMP(11, 3);
 }
 
 // ---- conv3 backward: dX and per-sample dW partials -----------------------
@@ -308,19 +335,6 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
   }
 }
 
-__global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
-  DQZ_STAMP(6, 0);
-  __shared__ float s_win[C3X_WIN];
-  const SampleJob sj = xcd_sample_job(12, a.B);
-  if (!sj.valid) return;
-  const int job = sj.job, b = sj.s;
-  if (job < 8)
-    conv3_bwd_dx(a, s_win, b, job & 3, job >> 2);
-  else
-    conv3_bwd_dw(a, s_win, b, job - 8);
-  DQZ_STAMP(6, 3);
-}
-
 // ---- conv2 backward: dX by stride phase and per-sample dW partials --------
 // grid (12, B).  Jobs 0..7: dX of stride phase (ph, pw) = (job & 3) >> 1,
 // job & 1 for input-channel half job >> 2: output pixels (2a + ph, 2c + pw),
@@ -472,17 +486,147 @@ __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win
   }
 }
 
-__global__ __launch_bounds__(256) void conv2_bwd_kernel(Conv2BwdArgs a) {
-  DQZ_STAMP(7, 0);
-  __shared__ float s_win[C2W_WIN];
-  const SampleJob sj = xcd_sample_job(12, a.B);
-  if (!sj.valid) return;
-  const int job = sj.job, b = sj.s;
-  if (job < 8)
-    conv2_bwd_dx(a, s_win, b, (job & 3) >> 1, job & 1, job >> 2);
-  else
-    conv2_bwd_dw(a, s_win, b, job - 8);
-  DQZ_STAMP(7, 3);
+// ---- fc1 dW + RMSProp, 16 rows x 128 columns per block -------------------
+// 784 light blocks (3 per CU) so they fill the gaps beside the conv3 dX
+// workgroups they share a launch with.  Block (kb, nq): W1 rows
+// [16 kb, 16 kb + 16), columns [128 nq, 128 nq + 128); wave w owns columns
+// [128 nq + 32 w, +32) (two 16-column MFMA tiles), K = the batch.
+constexpr int FC1W_LD = 144;  // LDS row stride of the dz1 slice: 144 = 16 (mod 32)
+constexpr int FC1W_SMEM = 32 * FC1W_LD;
+
+__device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, int blk) {
+  DQZ_STAMP(11, 0);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  const int kb = blk >> 2, nq = blk & 3;
+  const int k0 = 16 * kb, c0 = 128 * nq;
+  f32x4 gacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int c = 0; c < a.B; c += 32) {
+    if (c > 0) __syncthreads();
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = t + 256 * i, row = f >> 5;  // 32 float4 per row
+      const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + c0 + 4 * (f & 31));
+      v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float yv[8];  // A operand: y3[c + 4 kk + kq][k0 + n]
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int bb = c + 4 * kk + kq;
+      const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
+      yv[kk] = bb < a.B ? y : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = t + 256 * i;
+      *reinterpret_cast<float4*>(smem + (f >> 5) * FC1W_LD + 4 * (f & 31)) = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const float* d = smem + (4 * kk + kq) * FC1W_LD + 32 * w + n;
+      gacc[0] = mfma4(yv[kk], d[0], gacc[0]);
+      gacc[1] = mfma4(yv[kk], d[16], gacc[1]);
+    }
+  }
+  DQZ_STAMP(11, 2);
+  // C layout: row = 4 kq + r, col = n of tile q -> W1[k0 + 4 kq + r][c0 + 32 w + 16 q + n]
+  const Rms& R = a.rms;
+  const bool upd = R.gout == nullptr;
+  float o_th[8], o_mu[8], o_nu[8];
+  if (upd) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
+        o_th[4 * q + r] = a.th[e];
+        o_mu[4 * q + r] = a.mu[e];
+        o_nu[4 * q + r] = a.nu[e];
+      }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
+      const float g = gacc[q][r];
+      if (!upd) {
+        R.gout[e] = g;
+      } else {
+        const float m = R.c1 * g + R.decay * o_mu[4 * q + r];
+        const float vv = R.c1 * (g * g) + R.decay * o_nu[4 * q + r];
+        a.mu[e] = m;
+        a.nu[e] = vv;
+        a.th[e] = o_th[4 * q + r] + (-R.lr) * (g * rsqrtf(vv - m * m + R.eps));
+      }
+    }
+  DQZ_STAMP(11, 3);
+}
+
+// ---- backward launches ----------------------------------------------------
+// Each launch pairs a critical-path dX job set with an independent dW job set
+// so the latency-bound dX workgroups and the dW workgroups share the CUs
+// (one launch, no cross-stream dependency edges):
+//   fc1_dx_kernel                  fc1 dX
+//   bwd_b_kernel  = conv3 dX (8 jobs/sample)  + fc1 dW + RMSProp (784 blocks)
+//   bwd_c_kernel  = conv2 dX (8 jobs/sample)  + conv3 dW (4 jobs/sample)
+//   bwd_d_kernel  = conv1 dW (4 jobs/sample)  + conv2 dW (4 jobs/sample)
+constexpr size_t kBwdDSmem = (C2W_WIN * sizeof(float) > kConv1DwSmem) ? C2W_WIN * sizeof(float) : kConv1DwSmem;
+
+__global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[FC1B_SMEM];
+  fc1_bwd_body<true, false>(a, smem, blockIdx.x);
+  DQZ_STAMP(5, 3);
+}
+
+__global__ __launch_bounds__(256) void bwd_b_kernel(Conv3BwdArgs c3, Fc1BwdArgs f1) {
+  __shared__ __attribute__((aligned(16))) float smem[C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM];
+  const int n3 = 8 * ((c3.B + 7) / 8) * 8;
+  if ((int)blockIdx.x < n3) {
+    const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c3.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(6, 0);
+    conv3_bwd_dx(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
+    DQZ_STAMP(6, 3);
+  } else {
+    fc1_dw_body(f1, smem, blockIdx.x - n3);
+  }
+}
+
+__global__ __launch_bounds__(256) void bwd_c_kernel(Conv2BwdArgs c2, Conv3BwdArgs c3) {
+  __shared__ __attribute__((aligned(16))) float smem[C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN];
+  const int n2 = 8 * ((c2.B + 7) / 8) * 8;
+  if ((int)blockIdx.x < n2) {
+    const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c2.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(7, 0);
+    conv2_bwd_dx(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    DQZ_STAMP(7, 3);
+  } else {
+    const SampleJob sj = xcd_sample_job_at(blockIdx.x - n2, 4, c3.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(12, 0);
+    conv3_bwd_dw(c3, smem, sj.s, sj.job);
+    DQZ_STAMP(12, 3);
+  }
+}
+
+__global__ __launch_bounds__(256) void bwd_d_kernel(Conv1DwArgs c1, Conv2BwdArgs c2) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n1 = 4 * ((c1.B + 7) / 8) * 8;
+  if ((int)blockIdx.x < n1) {
+    const SampleJob sj = xcd_sample_job_at(blockIdx.x, C1_BLOCKS, c1.B);
+    if (!sj.valid) return;
+    conv1_dw_body(c1, smem, sj.job, sj.s);
+  } else {
+    const SampleJob sj = xcd_sample_job_at(blockIdx.x - n1, 4, c2.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(13, 0);
+    conv2_bwd_dw(c2, smem, sj.s, sj.job);
+    DQZ_STAMP(13, 3);
+  }
 }
 
 }  // namespace dqz

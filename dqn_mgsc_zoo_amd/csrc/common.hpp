@@ -151,6 +151,12 @@ struct SampleJob {
   bool valid;
 };
 
+__device__ __forceinline__ SampleJob xcd_sample_job_at(int i, int J, int nsamp) {
+  const int x = i & 7, slot = i >> 3;
+  const int s = 8 * (slot / J) + x;
+  return SampleJob{s, slot % J, s < nsamp};
+}
+
 __device__ __forceinline__ SampleJob xcd_sample_job(int J, int nsamp) {
   const int i = blockIdx.x, x = i & 7, slot = i >> 3;
   const int s = 8 * (slot / J) + x;

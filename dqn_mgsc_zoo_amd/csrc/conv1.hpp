@@ -163,14 +163,10 @@ struct Conv1DwArgs {
 // Partial dW/db of one 100-position block: part[k][co] = sum_p x(p,k) dy(p,co).
 // grid (4 row blocks, B); wave w owns kernel rows [64w, 64w+64) (two 32-row
 // MFMA tiles; row = kh*32 + kw*4 + ci), K' = 100 positions.
-__global__ __launch_bounds__(256) void conv1_dw_kernel(Conv1DwArgs a) {
+__device__ __forceinline__ void conv1_dw_body(const Conv1DwArgs& a, float* smem, int rb, int b) {
   DQZ_STAMP(8, 0);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                 // 8064
   float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
-  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.B);
-  if (!sj.valid) return;
-  const int rb = sj.job, b = sj.s;
   const float4* dy4 = reinterpret_cast<const float4*>(a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO);
   constexpr int ND4 = C1_POS * C1CO / 4;  // 800
   float4 dv[4];

@@ -243,8 +243,8 @@ static int init_kernel_attrs() {
   if (g_attr_done) return DQZ_OK;
   DQZ_HIP(hipFuncSetAttribute((const void*)conv1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kConv1FwdSmem));
-  DQZ_HIP(hipFuncSetAttribute((const void*)conv1_dw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kConv1DwSmem));
+  DQZ_HIP(hipFuncSetAttribute((const void*)bwd_d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kBwdDSmem));
   g_attr_done = 1;
   return DQZ_OK;
 }
@@ -455,6 +455,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   DQZ_HIP(launch_head(h, B, st));
   pe.mark(5, st);
 
+  // Backward: fc1 dX, then three launches that each pair the next dX job set
+  // of the critical path with an independent dW job set (bwd.hpp).
   Fc1BwdArgs fb;
   fb.dz1 = L->dz1;
   fb.y3 = L->y3;
@@ -465,7 +467,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.rms = rms;
   fb.B = B;
   fb.dy3 = L->dy3;
-  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+  hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
   DQZ_HIP(hipGetLastError());
   pe.mark(6, st);
 
@@ -476,10 +478,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
   c3b.B = B;
-  hipLaunchKernelGGL(conv3_bwd_kernel, xcd_grid(12, B), dim3(256), 0, st, c3b);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(7, st);
-
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -487,17 +485,20 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
   c2b.B = B;
-  hipLaunchKernelGGL(conv2_bwd_kernel, xcd_grid(12, B), dim3(256), 0, st, c2b);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(8, st);
-
   Conv1DwArgs c1dw;
   c1dw.src = src;
   c1dw.which = 0;
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  hipLaunchKernelGGL(conv1_dw_kernel, xcd_grid(C1_BLOCKS, B), dim3(256), kConv1DwSmem, st, c1dw);
+  const int B8 = (B + 7) / 8 * 8;
+  hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
+  DQZ_HIP(hipGetLastError());
+  pe.mark(7, st);
+  hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
+  DQZ_HIP(hipGetLastError());
+  pe.mark(8, st);
+  hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
   DQZ_HIP(hipGetLastError());
   pe.mark(9, st);
 

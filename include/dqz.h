@@ -133,12 +133,13 @@ int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_s
                      const int32_t* slots, const float* is_weights, float* grad_out, void* stream);
 
 /* Phases of one learner step, in launch order (dqz_learner_profile):
- *  0 conv1 fwd (frame gather fused)   1 conv2 fwd   2 conv3 fwd
- *  3 fc1 fwd (split-K)
+ *  0 conv1 fwd (uniform draw + frame gather fused)   1 conv2 fwd
+ *  2 conv3 fwd   3 fc1 fwd (split-K)
  *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample)
- *  5 fc1 backward: dX + dW + RMSProp of fc1/w in one pass over W1
- *  6 {conv3 dX, conv3 dW}             7 {conv2 dX, conv2 dW}
- *  8 conv1 dW (frame gather fused)
+ *  5 fc1 dX
+ *  6 conv3 dX  + fc1 dW and RMSProp of fc1/w   (one launch, two job sets)
+ *  7 conv2 dX  + conv3 dW partials
+ *  8 conv1 dW partials (frame gather fused) + conv2 dW partials
  *  9 gradient reductions + RMSProp (all leaves but fc1/w) */
 #define DQZ_NUM_PHASES 10
 

@@ -22,9 +22,9 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
 
-NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_bwd',
-         6: 'conv3_bwd', 7: 'conv2_bwd', 8: 'conv1_dw', 9: 'update'}
-ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9]
+NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
+         6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*'}
+ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
 K, NB, NS = 16, 1024, 4
 
 dev = torch.device('cuda:0')
@@ -64,6 +64,7 @@ torch.cuda.synchronize()
 fn(buf.ctypes.data, 0)
 t = buf.reshape(K, NB, NS).astype(np.int64)
 prev_end = None
+t0 = t[:, :, 0][t[:, :, 0] > 0].min()
 print('%-10s %8s %8s %8s | %8s %8s %8s %8s  (us; 100 MHz ticks)' % (
     'kernel', 'gap', 'span', 'blk_med', 's0-s1', 's1-s2', 's2-s3', 'nblk'))
 for k in ORDER:
@@ -79,6 +80,8 @@ for k in ORDER:
     x = t[k, live, b] - t[k, live, a]
     ok = (t[k, live, a] > 0) & (t[k, live, b] > 0)
     return np.median(x[ok]) / 100 if ok.any() else float('nan')
-  print('%-10s %8.2f %8.2f %8.2f | %8.2f %8.2f %8.2f %8d' % (
-      NAMES[k], gap, (end - start) / 100, np.median(s3 - s0) / 100, med(0, 1), med(1, 2), med(2, 3), live.sum()))
-  prev_end = end
+  print('%-10s %8.2f %8.2f %8.2f | %8.2f %8.2f %8.2f %8d  [%.2f .. %.2f]' % (
+      NAMES[k], gap, (end - start) / 100, np.median(s3 - s0) / 100, med(0, 1), med(1, 2), med(2, 3), live.sum(),
+      (start - t0) / 100, (end - t0) / 100))
+  if not NAMES[k].endswith('*'):
+    prev_end = end
