@@ -321,18 +321,38 @@ static int check_store(const dqz_store* S) {
   return DQZ_OK;
 }
 
-// Phase markers for dqz_learner_profile: ev[i] is recorded before phase i.
+// dqz_learner_profile: each phase's launch is repeated `reps` times back to
+// back between two events on the launch stream, so ms[i] is that kernel's
+// average duration in a saturated stream (what rocprofv3's kernel trace
+// reports), not a single launch plus its dispatch gap.
 struct PhaseEvents {
-  hipEvent_t* ev;
-  void mark(int i, hipStream_t st) const {
-    if (ev) (void)hipEventRecord(ev[i], st);
-  }
+  hipEvent_t e0, e1;
+  int reps;
+  float* ms;
+  bool on() const { return ms != nullptr; }
 };
+static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
+
+#define DQZ_PHASE(i, ...)                                                   \
+  do {                                                                      \
+    if (!pe.on()) {                                                         \
+      __VA_ARGS__;                                                          \
+    } else {                                                                \
+      DQZ_HIP(hipEventRecord(pe.e0, st));                                   \
+      for (int r_ = 0; r_ < pe.reps; ++r_) {                                \
+        __VA_ARGS__;                                                        \
+      }                                                                     \
+      DQZ_HIP(hipEventRecord(pe.e1, st));                                   \
+      DQZ_HIP(hipEventSynchronize(pe.e1));                                  \
+      float ms_ = 0.f;                                                      \
+      (void)hipEventElapsedTime(&ms_, pe.e0, pe.e1);                        \
+      pe.ms[i] = ms_ / (float)pe.reps;                                      \
+    }                                                                       \
+  } while (0)
 
 // conv1..fc1 forward of Z network copies (phases 0-3).
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
                         PhaseEvents pe) {
-  pe.mark(0, st);
   Conv1FwdArgs c1;
   c1.src = src;
   c1.nz = nz;
@@ -342,9 +362,8 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.Z = Z;
   c1.linear = 0;
   c1.out = L->y1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(1, st);
+  DQZ_PHASE(0, hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
+            DQZ_HIP(hipGetLastError()));
 
   LayerFwdArgs c2;
   c2.in = L->y1;
@@ -355,18 +374,16 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c2.Z = Z;
   c2.linear = 0;
   c2.out = L->y2;
-  hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(2, st);
+  DQZ_PHASE(1, hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
+            DQZ_HIP(hipGetLastError()));
 
   LayerFwdArgs c3 = c2;
   c3.in = L->y2;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(3, st);
+  DQZ_PHASE(2, hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
+            DQZ_HIP(hipGetLastError()));
 
   Fc1FwdArgs f1;
   f1.in = L->y3;
@@ -375,9 +392,8 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   f1.B = B;
   f1.MG = (B + 31) / 32;
   f1.part = L->fc1p;
-  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(4, st);
+  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
+            DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
 
@@ -452,8 +468,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.gq = L->gq;
   h.ga = L->ga;
   h.dz1 = L->dz1;
-  DQZ_HIP(launch_head(h, B, st));
-  pe.mark(5, st);
+  DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
 
   // Backward: fc1 dX, then three launches that each pair the next dX job set
   // of the critical path with an independent dW job set (bwd.hpp).
@@ -467,9 +482,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.rms = rms;
   fb.B = B;
   fb.dy3 = L->dy3;
-  hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(6, st);
+  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+            DQZ_HIP(hipGetLastError()));
 
   Conv3BwdArgs c3b;
   c3b.dy3 = L->dy3;
@@ -492,15 +506,12 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
   const int B8 = (B + 7) / 8 * 8;
-  hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(7, st);
-  hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(8, st);
-  hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(9, st);
+  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
+            DQZ_HIP(hipGetLastError()));
+  DQZ_PHASE(7, hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
+            DQZ_HIP(hipGetLastError()));
+  DQZ_PHASE(8, hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
+            DQZ_HIP(hipGetLastError()));
 
   UpdArgs u;
   u.th = P->online;
@@ -527,15 +538,15 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.nb2 = L->shared_bias ? 1 : A;
   u.rms = rms;
   const int64_t nupd = L->sz[0] + L->sz[1] + L->sz[2] + L->sz[3] + L->sz[4] + L->sz[5] + HID + (int64_t)HID * A + u.nb2;
-  hipLaunchKernelGGL(update_kernel, dim3((unsigned)((nupd + UPD_PARAMS - 1) / UPD_PARAMS)), dim3(256), 0, st, u);
-  DQZ_HIP(hipGetLastError());
-  pe.mark(DQZ_NUM_PHASES, st);
+  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3((unsigned)((nupd + UPD_PARAMS - 1) / UPD_PARAMS)), dim3(256), 0,
+                                  st, u);
+            DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
 
 int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream) {
-  return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr});
+  return step_impl(L, P, S, slots, is_weights, stream, kNoProfile);
 }
 
 int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_store* S, int64_t base, int64_t size,
@@ -546,36 +557,25 @@ int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_stor
   if (capacity < size || base < 0) return fail(DQZ_ERR_INVALID, "bad replay geometry");
   if (L && L->cfg.algo == DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "PER samples by priority, not uniformly");
   const UniformDraw d{base, size, capacity, seed, counter_dev, slots_out};
-  return step_impl(L, P, S, slots_out, nullptr, stream, PhaseEvents{nullptr}, nullptr, nullptr, &d);
+  return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, &d);
 }
 
 int dqz_learner_grad(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, float* grad_out, void* stream) {
   if (!grad_out) return fail(DQZ_ERR_INVALID, "null grad_out");
-  return step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{nullptr}, grad_out);
+  return step_impl(L, P, S, slots, is_weights, stream, kNoProfile, grad_out);
 }
 
 int dqz_learner_profile(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                         const float* is_weights, int iters, float* phase_ms, void* stream) {
   if (!phase_ms || iters < 1) return fail(DQZ_ERR_INVALID, "phase_ms must be non-null and iters >= 1");
-  hipEvent_t ev[DQZ_NUM_PHASES + 1];
-  for (int i = 0; i <= DQZ_NUM_PHASES; ++i) DQZ_HIP(hipEventCreate(&ev[i]));
   for (int i = 0; i < DQZ_NUM_PHASES; ++i) phase_ms[i] = 0.f;
-  int rc = DQZ_OK;
-  for (int it = 0; it < iters && rc == DQZ_OK; ++it) {
-    rc = step_impl(L, P, S, slots, is_weights, stream, PhaseEvents{ev});
-    if (rc) break;
-    if (hipEventSynchronize(ev[DQZ_NUM_PHASES]) != hipSuccess) {
-      rc = fail(DQZ_ERR_HIP, "hipEventSynchronize failed");
-      break;
-    }
-    for (int i = 0; i < DQZ_NUM_PHASES; ++i) {
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
-      phase_ms[i] += ms / (float)iters;
-    }
-  }
-  for (int i = 0; i <= DQZ_NUM_PHASES; ++i) (void)hipEventDestroy(ev[i]);
+  PhaseEvents pe{nullptr, nullptr, iters, phase_ms};
+  DQZ_HIP(hipEventCreate(&pe.e0));
+  DQZ_HIP(hipEventCreate(&pe.e1));
+  const int rc = step_impl(L, P, S, slots, is_weights, stream, pe);
+  (void)hipEventDestroy(pe.e0);
+  (void)hipEventDestroy(pe.e1);
   return rc;
 }
 
@@ -594,7 +594,7 @@ static int forward_q(dqz_learner* L, const float* params, const Conv1Src& src, i
   NetZ nz;
   nz.p[0] = nz.p[1] = nz.p[2] = params;
   nz.which[0] = nz.which[1] = nz.which[2] = which;
-  if (int rc = forward_impl(L, nz, 1, n, src, st, PhaseEvents{nullptr})) return rc;
+  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile)) return rc;
   HeadArgs h = make_head(L, nz, 1, n);
   h.fwd_only = 1;
   h.q = q_out;
@@ -878,7 +878,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   DQZ_HIP(hipGetLastError());
 
   // G = sum_i p_i g_i: one batched backward with p-weighted cotangents.
-  if (int rc = step_impl(L, P, S, slots, nullptr, stream, PhaseEvents{nullptr}, H->G, H->p)) return rc;
+  if (int rc = step_impl(L, P, S, slots, nullptr, stream, kNoProfile, H->G, H->p)) return rc;
 
   MetaRmsArgs ra;
   ra.lr = H->cfg.learning_rate;
@@ -898,7 +898,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   P1.target = P->online;
   P1.mu = nullptr;
   P1.nu = nullptr;
-  if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, PhaseEvents{nullptr}, H->G)) return rc;
+  if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->G)) return rc;
 
   // v = -2 u' du/dG -> thp buffer; partial sums of u'^2.
   hipLaunchKernelGGL(meta_rms2_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)H->mu1,
