@@ -76,6 +76,7 @@ class DqzMetaConfig(ctypes.Structure):
       ('b1', ctypes.c_float),
       ('b2', ctypes.c_float),
       ('meta_eps', ctypes.c_float),
+      ('second_order', ctypes.c_int),
   ]
 
 

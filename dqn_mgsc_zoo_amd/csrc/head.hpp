@@ -19,6 +19,7 @@ struct HeadArgs {
   const float* weights;  // PER importance weights or null
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
   uint64_t* advance;     // fused sampler's step counter, advanced once here (or null)
+  int unit;              // 1: unit cotangent on q[a] (gradient of q itself; HVP pass)
   float bound;           // grad_error_bound
   float* q;              // [Z][B][A]
   float* td;             // [B]
@@ -116,7 +117,9 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
     }
     const float td = (r + d * v) - s_q[0][a_tm1];
     float g;
-    if (h.meta_p) {
+    if (h.unit) {
+      g = -1.f;  // gq = d q[a] / d q[a] = 1
+    } else if (h.meta_p) {
       // meta mode: p_b * grad of loss_fn on the single transition b
       // (dqn_mgsc_batched/agent.py:152-158): batch of one, clip, then weight.
       g = pm * fminf(fmaxf(td, -h.bound), h.bound);

@@ -22,6 +22,7 @@
 #include "bwd.hpp"
 #include "head.hpp"
 #include "meta.hpp"
+#include "hvp.hpp"
 #include "sampling.hpp"
 
 namespace dqz {
@@ -422,7 +423,7 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 // meta_p != null: per-sample cotangents p_b * (-clip(td_b)) (MGSC meta mode).
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
-                     const float* meta_p = nullptr, const UniformDraw* draw = nullptr) {
+                     const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -462,6 +463,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
   h.meta_p = meta_p;
   h.advance = draw ? draw->counter : nullptr;
+  h.unit = unit;
   h.bound = L->cfg.grad_error_bound;
   h.td = L->td;
   h.loss_part = L->loss_part;
@@ -796,6 +798,10 @@ struct dqz_meta {
   float *zv1, *zv2, *zv3, *zvp;    // tangent forward outputs
   float *x, *p, *s, *dl, *loss, *loss_part;
   int nparts;
+  // second-order (reservoir) meta-gradient
+  float *GQ, *HQ, *s1_part;
+  float *ty1, *ty2, *ty3, *th4, *td4, *td3, *td2, *td1;
+  int nparts2;
   void* block;
 };
 
@@ -828,12 +834,19 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
   const int M = cfg->meta_batch;
   H->total = H->lm->total;
   H->nparts = (int)((H->total / 4 + 255) / 256);
+  H->nparts2 = (int)((H->total + 255) / 256);
+  const int64_t so = cfg->second_order ? 1 : 0;
   const int64_t sizes[] = {H->total, H->total, H->total, H->total, H->total,
                            (int64_t)M * C1M * C1CO, (int64_t)M * C2M * C2CO, (int64_t)M * FLAT,
                            (int64_t)H->lm->S_fc1 * M * HID,
-                           M, M, M, M, 1, H->nparts};
+                           M, M, M, M, 1, H->nparts2,
+                           so * H->total, so * H->total, so * H->nparts2,
+                           so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * HID, so * FLAT,
+                           so * C2M * C2CO, so * C1M * C1CO};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
-                    &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part};
+                    &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part,
+                    &H->GQ, &H->HQ, &H->s1_part,
+                    &H->ty1, &H->ty2, &H->ty3, &H->th4, &H->td4, &H->td3, &H->td2, &H->td1};
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
   if (hipMalloc(&H->block, tot * sizeof(float)) != hipSuccess || hipMemset(H->block, 0, tot * sizeof(float)) != hipSuccess) {
@@ -892,18 +905,83 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
                      (float4*)H->nu1, (float4*)H->J);
   DQZ_HIP(hipGetLastError());
 
-  // g' = grad loss_fn(theta', target = theta, online transition) -> G buffer.
   dqz_params P1;
   P1.online = H->thp;
   P1.target = P->online;
   P1.mu = nullptr;
   P1.nu = nullptr;
-  if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->G)) return rc;
-
-  // v = -2 u' du/dG -> thp buffer; partial sums of u'^2.
-  hipLaunchKernelGGL(meta_rms2_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)H->mu1,
-                     (const float4*)H->nu1, (const float4*)H->J, (float4*)H->thp, H->loss_part);
-  DQZ_HIP(hipGetLastError());
+  int nloss = H->nparts;
+  if (!H->cfg.second_order) {
+    // g' = grad loss_fn(theta', target = theta, online transition) -> G buffer.
+    if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->G)) return rc;
+    // v = -2 u' du/dG -> thp buffer; partial sums of u'^2.
+    hipLaunchKernelGGL(meta_rms2_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)H->mu1,
+                       (const float4*)H->nu1, (const float4*)H->J, (float4*)H->thp, H->loss_part);
+    DQZ_HIP(hipGetLastError());
+  } else {
+    // grad q[a] at theta' (unit cotangent) -> GQ; the one-sample learner keeps
+    // the primal activations, the unit-cotangent backward signals and td'.
+    dqz_learner* L1 = H->l1;
+    if (int rc = step_impl(L1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->GQ, nullptr, nullptr, 1))
+      return rc;
+    MetaSecondArgs sa;
+    sa.lr = ra.lr;
+    sa.decay = ra.decay;
+    sa.c1 = ra.c1;
+    sa.eps = ra.eps;
+    sa.bound = H->cfg.grad_error_bound;
+    sa.n = H->total;
+    sa.td = L1->td;
+    const dim3 eg1((unsigned)H->nparts2);
+    // v_dir -> mu1, w -> nu1, partial sums of u'^2 and grad q . w
+    hipLaunchKernelGGL(meta_second_kernel, eg1, dim3(256), 0, st, sa, H->GQ, H->G, H->mu1, H->nu1, H->loss_part,
+                       H->s1_part);
+    DQZ_HIP(hipGetLastError());
+    HvpArgs hv;
+    hv.frames = S1->frames;
+    hv.fidx = S1->fidx;
+    hv.slot = online_slot;
+    hv.action = S1->action;
+    hv.th = H->thp;
+    hv.tw = H->nu1;
+    for (int i = 0; i < 10; ++i) hv.off[i] = L1->off[i];
+    hv.A = A;
+    hv.y1 = L1->y1;
+    hv.y2 = L1->y2;
+    hv.y3 = L1->y3;
+    hv.h = L1->h1;
+    hv.d1 = L1->dy1;
+    hv.d2 = L1->dy2;
+    hv.d3 = L1->dy3;
+    hv.d4 = L1->dz1;
+    hv.ty1 = H->ty1;
+    hv.ty2 = H->ty2;
+    hv.ty3 = H->ty3;
+    hv.th4 = H->th4;
+    hv.td4 = H->td4;
+    hv.td3 = H->td3;
+    hv.td2 = H->td2;
+    hv.td1 = H->td1;
+    hv.hq = H->HQ;
+    auto g256 = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    hipLaunchKernelGGL(hvp_t1_kernel, g256(C1M * C1CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t2_kernel, g256(C2M * C2CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t3_kernel, g256(FLAT), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t4_kernel, g256(HID), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b3_kernel, g256(FLAT), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b2_kernel, g256(C2M * C2CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b1_kernel, g256(C1M * C1CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_g_conv1_kernel, g256((C1KK + 1) * C1CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_g_conv23_kernel, g256((C2KK + 1) * C2CO + (C3KK + 1) * C3CO), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_g_fc_kernel, g256((int64_t)FLAT * HID + HID + (int64_t)HID * A + A), dim3(256), 0, st,
+                       hv);
+    DQZ_HIP(hipGetLastError());
+    // v = v_dir + J (alpha s1 grad q - clip(td') H w) -> thp (theta' is no longer needed)
+    hipLaunchKernelGGL(meta_combine_kernel, eg1, dim3(256), 0, st, sa, H->mu1, H->J, H->GQ, H->HQ, H->s1_part,
+                       H->nparts2, H->thp);
+    DQZ_HIP(hipGetLastError());
+    nloss = H->nparts2;
+  }
   const float* v = H->thp;
 
   // Tangent forward over the stored online activations: V * y + vb per layer.
@@ -987,7 +1065,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.b2 = H->cfg.b2;
   ad.eps = H->cfg.meta_eps;
   ad.loss_part = H->loss_part;
-  ad.nparts = H->nparts;
+  ad.nparts = nloss;
   ad.loss = H->loss;
   ad.dlogits = H->dl;
   hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);

@@ -21,6 +21,7 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
   """Deep Q-Network agent with meta-learned replay logits."""
 
   _ALGO = 'dqn'
+  _SECOND_ORDER = False  # theta'' = stop_gradient(...) (agent.py:191)
 
   def __init__(self, preprocessor, sample_network_input, network, optimizer,
                transition_accumulator, replay, batch_size: int,
@@ -35,7 +36,8 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
                      grad_error_bound, rng_key, device=device)
     self._meta_batch_size = int(meta_batch_size)
     self._meta = learner_lib.MetaLearner(self._learner, self._meta_batch_size,
-                                         meta_optimizer)
+                                         meta_optimizer,
+                                         second_order=self._SECOND_ORDER)
     self._last_transitions = []
     self._slots_cache = None
 

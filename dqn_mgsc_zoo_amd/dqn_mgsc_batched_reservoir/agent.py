@@ -1,27 +1,19 @@
 """MGSC DQN agent over the learned-logit reservoir replay
 (drop-in for dqn_zoo/dqn_mgsc_batched_reservoir/agent.py).
 
-The reference file differs from dqn_mgsc_batched/agent.py in two places
-only: the replay type hint (MGSCReservoirTransitionReplay, :52) and the
-missing `jax.lax.stop_gradient` on theta'' (:191 of the batched agent),
-which makes its meta-gradient second order (d theta''/d theta' involves the
-Hessian of the online-transition loss).  The device meta-update implements
-the stop-gradient form; the second-order form is not on device yet, so this
-agent refuses to run it silently: pass meta_gradient='stop_gradient' to opt
-into the first-order meta-gradient explicitly.
+The reference file differs from dqn_mgsc_batched/agent.py in two places: the
+replay type hint (MGSCReservoirTransitionReplay, :52) and the missing
+`jax.lax.stop_gradient` on theta'' (present at :191 of the batched agent).
+Without it the meta-gradient also differentiates through the online
+transition's gradient at theta', i.e. a Hessian-vector product of that
+transition's loss; the device meta-update computes it (second_order mode,
+hvp.hpp), checked against torch double-backward and the fp64 oracle.
 """
 
 from dqn_mgsc_zoo_amd.dqn_mgsc_batched import agent as batched
 
 
 class MGSCDqn(batched.MGSCDqn):
-  """MGSC DQN over MGSCReservoirTransitionReplay."""
+  """MGSC DQN over MGSCReservoirTransitionReplay, second-order meta-gradient."""
 
-  def __init__(self, *args, meta_gradient='second_order', **kwargs):
-    if meta_gradient != 'stop_gradient':
-      raise NotImplementedError(
-          'dqn_mgsc_batched_reservoir differentiates through theta\'\' '
-          '(no stop_gradient, second-order meta-gradient); the device '
-          "meta-update implements the stop_gradient form only. Pass "
-          "meta_gradient='stop_gradient' to use it.")
-    super().__init__(*args, **kwargs)
+  _SECOND_ORDER = True

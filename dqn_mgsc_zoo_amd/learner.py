@@ -232,6 +232,11 @@ def adam(learning_rate, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0):
 class MetaLearner:
   """MGSC meta-update on device (dqn_mgsc_batched/agent.py:104-220, 302-334).
 
+  second_order=True is the reservoir agent's meta_loss_fn (no stop_gradient
+  on theta'', dqn_mgsc_batched_reservoir/agent.py): the gradient also flows
+  through the online transition's gradient at theta' (a Hessian-vector
+  product, hvp.hpp).
+
   Holds the meta optimizer state (optax ScaleByAdamState(count, mu, nu) over
   the M meta-batch logits, shared across calls exactly as the reference's
   `self._meta_opt_state`) and a one-slot frame store for the newest
@@ -241,7 +246,8 @@ class MetaLearner:
   (replay.update_priorities(indices, new_meta_params)).
   """
 
-  def __init__(self, learner: Learner, meta_batch_size, meta_optimizer=None):
+  def __init__(self, learner: Learner, meta_batch_size, meta_optimizer=None,
+               second_order=False):
     from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
     if learner.algo != 'dqn':
       raise ValueError('the MGSC agents use q_learning on dqn_atari_network')
@@ -249,6 +255,7 @@ class MetaLearner:
     self.learner = learner
     self.meta_batch_size = int(meta_batch_size)
     self.meta_optimizer = meta_optimizer
+    self.second_order = bool(second_order)
     dev = learner.device
     m = self.meta_batch_size
     self.adam_mu = torch.zeros((m,), dtype=torch.float32, device=dev)
@@ -265,7 +272,8 @@ class MetaLearner:
     cfg = _native.DqzMetaConfig(
         m, learner.network.num_actions, opt.learning_rate, opt.decay, opt.eps,
         learner.grad_error_bound, meta_optimizer.learning_rate,
-        meta_optimizer.b1, meta_optimizer.b2, meta_optimizer.eps)
+        meta_optimizer.b1, meta_optimizer.b2, meta_optimizer.eps,
+        int(bool(second_order)))
     handle = ctypes.c_void_p()
     _native.check(_native.lib().dqz_meta_create(ctypes.byref(cfg),
                                                 ctypes.byref(handle)))

@@ -243,6 +243,9 @@ typedef struct dqz_meta_config {
   float grad_error_bound;  /* rlax.clip_gradient bound */
   float meta_learning_rate; /* optax.adam lr, run_atari.py:241-243 */
   float b1, b2, meta_eps;  /* optax.adam defaults 0.9, 0.999, 1e-8 */
+  int second_order;        /* 0: theta'' = stop_gradient(...) (dqn_mgsc_batched/agent.py:191);
+                              1: no stop_gradient (dqn_mgsc_batched_reservoir/agent.py):
+                              d theta''/d theta' through the online transition's Hessian */
 } dqz_meta_config;
 
 typedef struct dqz_meta dqz_meta;
@@ -251,7 +254,8 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out);
 int dqz_meta_destroy(dqz_meta* meta);
 
 /* One jitted `meta_update` + `replay.update_priorities` (agent.py:211-220,
- * 302-334) for the stop-gradient (FIFO) variant:
+ * 302-334); written for the stop-gradient variant, cfg.second_order adds the
+ * reservoir variant's d theta''/d theta' term (Hessian-vector product):
  *   p = softmax(logits[pos]) (replay_circular.py:79-86); G = sum_i p_i g_i
  *   (per-transition grads of loss_fn, agent.py:152-172); theta' = theta +
  *   RMSProp(G; mu, nu); g' = grad loss_fn(theta', target=theta, online

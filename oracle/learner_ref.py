@@ -240,9 +240,76 @@ def rmsprop_update_jacobian(g, mu, nu, lr, decay, eps):
   return -lr * (dd - c * g * (g - m)) / dd**1.5
 
 
+def hvp(params, cache, dq, tangent, shared_bias=False):
+  """Hessian-vector product of sum(dq * q(theta)) along `tangent` (a tree).
+
+  Forward-over-reverse restatement of `forward`/`backward`: tangents of every
+  pre-activation with the ReLU masks held fixed, then the tangent of each
+  backward signal and of each weight gradient (product rule).  Used for the
+  second-order meta-gradient of dqn_mgsc_batched_reservoir/agent.py (no
+  stop_gradient on theta'').
+  """
+  def tw(name, leaf='w'):
+    return np.asarray(tangent[name][leaf], np.float64)
+
+  def pw(name, leaf='w'):
+    return np.asarray(params[name][leaf], np.float64)
+
+  # tangent forward
+  ydot = [None, None, None]
+  colsdot = [None, None, None]
+  prev = None
+  for i, ((k, st, _, co), name) in enumerate(zip(CONV_SPECS, CONV_NAMES)):
+    cols = cache['cols%d' % i]
+    zdot = cols @ tw(name).reshape(-1, co) + tw(name, 'b')
+    if prev is not None:
+      colsdot[i] = _im2col(prev, k, st)
+      zdot = zdot + colsdot[i] @ pw(name).reshape(-1, co)
+    ydot[i] = zdot * (cache['y%d' % i] > 0)
+    prev = ydot[i]
+  flat, h1 = cache['flat'], cache['h1']
+  flatdot = ydot[2].reshape(flat.shape)
+  w1 = pw(_HEAD + '/linear')
+  h1dot = (flat @ tw(_HEAD + '/linear') + flatdot @ w1 + tw(_HEAD + '/linear', 'b')) * (h1 > 0)
+  w2, _ = head_params(params, shared_bias)
+  w2dot = tw(_HEAD + '/linear_1')
+  out = {}
+  out[_HEAD + '/linear_1'] = {'w': h1dot.T @ dq}
+  if shared_bias:
+    out[_HEAD] = {'b': np.zeros(1)}
+  else:
+    out[_HEAD + '/linear_1']['b'] = np.zeros(dq.shape[1])
+  dh1 = (dq @ w2.T) * (h1 > 0)
+  dh1dot = (dq @ w2dot.T) * (h1 > 0)
+  out[_HEAD + '/linear'] = {'w': flatdot.T @ dh1 + flat.T @ dh1dot,
+                            'b': dh1dot.sum(axis=0)}
+  dflat = dh1 @ w1.T
+  dflatdot = dh1dot @ w1.T + dh1 @ tw(_HEAD + '/linear').T
+  dy = dflat.reshape(cache['y2'].shape)
+  dydot = dflatdot.reshape(cache['y2'].shape)
+  for i in (2, 1, 0):
+    k, st, _, co = CONV_SPECS[i]
+    mask = cache['y%d' % i] > 0
+    dz, dzdot = dy * mask, dydot * mask
+    cols = cache['cols%d' % i].reshape(-1, cache['cols%d' % i].shape[-1])
+    gw = cols.T @ dzdot.reshape(-1, co)
+    if colsdot[i] is not None:
+      gw = gw + colsdot[i].reshape(-1, cols.shape[-1]).T @ dz.reshape(-1, co)
+    out[CONV_NAMES[i]] = {'w': gw.reshape(np.asarray(params[CONV_NAMES[i]]['w']).shape),
+                          'b': dzdot.reshape(-1, co).sum(axis=0)}
+    if i > 0:
+      w = pw(CONV_NAMES[i]).reshape(-1, co)
+      wdot = tw(CONV_NAMES[i]).reshape(-1, co)
+      x_shape = cache['y%d' % (i - 1)].shape
+      dy = _col2im(dz @ w.T, x_shape, k, st)
+      dydot = _col2im(dzdot @ w.T + dz @ wdot.T, x_shape, k, st)
+  return out
+
+
 def meta_update(online, target, mu, nu, meta, logits, online_transition,
                 adam_m, adam_v, adam_count, lr=2.5e-4, decay=0.95,
-                eps=0.01 / 32**2, grad_error_bound=1.0 / 32, meta_lr=2.5e-4):
+                eps=0.01 / 32**2, grad_error_bound=1.0 / 32, meta_lr=2.5e-4,
+                stop_gradient=True):
   """MGSCDqn.meta_update (dqn_mgsc_batched/agent.py:104-220), fp64.
 
   meta: dict(s_tm1 [M,84,84,4], a_tm1, r_t, discount_t, s_t) — the meta batch.
@@ -286,7 +353,36 @@ def meta_update(online, target, mu, nu, meta, logits, online_transition,
   jac = _tree_map(lambda g, m, n: rmsprop_update_jacobian(g, m, n, lr, decay,
                                                           eps),
                   big_g, _tree_map(np.asarray, mu), _tree_map(np.asarray, nu))
-  v = _tree_map(lambda u, j: -2.0 * u * j, u_p, jac)
+  if stop_gradient:
+    # dL/dtheta' = -2 u' (theta'' is a constant): v = -2 u' dtheta'/dG
+    v = _tree_map(lambda u, j: -2.0 * u * j, u_p, jac)
+  else:
+    # dqn_mgsc_batched_reservoir: L = sum u'^2 with u' = F(g'(theta'), mu', nu')
+    # and mu' = d mu + c G, nu' = d nu + c G^2 (theta' cancels in theta' - theta'').
+    #   dL/dG = 2u' (c dF/dmu' + 2 c G dF/dnu') + J (H w),  w = 2u' dF/dg',
+    #   dF/dg' = -lr D^{-3/2} (D - c g' (g' - mu'')),  D = nu'' - mu''^2 + eps,
+    #   c dF/dmu' + 2cG dF/dnu' = c d lr g' D^{-3/2} (G - mu''),
+    #   H = alpha grad q grad q^T - clip(td') hess q  (the online transition's
+    #   loss at theta', target theta; alpha = 1 inside the clip bound).
+    c, d = 1.0 - decay, decay
+    g_p = step2['grads']
+    mu_pp, nu_pp = step2['mu'], step2['nu']
+    dd = _tree_map(lambda m, n: n - m * m + eps, mu_pp, nu_pp)
+    v_dir = _tree_map(lambda u, g, dv, gg, m: 2.0 * u * c * d * lr * g * dv**-1.5 * (gg - m),
+                      u_p, g_p, dd, big_g, mu_pp)
+    w = _tree_map(lambda u, g, dv, m: 2.0 * u * (-lr) * dv**-1.5 * (dv - c * g * (g - m)),
+                  u_p, g_p, dd, mu_pp)
+    q1, cache1 = forward(theta_p, ot['s_tm1'])
+    e_a = np.zeros_like(q1)
+    e_a[0, int(np.asarray(ot['a_tm1']).reshape(-1)[0])] = 1.0
+    grad_q = backward(theta_p, cache1, e_a)
+    hess_q_w = hvp(theta_p, cache1, e_a, w)
+    td_p = float(np.asarray(step2['td']).reshape(-1)[0])
+    alpha = 1.0 if abs(td_p) < grad_error_bound else 0.0
+    clip_td = float(np.clip(td_p, -grad_error_bound, grad_error_bound))
+    s1 = _tree_dot(grad_q, w)
+    h_w = _tree_map(lambda gq, hq: alpha * s1 * gq - clip_td * hq, grad_q, hess_q_w)
+    v = _tree_map(lambda vd, j, hw: vd + j * hw, v_dir, jac, h_w)
   dp = np.array([_tree_dot(v, g) for g in per_example])
   dlogits = p * (dp - np.dot(p, dp))
   new_logits, m, vv, count = adam(np.asarray(logits, np.float64), dlogits,

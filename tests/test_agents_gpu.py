@@ -269,3 +269,34 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
       grad_error_bound=BOUND)
   after = replay.logits.cpu().numpy()
   np.testing.assert_allclose(after[positions], ref['new_logits'], atol=1e-6)
+
+
+def test_mgsc_reservoir_agent_run_loop(device):
+  """dqn_mgsc_batched_reservoir: reservoir logits replay + second-order meta."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import parts
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  from dqn_mgsc_zoo_amd.dqn_mgsc_batched_reservoir import agent as agent_lib
+  replay = rc.MGSCReservoirTransitionReplay(
+      96, rc.Transition(None, None, None, None, None), np.random.default_rng(7))
+  agent = agent_lib.MGSCDqn(
+      preprocessor=fake_env.FrameStacker(),
+      sample_network_input=np.zeros((84, 84, 4), np.uint8),
+      network=networks.dqn_atari_network(6),
+      optimizer=learner_lib.rmsprop(LR, DECAY, EPS, centered=True),
+      transition_accumulator=rc.TransitionAccumulator(), replay=replay,
+      batch_size=32,
+      exploration_epsilon=parts.LinearSchedule(
+          begin_t=40, decay_steps=200, begin_value=1.0, end_value=0.1),
+      min_replay_capacity_fraction=0.25, learn_period=4,
+      target_network_update_period=40, grad_error_bound=BOUND,
+      rng_key=np.array([0, 7], np.uint32),
+      meta_optimizer=learner_lib.adam(2.5e-4), meta_batch_size=16)
+  assert agent.meta_learner.second_order
+  _run(agent, 200)
+  assert replay.size == replay.capacity
+  assert agent.meta_learner.get_state()['count'] > 10
+  lg = replay.logits.cpu().numpy()
+  assert np.isfinite(lg).all()
+  assert torch.isfinite(agent.learner.online).all()

@@ -134,3 +134,54 @@ def test_meta_update_matches_oracle(device, meta_batch):
   state = meta.get_state()
   assert state['count'] == 3
   np.testing.assert_allclose(state['mu'], ref['adam_m'], atol=2e-3 * scale)
+
+
+@pytest.mark.parametrize('bound', [5.0, 1.0 / 32])
+def test_second_order_meta_update_matches_oracle(device, bound):
+  """dqn_mgsc_batched_reservoir: no stop_gradient on theta'' (HVP path)."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  a, meta_batch = 6, 8
+  net = networks.dqn_atari_network(a)
+  online = net.init(51)
+  target = helpers.perturbed_tree(online, 52)
+  mu, nu = _rand_opt_state(online, 53)
+  lrn = learner_lib.Learner(net, 32, algo='dqn', grad_error_bound=bound)
+  lrn.set_params(online, target)
+  lrn.set_opt_state(mu, nu)
+  meta = learner_lib.MetaLearner(lrn, meta_batch, learner_lib.adam(2.5e-4),
+                                 second_order=True)
+  rng = np.random.default_rng(54)
+  capacity = 128
+  st, host = _store(capacity, 320, a, 55, device)
+  slots = rng.choice(capacity, meta_batch, replace=False).astype(np.int32)
+  logits = rng.standard_normal(64).astype(np.float32)
+  pos = rng.choice(64, meta_batch, replace=False).astype(np.int32)
+  ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot = replay_lib.Transition(ot_tm1, 2, 1.0, 0.99, ot_t)
+  mb = dict(s_tm1=helpers.stacks_from(host['frames'], host['fidx'], slots, 0),
+            a_tm1=host['action'][slots], r_t=host['reward'][slots],
+            discount_t=host['discount'][slots],
+            s_t=helpers.stacks_from(host['frames'], host['fidx'], slots, 1))
+  ref = learner_ref.meta_update(
+      _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
+      dict(s_tm1=ot_tm1, a_tm1=2, r_t=1.0, discount_t=0.99, s_t=ot_t),
+      np.zeros(meta_batch), np.zeros(meta_batch), 0, grad_error_bound=bound,
+      stop_gradient=False)
+  first = learner_ref.meta_update(
+      _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
+      dict(s_tm1=ot_tm1, a_tm1=2, r_t=1.0, discount_t=0.99, s_t=ot_t),
+      np.zeros(meta_batch), np.zeros(meta_batch), 0, grad_error_bound=bound)
+  meta.set_online_transition(ot)
+  logits_d = torch.from_numpy(logits).to(device)
+  meta.update(st, torch.from_numpy(slots).to(device), logits_d,
+              torch.from_numpy(pos).to(device))
+  probs, dlogits, td, loss = [t.cpu().numpy() for t in meta.fetch_outputs()]
+  np.testing.assert_allclose(probs, ref['probs'], rtol=1e-5)
+  np.testing.assert_allclose(loss[0], ref['loss'], rtol=2e-3)
+  scale = np.abs(ref['dlogits']).max()
+  np.testing.assert_allclose(dlogits, ref['dlogits'], atol=2e-3 * scale)
+  # and the second-order answer is not the first-order one
+  assert np.abs(ref['dlogits'] - first['dlogits']).max() > 0.05 * scale

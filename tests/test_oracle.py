@@ -213,3 +213,101 @@ def test_oracle_meta_update_matches_torch_autograd():
   want = logits - 2.5e-4 * (mm / (1 - b1**4)) / (np.sqrt(vv / (1 - b2**4)) + 1e-8)
   np.testing.assert_allclose(ref['new_logits'], want, rtol=1e-12)
   assert ref['adam_count'] == 4
+
+
+def test_oracle_hvp_matches_torch_double_backward():
+  a = 6
+  params = _init(a, False, 31)
+  rng = np.random.default_rng(32)
+  s = rng.integers(0, 256, (1, 84, 84, 4), dtype=np.uint8)
+  tangent = {m: {n: rng.standard_normal(np.shape(v)) for n, v in d.items()}
+             for m, d in params.items()}
+  q, cache = learner_ref.forward(params, s)
+  e = np.zeros_like(q)
+  e[0, 4] = 1.0
+  got = learner_ref.hvp(params, cache, e, tangent)
+  keys = [(m, n) for m in params for n in params[m]]
+  tp = {k: torch.tensor(params[k[0]][k[1]], dtype=torch.float64, requires_grad=True) for k in keys}
+  tree = {}
+  for (m, n), v in tp.items():
+    tree.setdefault(m, {})[n] = v
+  qt = _torch_q(tree, s, False)[0, 4]
+  gs = torch.autograd.grad(qt, [tp[k] for k in keys], create_graph=True)
+  dot = sum((g * torch.tensor(tangent[k[0]][k[1]])).sum() for g, k in zip(gs, keys))
+  hs = torch.autograd.grad(dot, [tp[k] for k in keys], allow_unused=True)
+  for h, k in zip(hs, keys):
+    want = np.zeros(np.shape(params[k[0]][k[1]])) if h is None else h.numpy()
+    np.testing.assert_allclose(got[k[0]][k[1]], want, rtol=1e-8,
+                               atol=1e-10 * (1 + np.abs(want).max()), err_msg=str(k))
+
+
+def test_oracle_second_order_meta_update_matches_torch_autograd():
+  """dqn_mgsc_batched_reservoir/agent.py: meta_loss_fn without stop_gradient
+  on theta'' -- autograd differentiates through g'(theta') (double backward)."""
+  a, m_size = 6, 3
+  online = _init(a, False, 41)
+  target = helpers.perturbed_tree(online, 42)
+  rng = np.random.default_rng(43)
+  meta = dict(s_tm1=rng.integers(0, 256, (m_size, 84, 84, 4), dtype=np.uint8),
+              a_tm1=rng.integers(0, a, m_size),
+              r_t=np.array([1.0, 0.0, -1.0]),
+              discount_t=np.array([0.99, 0.99, 0.0]),
+              s_t=rng.integers(0, 256, (m_size, 84, 84, 4), dtype=np.uint8))
+  ot = dict(s_tm1=rng.integers(0, 256, (84, 84, 4), dtype=np.uint8), a_tm1=1,
+            r_t=0.5, discount_t=0.99,
+            s_t=rng.integers(0, 256, (84, 84, 4), dtype=np.uint8))
+  mu = {m: {n: 1e-3 * rng.standard_normal(np.shape(v)) for n, v in d.items()}
+        for m, d in online.items()}
+  nu = {m: {n: mu[m][n]**2 + 1e-6 * rng.random(np.shape(v))
+            for n, v in d.items()} for m, d in mu.items()}
+  logits = rng.standard_normal(m_size).astype(np.float32)
+  lr, decay, eps = 2.5e-4, 0.95, 0.01 / 32**2
+  for bound in (5.0, 1e-3):  # online TD inside / outside the clip bound
+    ref = learner_ref.meta_update(online, target, mu, nu, meta, logits, ot,
+                                  np.zeros(m_size), np.zeros(m_size), 0, lr=lr,
+                                  decay=decay, eps=eps, grad_error_bound=bound,
+                                  stop_gradient=False)
+    keys = [(m, n) for m in online for n in online[m]]
+
+    def tree(flat):
+      out = {}
+      for (m, n), v in flat.items():
+        out.setdefault(m, {})[n] = v
+      return out
+
+    th = {k: torch.tensor(online[k[0]][k[1]], dtype=torch.float64) for k in keys}
+    tt = {k: torch.tensor(target[k[0]][k[1]], dtype=torch.float64) for k in keys}
+
+    def loss_of(params, tparams, s_tm1, act, r, d, s_t):
+      q = _torch_q(tree(params), s_tm1[None], False)
+      with torch.no_grad():
+        v = _torch_q(tree(tparams), s_t[None], False).max(dim=1).values
+      td = (r + d * v) - q[0, act]
+      return (0.5 * _ClipGrad.apply(td, -bound, bound)**2).mean()
+
+    x = torch.tensor(logits, dtype=torch.float64, requires_grad=True)
+    c = x.max()
+    probs = torch.exp(x - (c + torch.log(torch.sum(torch.exp(x - c)))))
+    per = []
+    for i in range(m_size):
+      p = {k: v.clone().requires_grad_(True) for k, v in th.items()}
+      li = loss_of(p, tt, meta['s_tm1'][i], meta['a_tm1'][i], meta['r_t'][i],
+                   meta['discount_t'][i], meta['s_t'][i])
+      per.append(dict(zip(keys, torch.autograd.grad(li, [p[k] for k in keys]))))
+    big_g = {k: sum(probs[i] * per[i][k] for i in range(m_size)) for k in keys}
+    th_p, mu_p, nu_p = {}, {}, {}
+    for k in keys:
+      th_p[k], mu_p[k], nu_p[k] = _torch_rms(th[k], big_g[k], torch.tensor(mu[k[0]][k[1]]),
+                                             torch.tensor(nu[k[0]][k[1]]), lr, decay, eps)
+    l2 = loss_of(th_p, th, ot['s_tm1'], ot['a_tm1'], ot['r_t'], ot['discount_t'], ot['s_t'])
+    g2 = dict(zip(keys, torch.autograd.grad(l2, [th_p[k] for k in keys], create_graph=True)))
+    loss = 0.0
+    for k in keys:
+      th_pp, _, _ = _torch_rms(th_p[k], g2[k], mu_p[k], nu_p[k], lr, decay, eps)
+      loss = loss + torch.sum((th_p[k] - th_pp)**2)
+    loss.backward()
+    np.testing.assert_allclose(ref['loss'], loss.item(), rtol=1e-9)
+    want = x.grad.numpy()
+    np.testing.assert_allclose(ref['dlogits'], want, rtol=1e-6,
+                               atol=1e-6 * np.abs(want).max(), err_msg='bound=%g' % bound)
+    assert np.abs(want).max() > 0
