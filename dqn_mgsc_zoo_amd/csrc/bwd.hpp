@@ -500,6 +500,22 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   const int n = lane & 15, kq = lane >> 4;
   const int kb = blk >> 2, nq = blk & 3;
   const int k0 = 16 * kb, c0 = 128 * nq;
+  // RMSProp operands of this lane's 8 entries (C layout: row 4 kq + r, column
+  // 32 w + 16 q + n), issued first so their HBM latency hides under the GEMM.
+  const Rms& R = a.rms;
+  const bool upd = R.gout == nullptr;
+  float o_th[8], o_mu[8], o_nu[8];
+  if (upd) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
+        o_th[4 * q + r] = a.th[e];
+        o_mu[4 * q + r] = a.mu[e];
+        o_nu[4 * q + r] = a.nu[e];
+      }
+  }
   f32x4 gacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   for (int c = 0; c < a.B; c += 32) {
     if (c > 0) __syncthreads();
@@ -532,20 +548,6 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   }
   DQZ_STAMP(11, 2);
   // C layout: row = 4 kq + r, col = n of tile q -> W1[k0 + 4 kq + r][c0 + 32 w + 16 q + n]
-  const Rms& R = a.rms;
-  const bool upd = R.gout == nullptr;
-  float o_th[8], o_mu[8], o_nu[8];
-  if (upd) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
-        o_th[4 * q + r] = a.th[e];
-        o_mu[4 * q + r] = a.mu[e];
-        o_nu[4 * q + r] = a.nu[e];
-      }
-  }
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll

@@ -52,14 +52,7 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   int a_tm1 = 0;
   float r = 0.f, d = 0.f, w = 1.f, pm = 0.f;
   if (h.advance && b == 0 && n == 0) *h.advance += 1;  // every conv1 block has read it
-  if (!h.fwd_only && n == 0) {
-    const int slot = h.slots[b];
-    a_tm1 = h.action[slot];
-    r = h.reward[slot];
-    d = h.discount[slot];
-    if (h.weights) w = h.weights[b];
-    if (h.meta_p) pm = h.meta_p[b];
-  }
+  const int slot = !h.fwd_only ? h.slots[b] : 0;  // uniform load, in flight with the partials
   float pv[3][SMAX], b1v[3], w2v[3][AMAX];
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
@@ -71,6 +64,13 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
     const float* w2 = h.nz.p[zc] + h.w2_off + n * A;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) w2v[z][a] = w2[min(a, A - 1)];
+  }
+  if (!h.fwd_only && n == 0) {  // second hop of the batch record chain, needed only for the TD
+    a_tm1 = h.action[slot];
+    r = h.reward[slot];
+    d = h.discount[slot];
+    if (h.weights) w = h.weights[b];
+    if (h.meta_p) pm = h.meta_p[b];
   }
   float h0 = 0.f;
   DQZ_STAMP(4, 1);

@@ -279,7 +279,7 @@ def test_mgsc_reservoir_agent_run_loop(device):
   from dqn_mgsc_zoo_amd import replay_circular as rc
   from dqn_mgsc_zoo_amd.dqn_mgsc_batched_reservoir import agent as agent_lib
   replay = rc.MGSCReservoirTransitionReplay(
-      96, rc.Transition(None, None, None, None, None), np.random.default_rng(7))
+      160, rc.Transition(None, None, None, None, None), np.random.default_rng(7))
   agent = agent_lib.MGSCDqn(
       preprocessor=fake_env.FrameStacker(),
       sample_network_input=np.zeros((84, 84, 4), np.uint8),
@@ -294,7 +294,7 @@ def test_mgsc_reservoir_agent_run_loop(device):
       rng_key=np.array([0, 7], np.uint32),
       meta_optimizer=learner_lib.adam(2.5e-4), meta_batch_size=16)
   assert agent.meta_learner.second_order
-  _run(agent, 200)
+  _run(agent, 260)
   assert replay.size == replay.capacity
   assert agent.meta_learner.get_state()['count'] > 10
   lg = replay.logits.cpu().numpy()
