@@ -182,3 +182,34 @@ def test_fused_uniform_step_matches_sample_then_step(device):
   assert int(c1.item()) == int(c2.item()) == 3
   for which in ('online', 'mu', 'nu'):
     assert torch.equal(getattr(lrn, which), getattr(lrn2, which))
+
+
+@pytest.mark.parametrize('algo,batch,num_actions', [
+    ('dqn', 1, 6), ('dqn', 20, 18), ('double', 48, 4), ('per', 40, 18)])
+def test_learner_step_odd_shapes(device, algo, batch, num_actions):
+  """Batches that are not multiples of the 8-XCD / 16-row / 32-row tilings,
+  and the full 18-action set (head kernel AMAX 32 path)."""
+  net, lrn, st, host, online, target, mu, nu = _setup(
+      algo, batch, capacity=96, num_frames=260, num_actions=num_actions,
+      seed=31 + batch)
+  rng = np.random.default_rng(batch)
+  slots = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+  weights = None
+  if algo == 'per':
+    weights = rng.uniform(0.2, 1.0, size=batch).astype(np.float32)
+  s_tm1 = helpers.stacks_from(host['frames'], host['fidx'], slots, 0)
+  s_t = helpers.stacks_from(host['frames'], host['fidx'], slots, 1)
+  ref = learner_ref.learner_step(
+      online, target, mu, nu, s_tm1, host['action'][slots],
+      host['reward'][slots], host['discount'][slots], s_t, algo=algo,
+      weights=weights)
+  lrn.step(st, torch.from_numpy(slots).to(device),
+           None if weights is None else torch.from_numpy(weights).to(device))
+  q, td, loss = lrn.fetch_outputs()
+  np.testing.assert_allclose(q.cpu().numpy(), ref['q_tm1'], atol=Q_ATOL)
+  np.testing.assert_allclose(td.cpu().numpy(), ref['td'], atol=Q_ATOL)
+  _compare_tree(lrn.params_tree('online'), ref['params'], P_ATOL, what='params')
+  # actor path at the same odd batch: q-values of s_t through dqz_forward
+  q_t = lrn.q_values(torch.from_numpy(s_t).to(device))
+  q_ref, _ = learner_ref.forward(ref['params'], s_t, algo != 'dqn')
+  np.testing.assert_allclose(q_t.cpu().numpy(), q_ref, atol=Q_ATOL)
