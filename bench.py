@@ -58,6 +58,67 @@ def phase_flops(algo, batch):
   }
 
 
+# f32 bytes of one sample's activations / uint8 bytes of one stacked state.
+ACT = dict(state=84 * 84 * 4, y1=4 * 32 * 20 * 20, y2=4 * 64 * 9 * 9,
+           y3=4 * 64 * 7 * 7, h=4 * 512)
+PARAM = dict(conv1=4 * (8 * 8 * 4 * 32 + 32), conv2=4 * (4 * 4 * 32 * 64 + 64),
+             conv3=4 * (3 * 3 * 64 * 64 + 64), fc1=4 * (3136 * 512 + 512),
+             fc2=4 * (512 * NUM_ACTIONS + NUM_ACTIONS))
+
+
+def phase_bytes(algo, batch):
+  """Algorithmic HBM bytes of each libdqz phase (one launch each).
+
+  Every tensor the phase consumes is read once and every tensor it produces
+  is written once; implementation scratch (split-K partials, per-sample dW
+  partials) is excluded.  Centered RMSProp reads and writes theta, mu, nu
+  (6 x 4 B per parameter); fc1's update runs inside conv3_dx+fc1_dw.
+  """
+  z = 2 if algo == 'dqn' else 3
+  b = batch
+  rms = 6 * (sum(PARAM.values()) - PARAM['fc1'])
+  return {
+      'conv1_fwd': z * b * (ACT['state'] + ACT['y1']) + z * PARAM['conv1'],
+      'conv2_fwd': z * b * (ACT['y1'] + ACT['y2']) + z * PARAM['conv2'],
+      'conv3_fwd': z * b * (ACT['y2'] + ACT['y3']) + z * PARAM['conv3'],
+      'fc1_fwd': z * b * (ACT['y3'] + ACT['h']) + z * PARAM['fc1'],
+      'head': z * b * ACT['h'] + z * PARAM['fc2'],
+      'fc1_dx': b * (ACT['h'] + 2 * ACT['y3']) + PARAM['fc1'],
+      'conv3_dx+fc1_dw': (b * (ACT['y3'] + 2 * ACT['y2']) + PARAM['conv3'] +
+                          b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
+      'conv2_dx+conv3_dw': (b * (ACT['y2'] + 2 * ACT['y1']) + PARAM['conv2'] +
+                            b * (ACT['y2'] + ACT['y3']) + PARAM['conv3']),
+      'conv1_dw+conv2_dw': (b * (ACT['state'] + ACT['y1']) + PARAM['conv1'] +
+                            b * (ACT['y1'] + ACT['y2']) + PARAM['conv2']),
+      'update': rms,
+  }
+
+
+# libdqz phase -> kernel symbol (rocprofv3 names, template args stripped).
+PHASE_KERNEL = {
+    'conv1_fwd': 'conv1_fwd_kernel', 'conv2_fwd': 'conv2_fwd_kernel',
+    'conv3_fwd': 'conv3_fwd_kernel', 'fc1_fwd': 'fc1_fwd_kernel',
+    'head': 'head_kernel', 'fc1_dx': 'fc1_dx_kernel',
+    'conv3_dx+fc1_dw': 'bwd_b_kernel', 'conv2_dx+conv3_dw': 'bwd_c_kernel',
+    'conv1_dw+conv2_dw': 'bwd_d_kernel', 'update': 'update_kernel'}
+PMC_JSON = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+
+
+def pmc_traffic(phase):
+  """Measured fabric bytes per launch of `phase`'s kernel, or None.
+
+  From the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+  (profiles/run_pmc.sh + pmc_summary.py, gfx950 FETCH_SIZE doubled).
+  """
+  try:
+    with open(PMC_JSON) as f:
+      rec = json.load(f).get(PHASE_KERNEL[phase], {})
+  except (OSError, ValueError):
+    return None
+  t = rec.get('traffic_bytes')
+  return None if t is None else int(t)
+
+
 def cpu_baseline(seconds, algo):
   """Times the oracle's fp64 learner step (a CPU *port*) on this host."""
   from threadpoolctl import threadpool_info, threadpool_limits  # pylint: disable=g-import-not-at-top
@@ -196,19 +257,28 @@ def main():
 
   value = world * steps / elapsed_max
   flops = phase_flops(algo, BATCH)
+  nbytes = phase_bytes(algo, BATCH)
   dom = max(phases, key=phases.get)
   dom_ms = phases[dom]
-  if flops[dom] > 0:
-    achieved = flops[dom] / (dom_ms * 1e-3) / 1e12
-    roof = {'bound': 'mfma', 'achieved': round(achieved, 3),
+  # The bound is whichever roof the kernel sits closer to.
+  tflops = flops[dom] / (dom_ms * 1e-3) / 1e12
+  gbs = nbytes[dom] / (dom_ms * 1e-3) / 1e9
+  mfma_frac = tflops / F32_MFMA_PEAK_TFLOPS
+  hbm_frac = gbs / HBM_PEAK_GBS
+  if mfma_frac >= hbm_frac:
+    roof = {'bound': 'mfma', 'achieved': round(tflops, 3),
             'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(achieved / F32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
-            'kernel': dom, 'kernel_ms': round(dom_ms, 5),
-            'algorithmic_flop_per_launch': flops[dom]}
+            'frac': round(mfma_frac, 4)}
   else:
-    roof = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': None, 'traffic': None, 'kernel': dom,
-            'kernel_ms': round(dom_ms, 5)}
+    roof = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(hbm_frac, 4)}
+  roof.update({
+      'traffic': pmc_traffic(dom) if algo == 'dqn' else None,
+      'kernel': PHASE_KERNEL[dom] + ' (' + dom + ')',
+      'kernel_ms': round(dom_ms, 5),
+      'algorithmic_flop_per_launch': flops[dom],
+      'algorithmic_bytes_per_launch': nbytes[dom],
+      'mfma_frac': round(mfma_frac, 4), 'hbm_frac': round(hbm_frac, 4)})
   per_gpu = steps / elapsed
   step_tflops = STEP_FLOP[algo] * per_gpu / 1e12
   step_gbs = STEP_BYTES[algo] * per_gpu / 1e9

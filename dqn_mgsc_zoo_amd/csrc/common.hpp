@@ -12,6 +12,10 @@
 
 namespace dqz {
 
+// MFMA operand / accumulator vectors (v_mfma_f32_16x16x4f32 / 32x32x2f32).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 // ---------------------------------------------------------------------------
 // errors (thread-local message behind dqz_last_error)
 

@@ -10,7 +10,6 @@
 // ds_read_b32 at compile-time immediate offsets.  Stacks never exist in HBM.
 #pragma once
 #include "common.hpp"
-#include "gemm.hpp"
 
 namespace dqz {
 

@@ -18,7 +18,6 @@
 // Work per launch: Z x B x 4 workgroups (256 at B = 32, Z = 2).
 #pragma once
 #include "common.hpp"
-#include "gemm.hpp"
 
 namespace dqz {
 

@@ -3,12 +3,12 @@
 // One step (dqn/agent.py:109-119, prioritized/agent.py:115-127), in launch order:
 //   0 conv1 fwd  (frame gather + /255 fused; z = online(s_tm1), target(s_t)
 //                 [, online(s_t) for double-Q])                  conv1.hpp
-//   1 conv2 fwd  2 conv3 fwd  3 fc1 fwd (split-K)                gemm.hpp ops
+//   1 conv2 fwd  2 conv3 fwd  3 fc1 fwd (split-K)                fwd.hpp
 //   4 head: fc1 reduce + fc2 + TD loss + dq + dz1, per sample    head.hpp
-//   5 fc1 dX -> dy3
-//   6 {conv3 dX -> dy2, conv3 dW partials, fc1 dW + fused RMSProp}
-//   7 {conv2 dX (stride-phase split) -> dy1, conv2 dW partials}
-//   8 conv1 dW partials (frame gather fused)                      conv1.hpp
+//   5 fc1 dX -> dy3                                              bwd.hpp
+//   6 {conv3 dX -> dy2, fc1 dW + fused RMSProp}                  bwd_b_kernel
+//   7 {conv2 dX (stride-phase split) -> dy1, conv3 dW partials}  bwd_c_kernel
+//   8 {conv1 dW partials (frame gather fused), conv2 dW partials} bwd_d_kernel
 //   9 reduce of every cross-sample / split-K gradient + centered RMSProp
 #include <hip/hip_runtime.h>
 
@@ -17,7 +17,6 @@
 
 #include "common.hpp"
 #include "conv1.hpp"
-#include "gemm.hpp"
 #include "fwd.hpp"
 #include "bwd.hpp"
 #include "head.hpp"
@@ -39,181 +38,6 @@ static void param_layout(int A, int shared_bias, int64_t off[10], int64_t sz[10]
   *total = o;
 }
 
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ float4 zero_unless(bool ok, float4 v) {
-  v.x = ok ? v.x : 0.f;
-  v.y = ok ? v.y : 0.f;
-  v.z = ok ? v.z : 0.f;
-  v.w = ok ? v.w : 0.f;
-  return v;
-}
-
-// ---------------------------------------------------------------------------
-// forward ops (gemm engine)
-
-// VALID conv over an NHWC f32 input (conv2, conv3) + bias + ReLU.
-// m = (b, oh, ow), k = (kh, kw, ci) (HWIO order), n = co.
-template <int IH, int CI, int KH, int S, int CO, int OH>
-struct ConvFwd : Shape {
-  static constexpr bool kAFastK = true, kBFastK = false;
-  const float* in;  // [Z][B][IH][IH][CI]
-  int B;
-  int linear;  // 1: pre-activation output (no ReLU)
-  NetZ nz;
-  int64_t w_off, b_off;
-  float* out;  // [Z][B*OH*OH][CO]
-  __device__ __forceinline__ const float* a_ptr(const TileCoord& tc, int m, int k) const {
-    const int b = m / (OH * OH), p = m % (OH * OH), oh = p / OH, ow = p % OH;
-    const int kh = k / (KH * CI), r = k % (KH * CI), kw = r / CI, ci = r % CI;
-    return in + ((((int64_t)tc.z * B + b) * IH + oh * S + kh) * IH + ow * S + kw) * CI + ci;
-  }
-  __device__ float4 a4(const TileCoord& tc, int m, int k) const { return ld4(a_ptr(tc, m, k)); }
-  __device__ float4 b4(const TileCoord& tc, int k, int n) const { return ld4(nz.p[tc.z] + w_off + k * CO + n); }
-  __device__ void store(const TileCoord& tc, int m, int n, float v) const {
-    const float y = v + nz.p[tc.z][b_off + n];
-    out[((int64_t)tc.z * M + m) * CO + n] = linear ? y : relu(y);
-  }
-};
-using Conv2Fwd = ConvFwd<C1O, C1CO, C2K, C2S, C2CO, C2O>;
-using Conv3Fwd = ConvFwd<C2O, C2CO, C3K, 1, C3CO, C3O>;
-
-// fc1 3136->512, split-K partial sums (bias/ReLU applied by the head).
-struct Fc1Fwd : Shape {
-  static constexpr bool kAFastK = true, kBFastK = false;
-  const float* in;  // [Z][B][3136]
-  NetZ nz;
-  int64_t w_off;
-  float* part;  // [Z][S][B][512]
-  __device__ float4 a4(const TileCoord& tc, int m, int k) const { return ld4(in + ((int64_t)tc.z * M + m) * FLAT + k); }
-  __device__ float4 b4(const TileCoord& tc, int k, int n) const {
-    return ld4(nz.p[tc.z] + w_off + (int64_t)k * HID + n);
-  }
-  __device__ void store(const TileCoord& tc, int m, int n, float v) const {
-    part[(((int64_t)tc.z * g.S + tc.split) * M + m) * HID + n] = v;
-  }
-};
-
-// ---------------------------------------------------------------------------
-// backward ops (online copy, z = 0 activations)
-
-// dflat = dz1 @ W1^T, masked by ReLU'(conv3) -> dy3
-struct Fc1Dx : Shape {
-  static constexpr bool kAFastK = true, kBFastK = true;
-  const float* dz1;  // [B][512]
-  const float* w1;   // online W1 [3136][512]
-  const float* y3;   // [B][3136] online conv3 output
-  float* dy3;
-  __device__ float4 a4(const TileCoord&, int m, int k) const { return ld4(dz1 + m * HID + k); }
-  __device__ float4 b4(const TileCoord&, int k, int n) const { return ld4(w1 + (int64_t)n * HID + k); }
-  __device__ void store(const TileCoord&, int m, int n, float v) const {
-    const int64_t i = (int64_t)m * FLAT + n;
-    dy3[i] = y3[i] > 0.f ? v : 0.f;
-  }
-};
-
-// dW1 = flat^T @ dz1 (K = B), centered RMSProp applied in the epilogue: the
-// W1 gradient (6.4 MB, 95% of the parameters) never touches HBM.
-struct Fc1DwRms : Shape {
-  static constexpr bool kAFastK = false, kBFastK = false;
-  const float* y3;   // [B][3136]
-  const float* dz1;  // [B][512]
-  float *th, *mu, *nu;
-  int64_t w_off;
-  Rms rms;
-  __device__ float4 a4(const TileCoord&, int m, int k) const { return ld4(y3 + (int64_t)k * FLAT + m); }
-  __device__ float4 b4(const TileCoord&, int k, int n) const { return ld4(dz1 + k * HID + n); }
-  __device__ void store(const TileCoord&, int m, int n, float v) const {
-    rms.apply(th, mu, nu, w_off + (int64_t)m * HID + n, v);
-  }
-};
-
-// conv3 dX (stride 1): da2[b,ih,iw,ci] = sum_{kh,kw,co} dy3[b,ih-kh,iw-kw,co] W3[kh,kw,ci,co]
-struct Conv3Dx : Shape {
-  static constexpr bool kAFastK = true, kBFastK = true;
-  const float* dy3;  // [B][7][7][64]
-  const float* w3;   // online conv3 w [3][3][64][64]
-  const float* y2;   // [B][9][9][64]
-  float* dy2;
-  __device__ float4 a4(const TileCoord&, int m, int k) const {
-    const int b = m / C2M, p = m % C2M, ih = p / C2O, iw = p % C2O;
-    const int kh = k / (C3K * C3CO), r = k % (C3K * C3CO), kw = r / C3CO, co = r % C3CO;
-    const int oh = ih - kh, ow = iw - kw;
-    const bool ok = oh >= 0 && ow >= 0 && oh < C3O && ow < C3O;
-    const int ohc = ok ? oh : 0, owc = ok ? ow : 0;
-    return zero_unless(ok, ld4(dy3 + ((b * C3O + ohc) * C3O + owc) * C3CO + co));
-  }
-  __device__ __forceinline__ const float* b_ptr(int k, int n) const {
-    const int kk = k / C3CO, co = k % C3CO;  // kk = kh*3+kw
-    return w3 + (kk * C3CI + n) * C3CO + co;
-  }
-  __device__ float4 b4(const TileCoord&, int k, int n) const { return ld4(b_ptr(k, n)); }
-  __device__ void store(const TileCoord&, int m, int n, float v) const {
-    const int64_t i = (int64_t)m * C3CI + n;
-    dy2[i] = y2[i] > 0.f ? v : 0.f;
-  }
-};
-
-// conv2 dX (stride 2, kernel 4), split into the 4 output-parity phases so no
-// zero taps are multiplied: for ih = 2*ih2 + ph only kh in {ph, ph+2} hit.
-//   z = phase (ph, pw); m = (b, ih2, iw2) over 10x10; k = (jh, jw, co).
-struct Conv2DxPhased : Shape {
-  static constexpr bool kAFastK = true, kBFastK = true;
-  const float* dy2;  // [B][9][9][64]
-  const float* w2;   // online conv2 w [4][4][32][64]
-  const float* y1;   // [B][20][20][32]
-  float* dy1;
-  __device__ float4 a4(const TileCoord&, int m, int k) const {
-    const int b = m / 100, p = m % 100, ih2 = p / 10, iw2 = p % 10;
-    const int jh = k >> 7, jw = (k >> 6) & 1, co = k & 63;
-    const int oh = ih2 - jh, ow = iw2 - jw;
-    const bool ok = oh >= 0 && ow >= 0 && oh < C2O && ow < C2O;
-    const int ohc = ok ? oh : 0, owc = ok ? ow : 0;
-    return zero_unless(ok, ld4(dy2 + ((b * C2O + ohc) * C2O + owc) * C2CO + co));
-  }
-  __device__ __forceinline__ const float* b_ptr(const TileCoord& tc, int k, int n) const {
-    const int ph = tc.z >> 1, pw = tc.z & 1;
-    const int jh = k >> 7, jw = (k >> 6) & 1, co = k & 63;
-    const int kh = ph + 2 * jh, kw = pw + 2 * jw;
-    return w2 + ((kh * C2K + kw) * C2CI + n) * C2CO + co;
-  }
-  __device__ float4 b4(const TileCoord& tc, int k, int n) const { return ld4(b_ptr(tc, k, n)); }
-  __device__ void store(const TileCoord& tc, int m, int n, float v) const {
-    const int ph = tc.z >> 1, pw = tc.z & 1;
-    const int b = m / 100, p = m % 100, ih = 2 * (p / 10) + ph, iw = 2 * (p % 10) + pw;
-    const int64_t i = (((int64_t)b * C1O + ih) * C1O + iw) * C1CO + n;
-    dy1[i] = y1[i] > 0.f ? v : 0.f;
-  }
-};
-
-// conv dW (+ bias as an extra row of ones), split-K partials:
-//   P[s][kidx][co] = sum_{positions in split s} col(pos, kidx) * dy(pos, co)
-template <int IH, int CI, int KH, int S, int CO, int OH>
-struct ConvDw : Shape {
-  static constexpr bool kAFastK = false, kBFastK = false;
-  static constexpr int KK = KH * KH * CI;
-  const float* in;  // layer input (online) [B][IH][IH][CI]
-  const float* dy;  // [B*OH*OH][CO]
-  float* part;      // [S][KK+1][CO]
-  __device__ __forceinline__ const float* a_ptr(int m, int k) const {
-    const int kh = m / (KH * CI), r = m % (KH * CI), kw = r / CI, ci = r % CI;
-    const int b = k / (OH * OH), p = k % (OH * OH), oh = p / OH, ow = p % OH;
-    return in + (((int64_t)b * IH + oh * S + kh) * IH + ow * S + kw) * CI + ci;
-  }
-  // Quads along m start at multiples of 4 and KK % 4 == 0: the quad at
-  // m == KK is the bias row (1, 0, 0, 0); its load is clamped into the weights.
-  __device__ float4 a4(const TileCoord&, int m, int k) const {
-    const bool bias = m >= KK;
-    const float4 v = ld4(a_ptr(bias ? KK - 4 : m, k));
-    return bias ? make_float4(1.f, 0.f, 0.f, 0.f) : v;
-  }
-  __device__ float4 b4(const TileCoord&, int k, int n) const { return ld4(dy + (int64_t)k * CO + n); }
-  __device__ void store(const TileCoord& tc, int m, int n, float v) const {
-    part[((int64_t)tc.split * (KK + 1) + m) * CO + n] = v;
-  }
-};
-using Conv3Dw = ConvDw<C2O, C2CO, C3K, 1, C3CO, C3O>;
-using Conv2Dw = ConvDw<C1O, C1CO, C2K, C2S, C2CO, C2O>;
-
 }  // namespace dqz
 
 // ---------------------------------------------------------------------------
@@ -230,13 +54,6 @@ struct dqz_learner {
   int32_t* ga;
   void* block;
 };
-
-// tile configurations
-using CfgConv = Cfg<32, 64, 32, 2, 2>;
-using CfgFc1 = Cfg<32, 64, 32, 2, 2>;
-using CfgFc1Dx = Cfg<32, 32, 32, 2, 2>;
-using CfgBwd2 = Cfg<64, 64, 32, 2, 2, 2>;
-using CfgBwd3 = Cfg<64, 32, 32, 4, 1>;
 
 static int g_attr_done = 0;
 
