@@ -25,7 +25,7 @@ from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, syntheti
 NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
          6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*'}
 ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
-K, NB, NS = 16, 1024, 4
+K, NB, NS = 16, 2048, 4
 
 dev = torch.device('cuda:0')
 net = networks.dqn_atari_network(6)
@@ -83,5 +83,8 @@ for k in ORDER:
   print('%-10s %8.2f %8.2f %8.2f | %8.2f %8.2f %8.2f %8d  [%.2f .. %.2f]' % (
       NAMES[k], gap, (end - start) / 100, np.median(s3 - s0) / 100, med(0, 1), med(1, 2), med(2, 3), live.sum(),
       (start - t0) / 100, (end - t0) / 100))
+  if os.environ.get('PCT'):  # start / end percentiles 0, 10, 50, 90, 100
+    q = lambda a: ' '.join('%.2f' % ((np.percentile(a, p) - t0) / 100) for p in (0, 10, 50, 90, 100))
+    print('%10s start %s | end %s' % ('', q(s0), q(s3)))
   if not NAMES[k].endswith('*'):
     prev_end = end
