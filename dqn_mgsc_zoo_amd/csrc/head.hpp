@@ -171,77 +171,143 @@ struct UpdArgs {
   Rms rms;
 };
 
-constexpr int UPD_PARAMS = 32;  // parameters per workgroup
-constexpr int UPD_GROUPS = 8;   // threads sharing one parameter's reduction
+constexpr int UPD_PAIRS = 32;                  // parameter pairs per workgroup (64 parameters)
+constexpr int UPD_PARAMS = 2 * UPD_PAIRS;
+constexpr int UPD_GROUPS = 8;                  // threads sharing one pair's reduction
 
-// Sum of p[s * stride + i] over s = g, g + G, g + 2G, ... < S, eight loads in
-// flight per iteration (the slabs are written by the previous kernel, so every
-// load is a cache miss; one dependent chain per slab would be latency-bound).
-__device__ __forceinline__ float sum_split(const float* p, int S, int64_t stride, int64_t i, int g) {
+// Sum of the float2 p[s * stride + j .. +1] over s = g, g + G, ... < S, eight
+// loads in flight per iteration (the slabs are written by the previous
+// kernel, so every load is a cache miss; one dependent chain per slab would
+// be latency-bound).
+__device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stride, int64_t j, int g) {
   constexpr int G = UPD_GROUPS;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float2 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = make_float2(0.f, 0.f);
   int s = g;
   for (; s + 7 * G < S; s += 8 * G) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += p[(int64_t)(s + u * G) * stride + i];
+    for (int u = 0; u < 8; ++u) {
+      const float2 v = *reinterpret_cast<const float2*>(p + (int64_t)(s + u * G) * stride + j);
+      a[u].x += v.x;
+      a[u].y += v.y;
+    }
   }
 #pragma unroll
   for (int u = 0; u < 8; ++u)
-    if (s + u * G < S) a[u] += p[(int64_t)(s + u * G) * stride + i];
-  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    if (s + u * G < S) {
+      const float2 v = *reinterpret_cast<const float2*>(p + (int64_t)(s + u * G) * stride + j);
+      a[u].x += v.x;
+      a[u].y += v.y;
+    }
+  return make_float2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
+                     ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
+}
+
+// One gradient element of the small head leaves (fc1/b, fc2/w, fc2/b): this
+// thread's share (samples grp, grp + G, ...) and its destination offset.
+__device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp, int64_t& dst) {
+  float g = 0.f;
+  if (e < HID) {  // fc1 bias: sum_b dz1
+    const int j = (int)e;
+#pragma unroll 4
+    for (int b = grp; b < u.B; b += UPD_GROUPS) g += u.dz1[(int64_t)b * HID + j];
+    dst = u.off[7] + j;
+  } else if (e < HID + (int64_t)HID * u.A) {  // fc2 w[j][a] = sum_{b: a_b = a} h1[b][j] gq[b]
+    const int64_t jj = e - HID;
+    const int j = (int)(jj / u.A), a = (int)(jj % u.A);
+#pragma unroll 4
+    for (int b = grp; b < u.B; b += UPD_GROUPS) {
+      const float v = u.h1[(int64_t)b * HID + j] * u.gq[b];
+      g += u.ga[b] == a ? v : 0.f;
+    }
+    dst = u.off[8] + jj;
+  } else if (e < HID + (int64_t)HID * u.A + u.nb2) {  // fc2 b
+    const int a = (int)(e - HID - (int64_t)HID * u.A);
+#pragma unroll 4
+    for (int b = grp; b < u.B; b += UPD_GROUPS) g += (u.nb2 == 1 || u.ga[b] == a) ? u.gq[b] : 0.f;
+    dst = u.off[9] + a;
+  }
+  return g;
 }
 
 // Reduces every gradient that crosses samples or split-K chunks and applies
 // centered RMSProp to every leaf except fc1/w (fused into its dW epilogue).
-// 256 threads = 32 parameters x 8 reduction groups, combined through LDS.
+// 256 threads = 32 parameter pairs x 8 reduction groups, combined through
+// LDS.  Grid: the small head leaves first (their blocks run the longest
+// per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
+// RMSProp operands are loaded at entry, under the reduction's latency.
 __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
   DQZ_STAMP(9, 0);
-  __shared__ float s_part[UPD_GROUPS][UPD_PARAMS];
-  const int pl = threadIdx.x % UPD_PARAMS, grp = threadIdx.x / UPD_PARAMS;
-  const int64_t i = (int64_t)blockIdx.x * UPD_PARAMS + pl;
-  const int64_t n0 = u.sz[0] + u.sz[1], n1 = n0 + u.sz[2] + u.sz[3], n2 = n1 + u.sz[4] + u.sz[5];
-  const int64_t n3 = n2 + HID, n4 = n3 + (int64_t)HID * u.A, n5 = n4 + u.nb2;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int b = 0; b < u.B; ++b) s += u.loss_part[b];
-    u.loss[0] = s / (float)u.B;
+  __shared__ float2 s_part[UPD_GROUPS][UPD_PAIRS];
+  const int pl = threadIdx.x % UPD_PAIRS, grp = threadIdx.x / UPD_PAIRS;
+  const int64_t nsmall = HID + (int64_t)HID * u.A + u.nb2;
+  const int small_blocks = (int)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS);
+  const int64_t c1 = u.sz[0] + u.sz[1], c2 = c1 + u.sz[2] + u.sz[3], c3 = c2 + u.sz[4] + u.sz[5];
+  float loss = 0.f;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    for (int b = threadIdx.x; b < u.B; b += 64) loss += u.loss_part[b];
   }
-  float g = 0.f;
-  int64_t dst = -1;
-  if (i < n0) {  // conv1: w rows 0..255, bias row 256
-    g = sum_split(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, i, grp);
-    dst = i < u.sz[0] ? u.off[0] + i : u.off[1] + (i - u.sz[0]);
-  } else if (i < n1) {
-    const int64_t j = i - n0;
-    g = sum_split(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, j, grp);
-    dst = j < u.sz[2] ? u.off[2] + j : u.off[3] + (j - u.sz[2]);
-  } else if (i < n2) {
-    const int64_t j = i - n1;
-    g = sum_split(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, j, grp);
-    dst = j < u.sz[4] ? u.off[4] + j : u.off[5] + (j - u.sz[4]);
-  } else if (i < n3) {  // fc1 bias: sum_b dz1
-    const int j = (int)(i - n2);
-    for (int b = grp; b < u.B; b += UPD_GROUPS) g += u.dz1[(int64_t)b * HID + j];
-    dst = u.off[7] + j;
-  } else if (i < n4) {  // fc2 w[j][a] = sum_{b: a_b = a} h1[b][j] gq[b]
-    const int64_t jj = i - n3;
-    const int j = (int)(jj / u.A), a = (int)(jj % u.A);
-    for (int b = grp; b < u.B; b += UPD_GROUPS)
-      if (u.ga[b] == a) g += u.h1[(int64_t)b * HID + j] * u.gq[b];
-    dst = u.off[8] + jj;
-  } else if (i < n5) {  // fc2 b
-    const int a = (int)(i - n4);
-    for (int b = grp; b < u.B; b += UPD_GROUPS)
-      if (u.nb2 == 1 || u.ga[b] == a) g += u.gq[b];
-    dst = u.off[9] + a;
+  int64_t dst[2] = {-1, -1};
+  float2 g = make_float2(0.f, 0.f);
+  if ((int)blockIdx.x < small_blocks) {
+    const int64_t e = (int64_t)blockIdx.x * UPD_PARAMS + 2 * pl;
+    g.x = small_grad(u, e, grp, dst[0]);
+    g.y = small_grad(u, e + 1, grp, dst[1]);
+  } else {
+    const int64_t j = (int64_t)(blockIdx.x - small_blocks) * UPD_PARAMS + 2 * pl;  // even; regions are even-sized
+    if (j < c1) {  // conv1: w rows 0..255, bias row 256
+      g = sum_split2(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, j, grp);
+      for (int h = 0; h < 2; ++h) dst[h] = j + h < u.sz[0] ? u.off[0] + j + h : u.off[1] + (j + h - u.sz[0]);
+    } else if (j < c2) {
+      const int64_t k = j - c1;
+      g = sum_split2(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, k, grp);
+      for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[2] ? u.off[2] + k + h : u.off[3] + (k + h - u.sz[2]);
+    } else if (j < c3) {
+      const int64_t k = j - c2;
+      g = sum_split2(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, k, grp);
+      for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[4] ? u.off[4] + k + h : u.off[5] + (k + h - u.sz[4]);
+    }
+  }
+  const Rms& R = u.rms;
+  float o_th[2] = {0.f, 0.f}, o_mu[2] = {0.f, 0.f}, o_nu[2] = {0.f, 0.f};
+  if (grp == 0 && R.gout == nullptr) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (dst[h] >= 0) {
+        o_th[h] = u.th[dst[h]];
+        o_mu[h] = u.mu[dst[h]];
+        o_nu[h] = u.nu[dst[h]];
+      }
   }
   s_part[grp][pl] = g;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    loss = wave_sum(loss);
+    if (threadIdx.x == 0) u.loss[0] = loss / (float)u.B;
+  }
   __syncthreads();
-  if (grp == 0 && dst >= 0) {
-    float gs = 0.f;
+  if (grp == 0) {
+    float2 gs = make_float2(0.f, 0.f);
 #pragma unroll
-    for (int gi = 0; gi < UPD_GROUPS; ++gi) gs += s_part[gi][pl];
-    u.rms.apply(u.th, u.mu, u.nu, dst, gs);
+    for (int gi = 0; gi < UPD_GROUPS; ++gi) {
+      gs.x += s_part[gi][pl].x;
+      gs.y += s_part[gi][pl].y;
+    }
+    const float gv[2] = {gs.x, gs.y};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (dst[h] < 0) continue;
+      const int64_t i = dst[h];
+      if (R.gout) {
+        R.gout[i] = gv[h];
+      } else {
+        const float m = R.c1 * gv[h] + R.decay * o_mu[h];
+        const float v = R.c1 * (gv[h] * gv[h]) + R.decay * o_nu[h];
+        u.mu[i] = m;
+        u.nu[i] = v;
+        u.th[i] = o_th[h] + (-R.lr) * (gv[h] * rsqrtf(v - m * m + R.eps));
+      }
+    }
   }
   DQZ_STAMP(9, 3);
 }

@@ -356,9 +356,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.B = B;
   u.nb2 = L->shared_bias ? 1 : A;
   u.rms = rms;
-  const int64_t nupd = L->sz[0] + L->sz[1] + L->sz[2] + L->sz[3] + L->sz[4] + L->sz[5] + HID + (int64_t)HID * A + u.nb2;
-  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3((unsigned)((nupd + UPD_PARAMS - 1) / UPD_PARAMS)), dim3(256), 0,
-                                  st, u);
+  const int64_t nconv = L->sz[0] + L->sz[1] + L->sz[2] + L->sz[3] + L->sz[4] + L->sz[5];
+  const int64_t nsmall = HID + (int64_t)HID * A + u.nb2;
+  const unsigned nblk = (unsigned)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS + (nconv + UPD_PARAMS - 1) / UPD_PARAMS);
+  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }

@@ -25,7 +25,7 @@ from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, syntheti
 NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
          6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*'}
 ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
-K, NB, NS = 16, 2048, 4
+K, NB, NS = 16, 4096, 4
 
 dev = torch.device('cuda:0')
 net = networks.dqn_atari_network(6)
@@ -86,5 +86,16 @@ for k in ORDER:
   if os.environ.get('PCT'):  # start / end percentiles 0, 10, 50, 90, 100
     q = lambda a: ' '.join('%.2f' % ((np.percentile(a, p) - t0) / 100) for p in (0, 10, 50, 90, 100))
     print('%10s start %s | end %s' % ('', q(s0), q(s3)))
+  rng = os.environ.get('RANGES_%d' % k)  # e.g. RANGES_9=0,257,1283,2437: per-block-range end percentiles
+  if rng:
+    cuts = [int(x) for x in rng.split(',')] + [NB]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+      sel = t[k, lo:hi, 0] > 0
+      if sel.any():
+        e = t[k, lo:hi, 3][sel]
+        b0 = t[k, lo:hi, 0][sel]
+        print('%10s blocks [%d, %d): start p50 %.2f | end p50 %.2f p90 %.2f max %.2f | life p50 %.2f' % (
+            '', lo, hi, (np.median(b0) - t0) / 100, (np.median(e) - t0) / 100,
+            (np.percentile(e, 90) - t0) / 100, (e.max() - t0) / 100, np.median(e - b0) / 100))
   if not NAMES[k].endswith('*'):
     prev_end = end
