@@ -64,7 +64,15 @@ constexpr int C1_IN_FLOATS = FC * C1_PLANE;       // 8064
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 // networks.py:192: x.astype(jnp.float32) / 255.0 (IEEE division, not a reciprocal multiply)
-__device__ __forceinline__ float u8n(unsigned v) { return (float)v / 255.0f; }
+// x / 255.0f correctly rounded (networks.py:192) without the IEEE division
+// sequence: q = x * (1/255) plus one FMA residual correction.  Checked in
+// exact arithmetic to equal the rounded quotient for every x in [0, 255].
+__device__ __forceinline__ float u8n(unsigned v) {
+  constexpr float r = 1.0f / 255.0f;
+  const float x = (float)v;
+  const float q = x * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
+}
 
 struct NetZ {
   const float* p[3];  // parameter buffer of network copy z
@@ -173,7 +181,7 @@ inline dim3 xcd_grid(int J, int nsamp) { return dim3((unsigned)(J * ((nsamp + 7)
 // draw i of step `ctr` -> live slot (base + floor(u * size)) mod capacity,
 // u from Philox(counter = (ctr, i), key = seed).
 struct UniformDraw {
-  int64_t base, size, capacity;
+  int64_t base, size, capacity;  // base in [0, capacity): callers pass base % capacity
   uint64_t seed;
   uint64_t* counter;  // device step counter (read by the sampling kernel, advanced later)
   int32_t* slots_out;
@@ -184,7 +192,8 @@ __device__ __forceinline__ int32_t uniform_slot(uint64_t ctr, int i, const Unifo
                              make_uint2((unsigned)d.seed, (unsigned)(d.seed >> 32)));
   const uint64_t u = ((uint64_t)r.x << 32) | r.y;
   const int64_t j = (int64_t)__umul64hi(u, (uint64_t)d.size);  // uniform in [0, size)
-  return (int32_t)((d.base + j) % d.capacity);
+  const int64_t k = d.base + j;  // base < capacity (host-normalised), j < size <= capacity
+  return (int32_t)(k >= d.capacity ? k - d.capacity : k);
 }
 
 }  // namespace dqz

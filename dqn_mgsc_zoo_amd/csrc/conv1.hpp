@@ -38,7 +38,7 @@ __device__ __forceinline__ void store_bytes_as_f32(float* dst, uint4 v) {
 // Stages input rows [20*rb, 20*rb + 24) of sample b, stack `which`, as
 // s_in[ci][row][col] = pixel / 255.
 __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& src, int b, int which, int rb,
-                                                  int z = 0) {
+                                                  int z = 0, int sk = -1) {
   const int row0 = rb * C1S * C1_ROWS;
   constexpr int QPC = C1_PLANE / 16;  // 126 16-byte pieces per channel
   if (src.states) {
@@ -67,6 +67,7 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
     } else {
       slot = src.slots[b];
     }
+    if (sk >= 0) DQZ_STAMP(sk, 0);
     const int32_t* fr = src.fidx + (int64_t)slot * 8 + which * 4;
     const int f0 = fr[0], f1 = fr[1], f2 = fr[2], f3 = fr[3];
     constexpr int NP = FC * QPC;  // 504
@@ -81,6 +82,7 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
       const uint4* g = reinterpret_cast<const uint4*>(src.frames + (int64_t)max(f, 0) * FB + row0 * FW);
       v[q] = g[j];
     }
+    if (sk >= 0) DQZ_STAMP(sk, 1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = (int)threadIdx.x + 256 * q;
@@ -91,6 +93,7 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
         store_bytes_as_f32(dst, v[q]);
       }
     }
+    if (sk >= 0) DQZ_STAMP(sk, 2);
   }
 }
 
@@ -115,12 +118,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   const int rb = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const float bias = a.nz.p[z][a.b_off + (threadIdx.x & 31)];  // epilogue operand, loaded early
   const float4* w4 = reinterpret_cast<const float4*>(a.nz.p[z] + a.w_off);
-  float4 wv[8];  // 256 x 32 weights = 8 float4 per thread, issued together
+  // 256 x 32 weights = 8 float4 per thread, staged first: they arrive with
+  // the sampler's counter load, and (left to the compiler) their loads would
+  // sink below the frame gather and add a round trip at the end.
+  float4 wv[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) wv[q] = w4[threadIdx.x + 256 * q];
-  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb, z);
 #pragma unroll
   for (int q = 0; q < 8; ++q) reinterpret_cast<float4*>(s_w)[threadIdx.x + 256 * q] = wv[q];
+  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb, z, 14);
   DQZ_STAMP(0, 1);
   __syncthreads();
 

@@ -376,7 +376,7 @@ int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_stor
   if (size < 1) return fail(DQZ_ERR_INVALID, "cannot sample from an empty replay (size=%lld)", (long long)size);
   if (capacity < size || base < 0) return fail(DQZ_ERR_INVALID, "bad replay geometry");
   if (L && L->cfg.algo == DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "PER samples by priority, not uniformly");
-  const UniformDraw d{base, size, capacity, seed, counter_dev, slots_out};
+  const UniformDraw d{base % capacity, size, capacity, seed, counter_dev, slots_out};
   return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, &d);
 }
 
@@ -448,7 +448,7 @@ int dqz_sample_uniform(int64_t base, int64_t size, int64_t capacity, int n, uint
   if (capacity < size) return fail(DQZ_ERR_INVALID, "size exceeds capacity");
   if (n < 1 || n > 65536) return fail(DQZ_ERR_INVALID, "n out of range");
   if (base < 0) return fail(DQZ_ERR_INVALID, "base must be >= 0");
-  hipLaunchKernelGGL(sample_uniform_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, base, size, capacity, n, seed,
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, base % capacity, size, capacity, n, seed,
                      counter_dev, out_slots);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;

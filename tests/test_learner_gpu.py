@@ -161,6 +161,14 @@ def test_sample_uniform_device(device):
   expected = counts.sum() / size
   # chi-square-ish bound on the per-slot counts
   assert np.abs(counts[live] - expected).max() < 6 * np.sqrt(expected)
+  # a base past the ring's end names the same window (base is taken mod capacity)
+  ca = torch.zeros((1,), dtype=torch.int64, device=device)
+  cb = torch.zeros((1,), dtype=torch.int64, device=device)
+  oa = torch.empty((512,), dtype=torch.int32, device=device)
+  ob = torch.empty((512,), dtype=torch.int32, device=device)
+  learner_lib.sample_uniform(base, size, capacity, 512, 99, ca, oa)
+  learner_lib.sample_uniform(base + 3 * capacity, size, capacity, 512, 99, cb, ob)
+  assert torch.equal(oa, ob)
 
 
 def test_fused_uniform_step_matches_sample_then_step(device):

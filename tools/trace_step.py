@@ -23,8 +23,8 @@ import torch  # noqa: E402
 from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
 
 NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
-         6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*'}
-ORDER = [10, 0, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
+         6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*', 14: 'c1_stage*'}
+ORDER = [10, 0, 14, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
 K, NB, NS = 16, 4096, 4
 
 dev = torch.device('cuda:0')
@@ -68,6 +68,14 @@ t0 = t[:, :, 0][t[:, :, 0] > 0].min()
 print('%-10s %8s %8s %8s | %8s %8s %8s %8s  (us; 100 MHz ticks)' % (
     'kernel', 'gap', 'span', 'blk_med', 's0-s1', 's1-s2', 's2-s3', 'nblk'))
 for k in ORDER:
+  if k == 14:  # conv1 fwd staging sub-stamps: start -> slot, slot -> frame loads issued, -> LDS staged
+    ok = (t[14, :, 0] > 0) & (t[0, :, 0] > 0)
+    if ok.any():
+      d = lambda a, b: np.median(a[ok] - b[ok]) / 100
+      print('%-10s start->slot %.2f  slot->fidx+issue %.2f  ->frames staged %.2f  ->W staged %.2f' % (
+          'c1_stage', d(t[14, :, 0], t[0, :, 0]), d(t[14, :, 1], t[14, :, 0]), d(t[14, :, 2], t[14, :, 1]),
+          d(t[0, :, 1], t[14, :, 2])))
+    continue
   s0 = t[k, :, 0]
   live = s0 > 0
   if not live.any():
