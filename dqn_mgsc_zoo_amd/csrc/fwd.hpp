@@ -190,7 +190,13 @@ struct Fc1FwdArgs {
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4][2][256];
-  const int nt = blockIdx.x, s = blockIdx.y, z = blockIdx.z / a.MG, mg = blockIdx.z % a.MG;
+  // Block -> tile map: the two 16-column tiles that share W1's 128-byte lines
+  // (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
+  // dispatch places on the same XCD, so each line is fetched into one L2.
+  const int i = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int slot = i >> 3, pair = (i & 7) + 8 * (slot >> 1);
+  const int nt = 2 * (pair % 16) + (slot & 1), rest = pair / 16;
+  const int s = rest % FC1_S, zm = rest / FC1_S, z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = s * FC1_KS + w * FC1_KW;
