@@ -20,6 +20,13 @@ struct Conv1Src {
   const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
   int fused;              // 1: slots come from the fused uniform sampler `draw`
   UniformDraw draw;
+  // Batch record: block (rb 0, z 0) of sample b also copies action / reward /
+  // discount of its slot into rec[b] = {a as int bits, r, d, 0}, so the head
+  // reads one record per sample instead of the slot -> record chain.
+  const int32_t* action = nullptr;
+  const float* reward = nullptr;
+  const float* discount = nullptr;
+  float4* rec = nullptr;
 };
 
 __device__ __forceinline__ void store_bytes_as_f32(float* dst, uint4 v) {
@@ -70,6 +77,9 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
     if (sk >= 0) DQZ_STAMP(sk, 0);
     const int32_t* fr = src.fidx + (int64_t)slot * 8 + which * 4;
     const int f0 = fr[0], f1 = fr[1], f2 = fr[2], f3 = fr[3];
+    const bool wrec = src.rec != nullptr && threadIdx.x == 0 && rb == 0 && z == 0;
+    float4 recv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (wrec) recv = make_float4(__int_as_float(src.action[slot]), src.reward[slot], src.discount[slot], 0.f);
     constexpr int NP = FC * QPC;  // 504
     uint4 v[2];
     int fq[2];
@@ -93,6 +103,7 @@ __device__ __forceinline__ void stage_conv1_input(float* s_in, const Conv1Src& s
         store_bytes_as_f32(dst, v[q]);
       }
     }
+    if (wrec) src.rec[b] = recv;
     if (sk >= 0) DQZ_STAMP(sk, 2);
   }
 }

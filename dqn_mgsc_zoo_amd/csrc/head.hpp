@@ -18,6 +18,7 @@ struct HeadArgs {
   const float* discount;
   const float* weights;  // PER importance weights or null
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
+  const float4* rec;     // batch records {a, r, d, 0} written by conv1, or null (slot chain)
   uint64_t* advance;     // fused sampler's step counter, advanced once here (or null)
   int unit;              // 1: unit cotangent on q[a] (gradient of q itself; HVP pass)
   float bound;           // grad_error_bound
@@ -47,12 +48,16 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = n >> 6;
   const int A = h.A, B = h.B, Z = h.Z, S = h.S;
   // Every global load is issued up front: the batch record chain
-  // (slot -> action/reward/discount), the Z x S fc1 partials, fc1 biases and
-  // the W2 rows; nothing below waits on more than one round trip.
+  // (slot -> action/reward/discount), the Z x S fc1 partials, fc1 biases,
+  // the W2 rows and the fc2 bias; nothing below waits on more than one round
+  // trip.  Global stores are deferred to the end: vmcnt counts stores too, so
+  // a store issued before a dependent load's wait would be waited for as well.
   int a_tm1 = 0;
   float r = 0.f, d = 0.f, w = 1.f, pm = 0.f;
-  if (h.advance && b == 0 && n == 0) *h.advance += 1;  // every conv1 block has read it
-  const int slot = !h.fwd_only ? h.slots[b] : 0;  // uniform load, in flight with the partials
+  const bool chain = !h.fwd_only && h.rec == nullptr;
+  const int slot = chain ? h.slots[b] : 0;  // uniform load, in flight with the partials
+  float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!h.fwd_only && h.rec != nullptr && n == 0) rv = h.rec[b];
   float pv[3][SMAX], b1v[3], w2v[3][AMAX];
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
@@ -65,81 +70,100 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) w2v[z][a] = w2[min(a, A - 1)];
   }
+  float b2v = 0.f;  // fc2 bias of output (z, a) = (n / AMAX, n % AMAX)
+  if (n < 3 * AMAX) {
+    const int zc = min(n / AMAX, Z - 1), a = min(n % AMAX, A - 1);
+    b2v = h.nz.p[zc][h.b2_off + (h.shared_bias ? 0 : a)];
+  }
   if (!h.fwd_only && n == 0) {  // second hop of the batch record chain, needed only for the TD
-    a_tm1 = h.action[slot];
-    r = h.reward[slot];
-    d = h.discount[slot];
+    if (chain) {
+      a_tm1 = h.action[slot];
+      r = h.reward[slot];
+      d = h.discount[slot];
+    } else {
+      a_tm1 = __float_as_int(rv.x);
+      r = rv.y;
+      d = rv.z;
+    }
     if (h.weights) w = h.weights[b];
     if (h.meta_p) pm = h.meta_p[b];
   }
-  float h0 = 0.f;
   DQZ_STAMP(4, 1);
+  float hz[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
     if (z < Z) {
       float acc = b1v[z];
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) acc += s < S ? pv[z][s] : 0.f;
-      const float hv = relu(acc);
-      h.h1[((int64_t)z * B + b) * HID + n] = hv;
-      if (z == 0) h0 = hv;
+      hz[z] = relu(acc);
+      if (z == 0) DQZ_STAMP(15, 0);  // fc1 partials of copy 0 have landed
 #pragma unroll
       for (int a = 0; a < AMAX; ++a) {
-        const float sa = wave_sum(hv * w2v[z][a]);
+        const float sa = wave_sum(hz[z] * w2v[z][a]);
         if (lane == 0) s_red[wave][z * AMAX + a] = sa;
       }
     }
   }
+  DQZ_STAMP(15, 1);  // wave sums done
   __syncthreads();
-  if (n < 3 * AMAX) {
-    const int z = n / AMAX, a = n % AMAX;
-    if (z < Z && a < A) {
-      float sa = 0.f;
+  float qv = 0.f;
+  const bool qthread = n < 3 * AMAX && n / AMAX < Z && n % AMAX < A;
+  if (qthread) {
+    float sa = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < 8; ++ww) sa += s_red[ww][n];
-      const float qv = sa + h.nz.p[z][h.b2_off + (h.shared_bias ? 0 : a)];
-      s_q[z][a] = qv;
-      h.q[((int64_t)z * B + b) * A + a] = qv;
-    }
+    for (int ww = 0; ww < 8; ++ww) sa += s_red[ww][n];
+    qv = sa + b2v;
+    s_q[n / AMAX][n % AMAX] = qv;
   }
-  if (h.fwd_only) return;
-  __syncthreads();
-  if (n == 0) {
-    float v;
-    if (h.algo == DQZ_ALGO_DQN) {
-      v = s_q[1][0];
-      for (int a = 1; a < A; ++a) v = fmaxf(v, s_q[1][a]);
-    } else {
-      int am = 0;  // online Q(s_t) selects, jnp.argmax: first maximum
-      for (int a = 1; a < A; ++a)
-        if (s_q[2][a] > s_q[2][am]) am = a;
-      v = s_q[1][am];
+  if (!h.fwd_only) {
+    __syncthreads();
+    DQZ_STAMP(15, 2);  // q values in LDS
+    if (n == 0) {
+      float v;
+      if (h.algo == DQZ_ALGO_DQN) {
+        v = s_q[1][0];
+        for (int a = 1; a < A; ++a) v = fmaxf(v, s_q[1][a]);
+      } else {
+        int am = 0;  // online Q(s_t) selects, jnp.argmax: first maximum
+        for (int a = 1; a < A; ++a)
+          if (s_q[2][a] > s_q[2][am]) am = a;
+        v = s_q[1][am];
+      }
+      const float td = (r + d * v) - s_q[0][a_tm1];
+      float g;
+      if (h.unit) {
+        g = -1.f;  // gq = d q[a] / d q[a] = 1
+      } else if (h.meta_p) {
+        // meta mode: p_b * grad of loss_fn on the single transition b
+        // (dqn_mgsc_batched/agent.py:152-158): batch of one, clip, then weight.
+        g = pm * fminf(fmaxf(td, -h.bound), h.bound);
+      } else {
+        g = w * td / (float)B;  // d mean(l2(td) * w) / d td
+        g = fminf(fmaxf(g, -h.bound), h.bound);
+      }
+      s_g = -g;
+      s_a = a_tm1;
+      h.td[b] = td;
+      h.loss_part[b] = 0.5f * td * td * w;
+      h.gq[b] = -g;
+      h.ga[b] = a_tm1;
     }
-    const float td = (r + d * v) - s_q[0][a_tm1];
-    float g;
-    if (h.unit) {
-      g = -1.f;  // gq = d q[a] / d q[a] = 1
-    } else if (h.meta_p) {
-      // meta mode: p_b * grad of loss_fn on the single transition b
-      // (dqn_mgsc_batched/agent.py:152-158): batch of one, clip, then weight.
-      g = pm * fminf(fmaxf(td, -h.bound), h.bound);
-    } else {
-      g = w * td / (float)B;  // d mean(l2(td) * w) / d td
-      g = fminf(fmaxf(g, -h.bound), h.bound);
-    }
-    h.td[b] = td;
-    h.loss_part[b] = 0.5f * td * td * w;
-    h.gq[b] = -g;
-    h.ga[b] = a_tm1;
-    s_g = -g;
-    s_a = a_tm1;
-  }
-  __syncthreads();
-  float wv = w2v[0][0];
+    __syncthreads();
+    float wv = w2v[0][0];
 #pragma unroll
-  for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
-  DQZ_STAMP(4, 2);
-  h.dz1[(int64_t)b * HID + n] = h0 > 0.f ? s_g * wv : 0.f;
+    for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
+    DQZ_STAMP(4, 2);
+    h.dz1[(int64_t)b * HID + n] = hz[0] > 0.f ? s_g * wv : 0.f;
+  }
+  // deferred outputs: fc1 activations (fc2 dW in the update kernel), q values
+#pragma unroll
+  for (int z = 0; z < 3; ++z)
+    if (z < Z) h.h1[((int64_t)z * B + b) * HID + n] = hz[z];
+  if (qthread) h.q[((int64_t)(n / AMAX) * B + b) * A + n % AMAX] = qv;
+  // the fused sampler's step counter: every conv1 block of this step has read it
+  if (h.advance && b == 0 && n == 0)
+    __hip_atomic_fetch_add(h.advance, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   DQZ_STAMP(4, 3);
 }
 

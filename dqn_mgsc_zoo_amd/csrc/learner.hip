@@ -50,7 +50,7 @@ struct dqz_learner {
   int Z, shared_bias;
   int64_t off[10], sz[10], total;
   int S_fc1, S2, S3;
-  float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq;
+  float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
   int32_t* ga;
   void* block;
 };
@@ -101,10 +101,11 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
-                    &L->gq,  reinterpret_cast<float**>(&L->ga)};
+                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec};
+  static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
   if (hipMalloc(&L->block, total * sizeof(float)) != hipSuccess) {
@@ -216,7 +217,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
 }
 
 static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
-  HeadArgs h;
+  HeadArgs h{};
   memset(&h, 0, sizeof(h));
   h.fc1p = L->fc1p;
   h.S = L->S_fc1;
@@ -255,6 +256,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   nz.which[1] = 1;
   nz.which[2] = 1;
   Conv1Src src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
+  src.action = S->action;
+  src.reward = S->reward;
+  src.discount = S->discount;
+  src.rec = reinterpret_cast<float4*>(L->rec);
   if (draw) {  // conv1 draws the batch itself; later kernels read the published slots
     Conv1Src fsrc = src;
     fsrc.fused = 1;
@@ -279,6 +284,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.discount = S->discount;
   h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
   h.meta_p = meta_p;
+  h.rec = reinterpret_cast<const float4*>(L->rec);
   h.advance = draw ? draw->counter : nullptr;
   h.unit = unit;
   h.bound = L->cfg.grad_error_bound;
@@ -320,6 +326,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.B = B;
   Conv1DwArgs c1dw;
   c1dw.src = src;
+  c1dw.src.rec = nullptr;
   c1dw.which = 0;
   c1dw.B = B;
   c1dw.dy1 = L->dy1;

@@ -23,8 +23,8 @@ import torch  # noqa: E402
 from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
 
 NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
-         6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*', 14: 'c1_stage*'}
-ORDER = [10, 0, 14, 1, 2, 3, 4, 5, 6, 11, 7, 12, 8, 13, 9]
+         6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*', 14: 'c1_stage*', 15: 'head_sub*'}
+ORDER = [10, 0, 14, 1, 2, 3, 4, 15, 5, 6, 11, 7, 12, 8, 13, 9]
 K, NB, NS = 16, 4096, 4
 
 dev = torch.device('cuda:0')
@@ -75,6 +75,14 @@ for k in ORDER:
       print('%-10s start->slot %.2f  slot->fidx+issue %.2f  ->frames staged %.2f  ->W staged %.2f' % (
           'c1_stage', d(t[14, :, 0], t[0, :, 0]), d(t[14, :, 1], t[14, :, 0]), d(t[14, :, 2], t[14, :, 1]),
           d(t[0, :, 1], t[14, :, 2])))
+    continue
+  if k == 15:  # head sub-stamps: start -> h(z=0) -> wave sums -> q in LDS -> dz1 stored
+    ok = (t[15, :, 0] > 0) & (t[4, :, 0] > 0)
+    if ok.any():
+      d = lambda a, b: np.median(a[ok] - b[ok]) / 100
+      print('%-10s start->h %.2f  ->wave sums %.2f  ->q %.2f  ->TD+dz1 %.2f' % (
+          'head_sub', d(t[15, :, 0], t[4, :, 0]), d(t[15, :, 1], t[15, :, 0]), d(t[15, :, 2], t[15, :, 1]),
+          d(t[4, :, 3], t[15, :, 2])))
     continue
   s0 = t[k, :, 0]
   live = s0 > 0
