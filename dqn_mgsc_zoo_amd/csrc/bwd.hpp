@@ -492,7 +492,8 @@ __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win
 // [16 kb, 16 kb + 16), columns [128 nq, 128 nq + 128); wave w owns columns
 // [128 nq + 32 w, +32) (two 16-column MFMA tiles), K = the batch.
 constexpr int FC1W_LD = 144;  // LDS row stride of the dz1 slice: 144 = 16 (mod 32)
-constexpr int FC1W_SMEM = 32 * FC1W_LD;
+constexpr int FC1W_TLD = 36;  // row stride of a wave's 16 x 32 dW transpose tile
+constexpr int FC1W_SMEM = 32 * FC1W_LD + 4 * 16 * FC1W_TLD;
 
 __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, int blk) {
   DQZ_STAMP(11, 0);
@@ -500,70 +501,92 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   const int n = lane & 15, kq = lane >> 4;
   const int kb = blk >> 2, nq = blk & 3;
   const int k0 = 16 * kb, c0 = 128 * nq;
-  // RMSProp operands of this lane's 8 entries (C layout: row 4 kq + r, column
-  // 32 w + 16 q + n), issued first so their HBM latency hides under the GEMM.
   const Rms& R = a.rms;
   const bool upd = R.gout == nullptr;
-  float o_th[8], o_mu[8], o_nu[8];
-  if (upd) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
-        o_th[4 * q + r] = a.th[e];
-        o_mu[4 * q + r] = a.mu[e];
-        o_nu[4 * q + r] = a.nu[e];
-      }
-  }
-  f32x4 gacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  for (int c = 0; c < a.B; c += 32) {
-    if (c > 0) __syncthreads();
-    float4 v[4];
+  // GEMM operands of a 32-sample chunk: dz1[c + row][c0 ..] (LDS) and
+  // y3[c + 4 kk + kq][k0 + n] (A operand, registers).
+  float4 v[4];
+  float yv[8];
+  auto load_chunk = [&](int c) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = t + 256 * i, row = f >> 5;  // 32 float4 per row
       const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + c0 + 4 * (f & 31));
       v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float yv[8];  // A operand: y3[c + 4 kk + kq][k0 + n]
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int bb = c + 4 * kk + kq;
       const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
       yv[kk] = bb < a.B ? y : 0.f;
     }
+  };
+  load_chunk(0);
+  // RMSProp operands in row-float4 layout: lane l owns W1[k0 + (l >> 3) + 8 h]
+  // [c0 + 32 w + 4 (l & 7) .. +3], h = 0, 1, so each wave instruction reads
+  // eight whole 128-byte lines.  Issued right AFTER the first chunk's GEMM
+  // operands and unconditionally (gradient-output mode re-reads theta: mu /
+  // nu may be null there): vmcnt is in order, so the GEMM waits for its own
+  // operands only and these loads land under it.
+  const float* pmu = upd ? a.mu : a.th;
+  const float* pnu = upd ? a.nu : a.th;
+  const int64_t e0 = a.w_off + (int64_t)(k0 + (lane >> 3)) * HID + c0 + 32 * w + 4 * (lane & 7);
+  float4 o_th[2], o_mu[2], o_nu[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t e = e0 + (int64_t)8 * h * HID;
+    o_th[h] = *reinterpret_cast<const float4*>(a.th + e);
+    o_mu[h] = *reinterpret_cast<const float4*>(pmu + e);
+    o_nu[h] = *reinterpret_cast<const float4*>(pnu + e);
+  }
+  f32x4 gacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int c = 0;;) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = t + 256 * i;
       *reinterpret_cast<float4*>(smem + (f >> 5) * FC1W_LD + 4 * (f & 31)) = v[i];
     }
     __syncthreads();
+    if (c == 0) DQZ_STAMP(11, 1);
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const float* d = smem + (4 * kk + kq) * FC1W_LD + 32 * w + n;
       gacc[0] = mfma4(yv[kk], d[0], gacc[0]);
       gacc[1] = mfma4(yv[kk], d[16], gacc[1]);
     }
+    c += 32;
+    if (c >= a.B) break;
+    __syncthreads();  // this chunk's LDS readers are done
+    load_chunk(c);
   }
   DQZ_STAMP(11, 2);
-  // C layout: row = 4 kq + r, col = n of tile q -> W1[k0 + 4 kq + r][c0 + 32 w + 16 q + n]
+  // C layout: row = 4 kq + r, col = 16 q + n of the wave's 16 x 32 tile ->
+  // wave-private LDS tile -> row-float4 layout (same-wave LDS accesses are
+  // ordered: no barrier).
+  float* tile = smem + 32 * FC1W_LD + w * 16 * FC1W_TLD;
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t e = a.w_off + (int64_t)(k0 + 4 * kq + r) * HID + c0 + 32 * w + 16 * q + n;
-      const float g = gacc[q][r];
-      if (!upd) {
-        R.gout[e] = g;
-      } else {
-        const float m = R.c1 * g + R.decay * o_mu[4 * q + r];
-        const float vv = R.c1 * (g * g) + R.decay * o_nu[4 * q + r];
-        a.mu[e] = m;
-        a.nu[e] = vv;
-        a.th[e] = o_th[4 * q + r] + (-R.lr) * (g * rsqrtf(vv - m * m + R.eps));
-      }
+    for (int r = 0; r < 4; ++r) tile[(4 * kq + r) * FC1W_TLD + 16 * q + n] = gacc[q][r];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float4 g = *reinterpret_cast<const float4*>(tile + ((lane >> 3) + 8 * h) * FC1W_TLD + 4 * (lane & 7));
+    const int64_t e = e0 + (int64_t)8 * h * HID;
+    if (!upd) {
+      *reinterpret_cast<float4*>(R.gout + e) = g;
+    } else {
+      float4 m, vv, th;
+#define DQZ_RMS1(X)                                            \
+  m.X = R.c1 * g.X + R.decay * o_mu[h].X;                      \
+  vv.X = R.c1 * (g.X * g.X) + R.decay * o_nu[h].X;             \
+  th.X = o_th[h].X + (-R.lr) * (g.X * rsqrtf(vv.X - m.X * m.X + R.eps));
+      DQZ_RMS1(x) DQZ_RMS1(y) DQZ_RMS1(z) DQZ_RMS1(w)
+#undef DQZ_RMS1
+      *reinterpret_cast<float4*>(a.mu + e) = m;
+      *reinterpret_cast<float4*>(a.nu + e) = vv;
+      *reinterpret_cast<float4*>(a.th + e) = th;
     }
+  }
   DQZ_STAMP(11, 3);
 }
 
