@@ -243,6 +243,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     }
   }
   __syncthreads();
+  DQZ_STAMP(6, 1);
   int base[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
@@ -260,6 +261,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     for (int m = 0; m < 3; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
   }
   __syncthreads();
+  DQZ_STAMP(6, 2);
   float* s_red = s_win;  // [4][48][16]
 #pragma unroll
   for (int m = 0; m < 3; ++m)
@@ -302,6 +304,7 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
     }
   }
   __syncthreads();
+  DQZ_STAMP(12, 1);
   // A operand: y2 window at (oh + kh, ow + kw), ci = 16 w + n; position p = 4 kk + kq
   int pb[13];
 #pragma unroll
@@ -395,6 +398,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     }
   }
   __syncthreads();
+  DQZ_STAMP(7, 1);
   int base[7];
 #pragma unroll
   for (int m = 0; m < 7; ++m) {
@@ -412,6 +416,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     for (int m = 0; m < 7; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
   }
   __syncthreads();
+  DQZ_STAMP(7, 2);
   float* s_red = s_win;  // [4][112][16]
 #pragma unroll
   for (int m = 0; m < 7; ++m)
@@ -454,6 +459,7 @@ __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win
     }
   }
   __syncthreads();
+  DQZ_STAMP(13, 1);
   int pb[21];
 #pragma unroll
   for (int kk = 0; kk < 21; ++kk) {

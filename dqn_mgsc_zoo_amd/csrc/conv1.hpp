@@ -193,6 +193,7 @@ __device__ __forceinline__ void conv1_dw_body(const Conv1DwArgs& a, float* smem,
   for (int q = 0; q < 4; ++q)
     if ((int)threadIdx.x + 256 * q < ND4) reinterpret_cast<float4*>(s_dy)[threadIdx.x + 256 * q] = dv[q];
   __syncthreads();
+  DQZ_STAMP(8, 1);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, i = lane & 31;
