@@ -579,7 +579,15 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
     const float4 g = *reinterpret_cast<const float4*>(tile + ((lane >> 3) + 8 * h) * FC1W_TLD + 4 * (lane & 7));
     const int64_t e = e0 + (int64_t)8 * h * HID;
     if (!upd) {
-      *reinterpret_cast<float4*>(R.gout + e) = g;
+      float4 o = g;
+      if (R.gacc) {
+        const float4 prev = *reinterpret_cast<const float4*>(R.gout + e);
+        o.x += prev.x;
+        o.y += prev.y;
+        o.z += prev.z;
+        o.w += prev.w;
+      }
+      *reinterpret_cast<float4*>(R.gout + e) = o;
     } else {
       float4 m, vv, th;
 #define DQZ_RMS1(X)                                            \

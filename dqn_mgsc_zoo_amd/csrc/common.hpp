@@ -87,9 +87,10 @@ struct NetZ {
 struct Rms {
   float lr, decay, c1, eps;
   float* gout;
+  int gacc;  // gradient-output mode: 1 adds into gout (meta-batch chunks), 0 overwrites
   __device__ __forceinline__ void apply(float* th, float* mu, float* nu, int64_t i, float g) const {
     if (gout) {
-      gout[i] = g;
+      gout[i] = gacc ? gout[i] + g : g;
       return;
     }
     const float m = c1 * g + decay * mu[i];

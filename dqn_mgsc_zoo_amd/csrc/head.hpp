@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
       if (dst[h] < 0) continue;
       const int64_t i = dst[h];
       if (R.gout) {
-        R.gout[i] = gv[h];
+        R.gout[i] = R.gacc ? R.gout[i] + gv[h] : gv[h];
       } else {
         const float m = R.c1 * gv[h] + R.decay * o_mu[h];
         const float v = R.c1 * (gv[h] * gv[h]) + R.decay * o_nu[h];

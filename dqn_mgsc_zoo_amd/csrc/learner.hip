@@ -241,7 +241,8 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 // meta_p != null: per-sample cotangents p_b * (-clip(td_b)) (MGSC meta mode).
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
-                     const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0) {
+                     const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
+                     int gacc = 0) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -275,6 +276,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   rms.c1 = (float)(1.0 - (double)L->cfg.decay);
   rms.eps = L->cfg.eps;
   rms.gout = gout;
+  rms.gacc = gacc;
 
   HeadArgs h = make_head(L, nz, Z, B);
   h.fwd_only = 0;
@@ -616,12 +618,19 @@ int dqz_target_copy(float* target, const float* online, int64_t total, void* str
 
 struct dqz_meta {
   dqz_meta_config cfg;
-  dqz_learner* lm;   // meta batch learner (B = M)
+  // Meta batches larger than the learner's MAXB run in K chunks of C samples
+  // (the last one padded with p = 0 samples): G accumulates over the chunks,
+  // and once v is known each chunk's backward signals are recomputed for the
+  // tangent pass (K = 1 keeps them from the first pass).
+  int C, K;
+  dqz_learner* lm;   // meta batch learner (B = C)
   dqz_learner* l1;   // one-transition learner (B = 1)
   int64_t total;
   float *G, *thp, *mu1, *nu1, *J;  // [total] each; G also holds g', thp also holds v
   float *zv1, *zv2, *zv3, *zvp;    // tangent forward outputs
-  float *x, *p, *s, *dl, *loss, *loss_part;
+  float *x, *p, *s, *dl, *loss, *loss_part, *td;  // p, s, td: [K C] (p = 0 past M)
+  int32_t* slots_pad;                                // [K C]
+  float* Gs;                                         // [total] scratch gradient of the recompute pass (K > 1)
   int nparts;
   // second-order (reservoir) meta-gradient
   float *GQ, *HQ, *s1_part;
@@ -634,10 +643,11 @@ extern "C" {
 
 int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
   if (!cfg || !out) return fail(DQZ_ERR_INVALID, "null argument");
-  if (cfg->meta_batch < 1 || cfg->meta_batch > MAXB)
-    return fail(DQZ_ERR_UNSUPPORTED, "meta_batch must be in [1, %d]", MAXB);
+  if (cfg->meta_batch < 1 || cfg->meta_batch > (1 << 26))
+    return fail(DQZ_ERR_INVALID, "meta_batch must be in [1, 2^26]");
+  const int C = std::min(cfg->meta_batch, MAXB), K = (cfg->meta_batch + C - 1) / C;
   dqz_learner_config lc;
-  lc.batch = cfg->meta_batch;
+  lc.batch = C;
   lc.num_actions = cfg->num_actions;
   lc.algo = DQZ_ALGO_DQN;
   lc.learning_rate = cfg->learning_rate;
@@ -646,6 +656,8 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
   lc.grad_error_bound = cfg->grad_error_bound;
   dqz_meta* H = new dqz_meta();
   H->cfg = *cfg;
+  H->C = C;
+  H->K = K;
   if (int rc = dqz_learner_create(&lc, &H->lm)) {
     delete H;
     return rc;
@@ -657,21 +669,24 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
     return rc;
   }
   const int M = cfg->meta_batch;
+  const int64_t KC = (int64_t)K * C, multi = K > 1 ? 1 : 0;
   H->total = H->lm->total;
   H->nparts = (int)((H->total / 4 + 255) / 256);
   H->nparts2 = (int)((H->total + 255) / 256);
   const int64_t so = cfg->second_order ? 1 : 0;
   const int64_t sizes[] = {H->total, H->total, H->total, H->total, H->total,
-                           (int64_t)M * C1M * C1CO, (int64_t)M * C2M * C2CO, (int64_t)M * FLAT,
-                           (int64_t)H->lm->S_fc1 * M * HID,
-                           M, M, M, M, 1, H->nparts2,
+                           (int64_t)C * C1M * C1CO, (int64_t)C * C2M * C2CO, (int64_t)C * FLAT,
+                           (int64_t)H->lm->S_fc1 * C * HID,
+                           M, KC, KC, M, 1, H->nparts2, KC, KC, multi * H->total,
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * HID, so * FLAT,
                            so * C2M * C2CO, so * C1M * C1CO};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
-                    &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part,
+                    &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
+                    reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
                     &H->ty1, &H->ty2, &H->ty3, &H->th4, &H->td4, &H->td3, &H->td2, &H->td1};
+  static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
   if (hipMalloc(&H->block, tot * sizeof(float)) != hipSuccess || hipMemset(H->block, 0, tot * sizeof(float)) != hipSuccess) {
@@ -711,12 +726,22 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   dqz_learner* L = H->lm;
   const int M = H->cfg.meta_batch, A = H->cfg.num_actions;
 
-  // p = softmax(logits[pos])
+  const int C = H->C, K = H->K;
+
+  // p = softmax(logits[pos]); slots padded to K C with slots[M - 1] (p = 0 there)
   hipLaunchKernelGGL(meta_softmax_kernel, dim3(1), dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p);
+  hipLaunchKernelGGL(meta_pad_slots_kernel, dim3((unsigned)((K * C + 255) / 256)), dim3(256), 0, st, slots, M,
+                     K * C, H->slots_pad);
   DQZ_HIP(hipGetLastError());
 
-  // G = sum_i p_i g_i: one batched backward with p-weighted cotangents.
-  if (int rc = step_impl(L, P, S, slots, nullptr, stream, kNoProfile, H->G, H->p)) return rc;
+  // G = sum_i p_i g_i: batched backwards with p-weighted cotangents, one per
+  // chunk of C samples, accumulated in chunk order (deterministic).
+  for (int k = 0; k < K; ++k) {
+    if (int rc = step_impl(L, P, S, H->slots_pad + (int64_t)k * C, nullptr, stream, kNoProfile, H->G,
+                           H->p + (int64_t)k * C, nullptr, 0, k > 0 ? 1 : 0))
+      return rc;
+    DQZ_HIP(hipMemcpyAsync(H->td + (int64_t)k * C, L->td, sizeof(float) * C, hipMemcpyDeviceToDevice, st));
+  }
 
   MetaRmsArgs ra;
   ra.lr = H->cfg.learning_rate;
@@ -809,71 +834,79 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   }
   const float* v = H->thp;
 
-  // Tangent forward over the stored online activations: V * y + vb per layer.
+  // Tangent forward over the stored online activations: V * y + vb per layer,
+  // chunk by chunk (K > 1: the chunk's forward / backward is recomputed first
+  // so L holds its activations and p-weighted backward signals).
   NetZ nv;
   nv.p[0] = nv.p[1] = nv.p[2] = v;
   nv.which[0] = nv.which[1] = nv.which[2] = 0;
-  Conv1FwdArgs c1;
-  c1.src = Conv1Src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
-  c1.nz = nv;
-  c1.w_off = L->off[0];
-  c1.b_off = L->off[1];
-  c1.B = M;
-  c1.Z = 1;
-  c1.linear = 1;
-  c1.out = H->zv1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, M), dim3(256), kConv1FwdSmem, st, c1);
-  DQZ_HIP(hipGetLastError());
-  LayerFwdArgs c2;
-  c2.in = L->y1;
-  c2.nz = nv;
-  c2.w_off = L->off[2];
-  c2.b_off = L->off[3];
-  c2.B = M;
-  c2.Z = 1;
-  c2.linear = 1;
-  c2.out = H->zv2;
-  hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, M), dim3(256), 0, st, c2);
-  DQZ_HIP(hipGetLastError());
-  LayerFwdArgs c3 = c2;
-  c3.in = L->y2;
-  c3.w_off = L->off[4];
-  c3.b_off = L->off[5];
-  c3.out = H->zv3;
-  hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, M), dim3(256), 0, st, c3);
-  DQZ_HIP(hipGetLastError());
-  Fc1FwdArgs f1;
-  f1.in = L->y3;
-  f1.nz = nv;
-  f1.w_off = L->off[6];
-  f1.B = M;
-  f1.MG = (M + 31) / 32;
-  f1.part = H->zvp;
-  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, f1.MG), dim3(256), 0, st, f1);
-  DQZ_HIP(hipGetLastError());
+  for (int k = 0; k < K; ++k) {
+    const int32_t* ks = H->slots_pad + (int64_t)k * C;
+    if (K > 1) {
+      if (int rc = step_impl(L, P, S, ks, nullptr, stream, kNoProfile, H->Gs, H->p + (int64_t)k * C)) return rc;
+    }
+    Conv1FwdArgs c1;
+    c1.src = Conv1Src{S->frames, S->fidx, ks, nullptr, 0, UniformDraw{}};
+    c1.nz = nv;
+    c1.w_off = L->off[0];
+    c1.b_off = L->off[1];
+    c1.B = C;
+    c1.Z = 1;
+    c1.linear = 1;
+    c1.out = H->zv1;
+    hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, C), dim3(256), kConv1FwdSmem, st, c1);
+    DQZ_HIP(hipGetLastError());
+    LayerFwdArgs c2;
+    c2.in = L->y1;
+    c2.nz = nv;
+    c2.w_off = L->off[2];
+    c2.b_off = L->off[3];
+    c2.B = C;
+    c2.Z = 1;
+    c2.linear = 1;
+    c2.out = H->zv2;
+    hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, C), dim3(256), 0, st, c2);
+    DQZ_HIP(hipGetLastError());
+    LayerFwdArgs c3 = c2;
+    c3.in = L->y2;
+    c3.w_off = L->off[4];
+    c3.b_off = L->off[5];
+    c3.out = H->zv3;
+    hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, C), dim3(256), 0, st, c3);
+    DQZ_HIP(hipGetLastError());
+    Fc1FwdArgs f1;
+    f1.in = L->y3;
+    f1.nz = nv;
+    f1.w_off = L->off[6];
+    f1.B = C;
+    f1.MG = (C + 31) / 32;
+    f1.part = H->zvp;
+    hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, f1.MG), dim3(256), 0, st, f1);
+    DQZ_HIP(hipGetLastError());
 
-  MetaDotArgs md;
-  md.dy1 = L->dy1;
-  md.dy2 = L->dy2;
-  md.dy3 = L->dy3;
-  md.dz1 = L->dz1;
-  md.gq = L->gq;
-  md.ga = L->ga;
-  md.zv1 = H->zv1;
-  md.zv2 = H->zv2;
-  md.zv3 = H->zv3;
-  md.zvp = H->zvp;
-  md.S = FC1_S;
-  md.M = M;
-  md.A = A;
-  md.v = v;
-  md.b1_off = L->off[7];
-  md.w2_off = L->off[8];
-  md.b2_off = L->off[9];
-  md.h1 = L->h1;
-  md.s_out = H->s;
-  hipLaunchKernelGGL(meta_dot_kernel, dim3(M), dim3(512), 0, st, md);
-  DQZ_HIP(hipGetLastError());
+    MetaDotArgs md;
+    md.dy1 = L->dy1;
+    md.dy2 = L->dy2;
+    md.dy3 = L->dy3;
+    md.dz1 = L->dz1;
+    md.gq = L->gq;
+    md.ga = L->ga;
+    md.zv1 = H->zv1;
+    md.zv2 = H->zv2;
+    md.zv3 = H->zv3;
+    md.zvp = H->zvp;
+    md.S = FC1_S;
+    md.M = C;
+    md.A = A;
+    md.v = v;
+    md.b1_off = L->off[7];
+    md.w2_off = L->off[8];
+    md.b2_off = L->off[9];
+    md.h1 = L->h1;
+    md.s_out = H->s + (int64_t)k * C;
+    hipLaunchKernelGGL(meta_dot_kernel, dim3(C), dim3(512), 0, st, md);
+    DQZ_HIP(hipGetLastError());
+  }
 
   MetaAdamArgs ad;
   ad.x = H->x;
@@ -904,7 +937,7 @@ int dqz_meta_outputs(dqz_meta* H, float* probs, float* dlogits, float* td, float
   const int M = H->cfg.meta_batch;
   if (probs) DQZ_HIP(hipMemcpyAsync(probs, H->p, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
   if (dlogits) DQZ_HIP(hipMemcpyAsync(dlogits, H->dl, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
-  if (td) DQZ_HIP(hipMemcpyAsync(td, H->lm->td, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
+  if (td) DQZ_HIP(hipMemcpyAsync(td, H->td, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
   if (loss) DQZ_HIP(hipMemcpyAsync(loss, H->loss, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }

@@ -44,21 +44,30 @@ __device__ __forceinline__ float block_max_f32(float v, float* sbuf) {
 }
 
 // p = exp(x - (c + log(sum exp(x - c)))), c = max x  (JNPprobabilities_from_logits,
-// replay_circular.py:79-86).  One block; x gathered from logits[pos].
+// replay_circular.py:79-86).  One block striding over the M meta-batch
+// entries; x gathered from logits[pos].
 __global__ __launch_bounds__(META_THREADS) void meta_softmax_kernel(const float* __restrict__ logits,
                                                                     const int32_t* __restrict__ pos, int M,
                                                                     float* __restrict__ x_out,
                                                                     float* __restrict__ p_out) {
   __shared__ float sbuf[META_THREADS / 64];
-  const int i = threadIdx.x;
-  const float x = i < M ? logits[pos[i]] : -INFINITY;
-  const float c = block_max_f32(x, sbuf);
-  const float s = block_sum_f32(i < M ? expf(x - c) : 0.f, sbuf);
-  const float lse = c + logf(s);
-  if (i < M) {
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < M; i += META_THREADS) {
+    const float x = logits[pos[i]];
     x_out[i] = x;
-    p_out[i] = expf(x - lse);
+    mx = fmaxf(mx, x);
   }
+  const float c = block_max_f32(mx, sbuf);
+  float se = 0.f;
+  for (int i = threadIdx.x; i < M; i += META_THREADS) se += expf(x_out[i] - c);
+  const float lse = c + logf(block_sum_f32(se, sbuf));
+  for (int i = threadIdx.x; i < M; i += META_THREADS) p_out[i] = expf(x_out[i] - lse);
+}
+
+// slots padded to the chunked meta batch: dst[i] = src[min(i, M - 1)].
+__global__ void meta_pad_slots_kernel(const int32_t* __restrict__ src, int M, int n, int32_t* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[min(i, M - 1)];
 }
 
 struct MetaRmsArgs {
@@ -211,29 +220,30 @@ struct MetaAdamArgs {
 };
 
 // softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
-// new logits scattered back.  One block.
+// new logits scattered back.  One block striding over the M entries.
 __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) {
   __shared__ float sbuf[META_THREADS / 64];
-  const int i = threadIdx.x;
-  const float si = i < a.M ? a.s[i] : 0.f;
-  const float tot = block_sum_f32(si, sbuf);
+  float st = 0.f;
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += a.s[i];
+  const float tot = block_sum_f32(st, sbuf);
   float lp = 0.f;
-  for (int j = i; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+  for (int j = threadIdx.x; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
   lp = block_sum_f32(lp, sbuf);
   const int32_t cnt = *a.count + 1;
+  const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
   __syncthreads();
-  if (i < a.M) {
-    const float g = si - a.p[i] * tot;
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
+    const float g = a.s[i] - a.p[i] * tot;
     const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
     const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
-    const float mh = m / (1.f - powf(a.b1, (float)cnt));
-    const float vh = v / (1.f - powf(a.b2, (float)cnt));
+    const float mh = m / c1;
+    const float vh = v / c2;
     a.m[i] = m;
     a.v[i] = v;
     a.dlogits[i] = g;
     a.logits[a.pos[i]] = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
   }
-  if (i == 0) {
+  if (threadIdx.x == 0) {
     *a.count = cnt;
     *a.loss = lp;
   }

@@ -235,7 +235,7 @@ int dqz_target_copy(float* target, const float* online, int64_t total, void* str
 /* ---- MGSC meta-update (dqn_mgsc_batched/agent.py:104-220) -------------- */
 
 typedef struct dqz_meta_config {
-  int meta_batch;          /* M (meta_batch_size, run_atari.py:101), 1..256 */
+  int meta_batch;          /* M (meta_batch_size, run_atari.py:101), any size: batches past 256 run in chunks */
   int num_actions;         /* A; the network is dqn_atari_network (per-action bias) */
   float learning_rate;     /* inner optax.rmsprop(centered) lr, run_atari.py:218-223 */
   float decay;             /* 0.95 */

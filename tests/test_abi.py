@@ -60,8 +60,8 @@ def test_error_paths_without_a_gpu(libdqz):
   h = ctypes.c_void_p()
   assert lib.dqz_learner_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
   assert b'batch' in lib.dqz_last_error()
-  mcfg = _native.DqzMetaConfig(100000, 6, 2.5e-4, 0.95, 1e-5, 1 / 32, 2.5e-4,
+  mcfg = _native.DqzMetaConfig(0, 6, 2.5e-4, 0.95, 1e-5, 1 / 32, 2.5e-4,
                                0.9, 0.999, 1e-8)
-  assert lib.dqz_meta_create(ctypes.byref(mcfg), ctypes.byref(h)) == -3
+  assert lib.dqz_meta_create(ctypes.byref(mcfg), ctypes.byref(h)) == -1
   with pytest.raises(_native.NativeLibraryError, match='meta_batch'):
     _native.check(lib.dqz_meta_create(ctypes.byref(mcfg), ctypes.byref(h)))

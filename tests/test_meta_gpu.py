@@ -74,7 +74,7 @@ def test_learner_grad_matches_oracle(device, algo):
                                  err_msg='%s/%s' % (m, n))
 
 
-@pytest.mark.parametrize('meta_batch', [8, 100])
+@pytest.mark.parametrize('meta_batch', [8, 100, 300])
 def test_meta_update_matches_oracle(device, meta_batch):
   from dqn_mgsc_zoo_amd import learner as learner_lib
   from dqn_mgsc_zoo_amd import networks
@@ -93,8 +93,8 @@ def test_meta_update_matches_oracle(device, meta_batch):
   av = (1e-6 * rng.random(meta_batch)).astype(np.float32)
   meta.set_state({'count': 2, 'mu': am, 'nu': av})
 
-  capacity = 256
-  st, host = _store(capacity, 640, a, 25, device)
+  capacity = max(256, 2 * meta_batch)  # 300: two chunks of 256, the second padded
+  st, host = _store(capacity, 2 * capacity + 128, a, 25, device)
   slots = rng.choice(capacity, meta_batch, replace=False).astype(np.int32)
   cap_logits = 1000
   logits = rng.standard_normal(cap_logits).astype(np.float32)
@@ -136,13 +136,14 @@ def test_meta_update_matches_oracle(device, meta_batch):
   np.testing.assert_allclose(state['mu'], ref['adam_m'], atol=2e-3 * scale)
 
 
-@pytest.mark.parametrize('bound', [5.0, 1.0 / 32])
-def test_second_order_meta_update_matches_oracle(device, bound):
-  """dqn_mgsc_batched_reservoir: no stop_gradient on theta'' (HVP path)."""
+@pytest.mark.parametrize('bound,meta_batch', [(5.0, 8), (1.0 / 32, 8), (5.0, 260)])
+def test_second_order_meta_update_matches_oracle(device, bound, meta_batch):
+  """dqn_mgsc_batched_reservoir: no stop_gradient on theta'' (HVP path);
+  meta_batch 260 runs as two chunks (256 + 4 padded to 256)."""
   from dqn_mgsc_zoo_amd import learner as learner_lib
   from dqn_mgsc_zoo_amd import networks
   from dqn_mgsc_zoo_amd import replay as replay_lib
-  a, meta_batch = 6, 8
+  a = 6
   net = networks.dqn_atari_network(a)
   online = net.init(51)
   target = helpers.perturbed_tree(online, 52)
@@ -153,11 +154,11 @@ def test_second_order_meta_update_matches_oracle(device, bound):
   meta = learner_lib.MetaLearner(lrn, meta_batch, learner_lib.adam(2.5e-4),
                                  second_order=True)
   rng = np.random.default_rng(54)
-  capacity = 128
-  st, host = _store(capacity, 320, a, 55, device)
+  capacity = max(128, 2 * meta_batch)
+  st, host = _store(capacity, 2 * capacity + 64, a, 55, device)
   slots = rng.choice(capacity, meta_batch, replace=False).astype(np.int32)
-  logits = rng.standard_normal(64).astype(np.float32)
-  pos = rng.choice(64, meta_batch, replace=False).astype(np.int32)
+  logits = rng.standard_normal(max(64, 2 * meta_batch)).astype(np.float32)
+  pos = rng.choice(logits.size, meta_batch, replace=False).astype(np.int32)
   ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
   ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
   ot = replay_lib.Transition(ot_tm1, 2, 1.0, 0.99, ot_t)
