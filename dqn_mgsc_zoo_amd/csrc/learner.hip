@@ -573,8 +573,13 @@ int dqz_sumtree_set(double* tree, int64_t cap, const int64_t* idx, const double*
   if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
   if (n < 0 || n > 65536) return fail(DQZ_ERR_INVALID, "n out of range");
   if (n == 0) return DQZ_OK;
-  hipLaunchKernelGGL(sumtree_set_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, tree_levels(cap), idx,
-                     values, n);
+  const int levels = tree_levels(cap);
+  if (n <= ST_FAST && levels <= 32)
+    hipLaunchKernelGGL(sumtree_set_small_kernel, dim3(1), dim3(ST_FAST), 0, (hipStream_t)stream, tree, cap, levels,
+                       idx, values, n);
+  else
+    hipLaunchKernelGGL(sumtree_set_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, levels, idx,
+                       values, n);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }

@@ -117,11 +117,30 @@ __global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float*
   if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
 }
 
+// Inclusive scan of one double per thread over the block, in a fixed
+// (Hillis-Steele) order: deterministic run to run.
+__device__ __forceinline__ double block_scan_incl_f64(double v, double* s) {
+  const int t = threadIdx.x;
+  s[t] = v;
+  __syncthreads();
+#pragma unroll
+  for (int o = 1; o < SM_THREADS; o <<= 1) {
+    const double add = t >= o ? s[t - o] : 0.0;
+    __syncthreads();
+    v += add;
+    s[t] = v;
+    __syncthreads();
+  }
+  return v;
+}
+
 // One block per query u: find the chunk whose normalised cumulative sum
-// first exceeds u (block sums scanned by one lane), then inside the chunk a
-// 256-way parallel prefix (16 logits per lane) and a 16-step scan by the lane
-// that holds the crossing.  Returns the first index with cdf > u
-// (searchsorted side='right'); cdf = cumsum(float64(p)) / total.
+// first exceeds u, then inside the chunk the lane (16 logits each) and the
+// logit.  Both levels are parallel: each lane sums a contiguous run of block
+// sums / holds 16 logits, a block-wide scan gives the exclusive prefixes,
+// and the first crossing is the minimum index any lane finds.  Returns the
+// first index with cdf > u (searchsorted side='right'); cdf = cumsum(float64
+// p) / total.
 constexpr int SM_PER_LANE = SM_CHUNK / SM_THREADS;  // 16
 
 __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float* __restrict__ x, int64_t n,
@@ -130,66 +149,67 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float*
                                                                     const double* __restrict__ uniforms,
                                                                     int64_t* __restrict__ out) {
   __shared__ double s_scan[SM_THREADS];
-  __shared__ double s_tot, s_before;
+  __shared__ double s_before;
   __shared__ int s_blk;
-  __shared__ int64_t s_idx;
+  __shared__ unsigned long long s_idx;
+  const int t = threadIdx.x;
   const float L = *lse;
   const double u = uniforms[blockIdx.x];
-  if (threadIdx.x == 0) {
-    double tot = 0.0;
-    for (int b = 0; b < nblocks; ++b) tot += bsum[b];
-    double run = 0.0;
-    int blk = nblocks - 1;
-    for (int b = 0; b < nblocks; ++b) {
+  // level 1: lane t owns block sums [t seg, (t + 1) seg)
+  const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
+  const int b0 = min(t * seg, nblocks), b1 = min(b0 + seg, nblocks);
+  double mine = 0.0;
+  for (int b = b0; b < b1; ++b) mine += bsum[b];
+  if (t == 0) {
+    s_blk = nblocks - 1;
+    s_idx = ~0ull;
+  }
+  const double incl = block_scan_incl_f64(mine, s_scan);
+  const double tot = s_scan[SM_THREADS - 1];
+  {
+    double run = incl - mine;
+    for (int b = b0; b < b1; ++b) {
       if ((run + bsum[b]) / tot > u) {
-        blk = b;
+        atomicMin(&s_blk, b);
         break;
       }
       run += bsum[b];
     }
-    s_tot = tot;
-    s_blk = blk;
-    s_before = run;
-    s_idx = -1;
   }
   __syncthreads();
-  const int64_t base = (int64_t)s_blk * SM_CHUNK + threadIdx.x * SM_PER_LANE;
+  const int blk = s_blk;
+  if (blk >= b0 && blk < b1) {  // the owner of the crossing block publishes the mass before it
+    double run = incl - mine;
+    for (int b = b0; b < blk; ++b) run += bsum[b];
+    s_before = run;
+  }
+  // level 2: the chunk's 256 lanes x 16 logits
+  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
   double p[SM_PER_LANE];
-  double mine = 0.0;
+  double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) {
     p[i] = base + i < n ? (double)expf(x[base + i] - L) : 0.0;
-    mine += p[i];
+    lane += p[i];
   }
-  s_scan[threadIdx.x] = mine;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive prefix over the 256 lane sums
-    double run = s_before;
-    for (int t = 0; t < SM_THREADS; ++t) {
-      const double v = s_scan[t];
-      s_scan[t] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
-  const double tot = s_tot;
-  double run = s_scan[threadIdx.x];
-  const double next = threadIdx.x + 1 < SM_THREADS ? s_scan[threadIdx.x + 1] : run + mine;
-  if (run / tot <= u && next / tot > u) {
+  __syncthreads();  // s_before published
+  const double lincl = block_scan_incl_f64(lane, s_scan);
+  double run = s_before + (lincl - lane);
+  if (run / tot <= u && (run + lane) / tot > u) {
     for (int i = 0; i < SM_PER_LANE; ++i) {
       run += p[i];
       if (run / tot > u) {
-        s_idx = base + i;
+        atomicMin(&s_idx, (unsigned long long)(base + i));
         break;
       }
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t idx = s_idx;
+  if (t == 0) {
+    int64_t idx = s_idx == ~0ull ? -1 : (int64_t)s_idx;
     if (idx < 0) {  // rounding at the chunk edge: last live slot of the chunk
-      const int64_t end = min(n, (int64_t)(s_blk + 1) * SM_CHUNK);
-      for (int64_t j = end - 1; j >= (int64_t)s_blk * SM_CHUNK; --j)
+      const int64_t end = min(n, (int64_t)(blk + 1) * SM_CHUNK);
+      for (int64_t j = end - 1; j >= (int64_t)blk * SM_CHUNK; --j)
         if (x[j] != -INFINITY) {
           idx = j;
           break;
@@ -221,6 +241,62 @@ __global__ __launch_bounds__(1024) void sumtree_set_kernel(double* tree, int64_t
       __hip_atomic_store(&tree[node], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+  }
+}
+
+// Fast path for small updates (n <= 256, the PER write-back of one batch):
+// every sibling on every leaf's path is fetched in one batch up front, then
+// the ancestors are rebuilt level by level in LDS.  Leaves a and b have
+// sibling ancestors exactly at level msb(a ^ b), so one O(n) pass tells each
+// leaf at which levels its sibling is itself being updated and by whom; each
+// level then costs two LDS reads and two barriers instead of a global round
+// trip.  Same left + right sums as sumtree_set_kernel (bit-identical).
+// Caller passes distinct leaves.
+constexpr int ST_FAST = 256;
+
+__global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree, int64_t cap, int levels,
+                                                                    const int64_t* idx, const double* vals, int n) {
+  __shared__ int64_t s_leaf[ST_FAST];
+  __shared__ double s_val[ST_FAST];
+  __shared__ double s_sib[32][ST_FAST];  // old sibling per level; later the new ancestor values
+  __shared__ short s_rep[32][ST_FAST];   // updated leaf whose ancestor is my sibling at level l, or -1
+  const int i = threadIdx.x;
+  const bool live = i < n;
+  const int64_t leaf = live ? cap + idx[i] : -1;
+  double v = live ? vals[i] : 0.0;
+  const double leaf_v = v;
+  for (int l0 = 0; l0 < levels; l0 += 8) {  // one batch of loads per 8 levels
+    double t8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t8[j] = live && l0 + j < levels ? tree[(leaf >> (l0 + j)) ^ 1] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (l0 + j < levels) s_sib[l0 + j][i] = t8[j];
+  }
+  for (int l = 0; l < levels; ++l) s_rep[l][i] = -1;
+  s_leaf[i] = leaf;
+  s_val[i] = v;
+  __syncthreads();
+  if (live)
+    for (int j = 0; j < n; ++j) {
+      const uint64_t d = (uint64_t)(leaf ^ s_leaf[j]);
+      if (d != 0) s_rep[63 - __builtin_clzll(d)][i] = (short)j;
+    }
+  __syncthreads();
+  for (int l = 0; l < levels; ++l) {
+    const int r = s_rep[l][i];
+    const double other = r >= 0 ? s_val[r] : s_sib[l][i];
+    const double parent = ((leaf >> l) & 1) ? other + v : v + other;
+    __syncthreads();
+    v = parent;
+    s_val[i] = v;
+    s_sib[l][i] = v;  // this level's sibling is consumed -> the new level-(l + 1) value
+    __syncthreads();
+  }
+  // stores last: a barrier would otherwise wait for every pending store
+  if (live) {
+    tree[leaf] = leaf_v;
+    for (int l = 0; l < levels; ++l) tree[leaf >> (l + 1)] = s_sib[l][i];
   }
 }
 
