@@ -31,143 +31,158 @@ struct HvpArgs {
   const float *d1, *d2, *d3, *d4; // same shapes (pre-activation grads of q[a])
   // tangent scratch
   float *ty1, *ty2, *ty3, *th4, *td4, *td3, *td2, *td1;
-  float* hq;  // output, parameter layout
+  float* hq;    // output, parameter layout
+  float* part;  // [HVP_SPLITS][C1M * C1CO] K-split partial sums of the current stage
 };
+
+// Every stage below splits its reduction (K) over blockIdx.y and writes
+// part[split][i]; hvp_fin_kernel then sums the splits in order (deterministic),
+// adds the tangent bias and applies the fixed ReLU mask.  One thread per
+// (output, split): thousands of waves instead of one long loop per output.
+constexpr int HVP_SPLITS = 16;
 
 __device__ __forceinline__ float hvp_x(const HvpArgs& a, int ih, int iw, int ci) {
   const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
   return f < 0 ? 0.f : u8n(a.frames[(int64_t)f * FB + ih * FW + iw]);
 }
 
-// 1. conv1 tangent: ydot1 = relu'(y1) (conv(x, Wdot1) + bdot1)
-__global__ void hvp_t1_kernel(HvpArgs a) {
+// out[i] = mask[i] > 0 ? bias[i % nb] + sum_s part[s][i] : 0   (mask / bias optional)
+__global__ void hvp_fin_kernel(const float* __restrict__ part, int S, int N, const float* __restrict__ mask,
+                               const float* __restrict__ bias, int nb, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  float z = bias ? bias[i % nb] : 0.f;
+  for (int s = 0; s < S; ++s) z += part[(int64_t)s * N + i];
+  out[i] = (mask == nullptr || mask[i] > 0.f) ? z : 0.f;
+}
+
+// 1. conv1 tangent partial over kernel row kh = split: conv(x, Wdot1)
+__global__ void hvp_t1_kernel(HvpArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
   if (i >= C1M * C1CO) return;
   const int p = i / C1CO, co = i % C1CO, oh = p / C1O, ow = p % C1O;
   const float* W = a.tw + a.off[0];
-  float z = a.tw[a.off[1] + co];
-  for (int kh = 0; kh < C1K; ++kh)
-    for (int kw = 0; kw < C1K; ++kw)
-      for (int ci = 0; ci < FC; ++ci)
-        z += hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci) * W[((kh * C1K + kw) * FC + ci) * C1CO + co];
-  a.ty1[i] = a.y1[i] > 0.f ? z : 0.f;
+  float z = 0.f;
+  for (int kw = 0; kw < C1K; ++kw)
+#pragma unroll
+    for (int ci = 0; ci < FC; ++ci)
+      z += hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci) * W[((kh * C1K + kw) * FC + ci) * C1CO + co];
+  a.part[(int64_t)kh * (C1M * C1CO) + i] = z;
 }
 
-// 2./3. conv2 / conv3 tangent: conv(y, Wdot) + conv(ydot, W) + bdot
+// 2./3. conv2 / conv3 tangent partial over kernel row kh: conv(y, Wdot) + conv(ydot, W)
 template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ float hvp_conv_t(const float* y, const float* yd, const float* W, const float* Wd,
-                                            int p, int co) {
+                                            int p, int co, int kh) {
   const int oh = p / OH, ow = p % OH;
   float z = 0.f;
-  for (int kh = 0; kh < K; ++kh)
-    for (int kw = 0; kw < K; ++kw)
-      for (int ci = 0; ci < CI; ++ci) {
-        const int src = ((oh * S + kh) * IH + ow * S + kw) * CI + ci;
-        const int wi = ((kh * K + kw) * CI + ci) * CO + co;
-        z += y[src] * Wd[wi] + yd[src] * W[wi];
-      }
+  for (int kw = 0; kw < K; ++kw)
+    for (int ci = 0; ci < CI; ++ci) {
+      const int src = ((oh * S + kh) * IH + ow * S + kw) * CI + ci;
+      const int wi = ((kh * K + kw) * CI + ci) * CO + co;
+      z += y[src] * Wd[wi] + yd[src] * W[wi];
+    }
   return z;
 }
 
 __global__ void hvp_t2_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
   if (i >= C2M * C2CO) return;
-  const int p = i / C2CO, co = i % C2CO;
-  const float z = a.tw[a.off[3] + co] + hvp_conv_t<C1O, C1CO, C2K, C2S, C2CO, C2O>(
-                                            a.y1, a.ty1, a.th + a.off[2], a.tw + a.off[2], p, co);
-  a.ty2[i] = a.y2[i] > 0.f ? z : 0.f;
+  a.part[(int64_t)kh * (C2M * C2CO) + i] = hvp_conv_t<C1O, C1CO, C2K, C2S, C2CO, C2O>(
+      a.y1, a.ty1, a.th + a.off[2], a.tw + a.off[2], i / C2CO, i % C2CO, kh);
 }
 
 __global__ void hvp_t3_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
   if (i >= FLAT) return;
-  const int p = i / C3CO, co = i % C3CO;
-  const float z = a.tw[a.off[5] + co] + hvp_conv_t<C2O, C2CO, C3K, 1, C3CO, C3O>(
-                                            a.y2, a.ty2, a.th + a.off[4], a.tw + a.off[4], p, co);
-  a.ty3[i] = a.y3[i] > 0.f ? z : 0.f;
+  a.part[(int64_t)kh * FLAT + i] = hvp_conv_t<C2O, C2CO, C3K, 1, C3CO, C3O>(
+      a.y2, a.ty2, a.th + a.off[4], a.tw + a.off[4], i / C3CO, i % C3CO, kh);
 }
 
-// 4. fc1 tangent (hdot) and the fc2-level backward tangent ddot4 = relu'(h) Wdot2[:, a]
+// 4. fc1 tangent partial over k in [196 s, 196 s + 196) (hdot), and the
+// fc2-level backward tangent ddot4 = relu'(h) Wdot2[:, a] (split 0)
+constexpr int HVP_FC_KS = FLAT / HVP_SPLITS;  // 196
 __global__ void hvp_t4_kernel(HvpArgs a) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
   if (n >= HID) return;
   const float *W = a.th + a.off[6], *Wd = a.tw + a.off[6];
-  float z = a.tw[a.off[7] + n];
-  for (int k = 0; k < FLAT; ++k) z += a.y3[k] * Wd[(int64_t)k * HID + n] + a.ty3[k] * W[(int64_t)k * HID + n];
-  const bool on = a.h[n] > 0.f;
-  a.th4[n] = on ? z : 0.f;
-  const int act = a.action[a.slot[0]];
-  a.td4[n] = on ? a.tw[a.off[8] + n * a.A + act] : 0.f;
+  float z = 0.f;
+  for (int k = s * HVP_FC_KS; k < (s + 1) * HVP_FC_KS; ++k)
+    z += a.y3[k] * Wd[(int64_t)k * HID + n] + a.ty3[k] * W[(int64_t)k * HID + n];
+  a.part[(int64_t)s * HID + n] = z;
+  if (s == 0) {
+    const int act = a.action[a.slot[0]];
+    a.td4[n] = a.h[n] > 0.f ? a.tw[a.off[8] + n * a.A + act] : 0.f;
+  }
 }
 
-// 5. ddot3 = relu'(y3) (Wdot1 d4 + W1 ddot4)
+// 5. ddot3 partial over n in [32 s, 32 s + 32): Wdot1 d4 + W1 ddot4
 __global__ void hvp_b3_kernel(HvpArgs a) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
   if (k >= FLAT) return;
   const float *W = a.th + a.off[6] + (int64_t)k * HID, *Wd = a.tw + a.off[6] + (int64_t)k * HID;
+  constexpr int NS = HID / HVP_SPLITS;  // 32
   float z = 0.f;
-  for (int n = 0; n < HID; ++n) z += Wd[n] * a.d4[n] + W[n] * a.td4[n];
-  a.td3[k] = a.y3[k] > 0.f ? z : 0.f;
+  for (int n = s * NS; n < (s + 1) * NS; ++n) z += Wd[n] * a.d4[n] + W[n] * a.td4[n];
+  a.part[(int64_t)s * FLAT + k] = z;
 }
 
-// 6./7. transposed-conv tangents
+// 6./7. transposed-conv tangent partials over kernel row kh = split
 template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ float hvp_convT_t(const float* d, const float* dd, const float* W, const float* Wd,
-                                             int ih, int iw, int ci) {
+                                             int ih, int iw, int ci, int kh) {
   float z = 0.f;
-  for (int kh = 0; kh < K; ++kh) {
-    const int th = ih - kh;
-    if (th < 0 || th % S) continue;
-    const int oh = th / S;
-    if (oh >= OH) continue;
-    for (int kw = 0; kw < K; ++kw) {
-      const int tw = iw - kw;
-      if (tw < 0 || tw % S) continue;
-      const int ow = tw / S;
-      if (ow >= OH) continue;
-      for (int co = 0; co < CO; ++co) {
-        const int src = (oh * OH + ow) * CO + co;
-        const int wi = ((kh * K + kw) * CI + ci) * CO + co;
-        z += d[src] * Wd[wi] + dd[src] * W[wi];
-      }
+  const int th = ih - kh;
+  if (th < 0 || th % S) return 0.f;
+  const int oh = th / S;
+  if (oh >= OH) return 0.f;
+  for (int kw = 0; kw < K; ++kw) {
+    const int tw = iw - kw;
+    if (tw < 0 || tw % S) continue;
+    const int ow = tw / S;
+    if (ow >= OH) continue;
+    for (int co = 0; co < CO; ++co) {
+      const int src = (oh * OH + ow) * CO + co;
+      const int wi = ((kh * K + kw) * CI + ci) * CO + co;
+      z += d[src] * Wd[wi] + dd[src] * W[wi];
     }
   }
   return z;
 }
 
 __global__ void hvp_b2_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
   if (i >= C2M * C2CO) return;
   const int pix = i / C2CO, ci = i % C2CO;
-  const float z = hvp_convT_t<C2O, C3CI, C3K, 1, C3CO, C3O>(a.d3, a.td3, a.th + a.off[4], a.tw + a.off[4],
-                                                            pix / C2O, pix % C2O, ci);
-  a.td2[i] = a.y2[i] > 0.f ? z : 0.f;
+  a.part[(int64_t)kh * (C2M * C2CO) + i] = hvp_convT_t<C2O, C3CI, C3K, 1, C3CO, C3O>(
+      a.d3, a.td3, a.th + a.off[4], a.tw + a.off[4], pix / C2O, pix % C2O, ci, kh);
 }
 
 __global__ void hvp_b1_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
   if (i >= C1M * C1CO) return;
   const int pix = i / C1CO, ci = i % C1CO;
-  const float z = hvp_convT_t<C1O, C2CI, C2K, C2S, C2CO, C2O>(a.d2, a.td2, a.th + a.off[2], a.tw + a.off[2],
-                                                              pix / C1O, pix % C1O, ci);
-  a.td1[i] = a.y1[i] > 0.f ? z : 0.f;
+  a.part[(int64_t)kh * (C1M * C1CO) + i] = hvp_convT_t<C1O, C2CI, C2K, C2S, C2CO, C2O>(
+      a.d2, a.td2, a.th + a.off[2], a.tw + a.off[2], pix / C1O, pix % C1O, ci, kh);
 }
 
-// 8.-12. d/deps of every weight gradient of q[a]
+// 8. d/deps of conv1's weight gradient, partial over positions [25 s, 25 s + 25);
+// row 256 = the bias (sum over positions of ddot1)
+constexpr int HVP_C1_PS = C1M / HVP_SPLITS;  // 25
 __global__ void hvp_g_conv1_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (C1KK + 1) * C1CO) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+  constexpr int N = (C1KK + 1) * C1CO;
+  if (i >= N) return;
   const int k = i / C1CO, co = i % C1CO;
   float g = 0.f;
   if (k == C1KK) {
-    for (int p = 0; p < C1M; ++p) g += a.td1[p * C1CO + co];
-    a.hq[a.off[1] + co] = g;
-    return;
+    for (int p = s * HVP_C1_PS; p < (s + 1) * HVP_C1_PS; ++p) g += a.td1[p * C1CO + co];
+  } else {
+    const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
+    for (int p = s * HVP_C1_PS; p < (s + 1) * HVP_C1_PS; ++p)
+      g += hvp_x(a, C1S * (p / C1O) + kh, C1S * (p % C1O) + kw, ci) * a.td1[p * C1CO + co];
   }
-  const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
-  for (int p = 0; p < C1M; ++p)
-    g += hvp_x(a, C1S * (p / C1O) + kh, C1S * (p % C1O) + kw, ci) * a.td1[p * C1CO + co];
-  a.hq[a.off[0] + k * C1CO + co] = g;
+  a.part[(int64_t)s * N + i] = g;
 }
 
 template <int IH, int CI, int K, int S, int CO, int OH>

@@ -638,7 +638,7 @@ struct dqz_meta {
   float* Gs;                                         // [total] scratch gradient of the recompute pass (K > 1)
   int nparts;
   // second-order (reservoir) meta-gradient
-  float *GQ, *HQ, *s1_part;
+  float *GQ, *HQ, *s1_part, *hpart;
   float *ty1, *ty2, *ty3, *th4, *td4, *td3, *td2, *td1;
   int nparts2;
   void* block;
@@ -685,12 +685,12 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            M, KC, KC, M, 1, H->nparts2, KC, KC, multi * H->total,
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * HID, so * FLAT,
-                           so * C2M * C2CO, so * C1M * C1CO};
+                           so * C2M * C2CO, so * C1M * C1CO, so * HVP_SPLITS * C1M * C1CO};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
-                    &H->ty1, &H->ty2, &H->ty3, &H->th4, &H->td4, &H->td3, &H->td2, &H->td1};
+                    &H->ty1, &H->ty2, &H->ty3, &H->th4, &H->td4, &H->td3, &H->td2, &H->td1, &H->hpart};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
@@ -818,15 +818,30 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hv.td2 = H->td2;
     hv.td1 = H->td1;
     hv.hq = H->HQ;
+    hv.part = H->hpart;
     auto g256 = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
-    hipLaunchKernelGGL(hvp_t1_kernel, g256(C1M * C1CO), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t2_kernel, g256(C2M * C2CO), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t3_kernel, g256(FLAT), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t4_kernel, g256(HID), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b3_kernel, g256(FLAT), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b2_kernel, g256(C2M * C2CO), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b1_kernel, g256(C1M * C1CO), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_g_conv1_kernel, g256((C1KK + 1) * C1CO), dim3(256), 0, st, hv);
+    auto gs = [](int64_t n, int splits) { return dim3((unsigned)((n + 255) / 256), (unsigned)splits); };
+    auto fin = [&](int S, int N, const float* mask, const float* bias, int nb, float* out) {
+      hipLaunchKernelGGL(hvp_fin_kernel, g256(N), dim3(256), 0, st, H->hpart, S, N, mask, bias, nb, out);
+    };
+    const float* tw = H->nu1;
+    hipLaunchKernelGGL(hvp_t1_kernel, gs(C1M * C1CO, C1K), dim3(256), 0, st, hv);
+    fin(C1K, C1M * C1CO, L1->y1, tw + L1->off[1], C1CO, H->ty1);
+    hipLaunchKernelGGL(hvp_t2_kernel, gs(C2M * C2CO, C2K), dim3(256), 0, st, hv);
+    fin(C2K, C2M * C2CO, L1->y2, tw + L1->off[3], C2CO, H->ty2);
+    hipLaunchKernelGGL(hvp_t3_kernel, gs(FLAT, C3K), dim3(256), 0, st, hv);
+    fin(C3K, FLAT, L1->y3, tw + L1->off[5], C3CO, H->ty3);
+    hipLaunchKernelGGL(hvp_t4_kernel, gs(HID, HVP_SPLITS), dim3(256), 0, st, hv);
+    fin(HVP_SPLITS, HID, L1->h1, tw + L1->off[7], HID, H->th4);
+    hipLaunchKernelGGL(hvp_b3_kernel, gs(FLAT, HVP_SPLITS), dim3(256), 0, st, hv);
+    fin(HVP_SPLITS, FLAT, L1->y3, nullptr, 1, H->td3);
+    hipLaunchKernelGGL(hvp_b2_kernel, gs(C2M * C2CO, C3K), dim3(256), 0, st, hv);
+    fin(C3K, C2M * C2CO, L1->y2, nullptr, 1, H->td2);
+    hipLaunchKernelGGL(hvp_b1_kernel, gs(C1M * C1CO, C2K), dim3(256), 0, st, hv);
+    fin(C2K, C1M * C1CO, L1->y1, nullptr, 1, H->td1);
+    // conv1 w rows 0..255 and its bias row are contiguous in the layout (off[1] = off[0] + 8192)
+    hipLaunchKernelGGL(hvp_g_conv1_kernel, gs((C1KK + 1) * C1CO, HVP_SPLITS), dim3(256), 0, st, hv);
+    fin(HVP_SPLITS, (C1KK + 1) * C1CO, nullptr, nullptr, 1, H->HQ + L1->off[0]);
     hipLaunchKernelGGL(hvp_g_conv23_kernel, g256((C2KK + 1) * C2CO + (C3KK + 1) * C3CO), dim3(256), 0, st, hv);
     hipLaunchKernelGGL(hvp_g_fc_kernel, g256((int64_t)FLAT * HID + HID + (int64_t)HID * A + A), dim3(256), 0, st,
                        hv);
