@@ -514,12 +514,13 @@ int dqz_logit_buffer_destroy(dqz_logit_buffer* b) {
   return DQZ_OK;
 }
 
-static int logits_lse(dqz_logit_buffer* b, const float* logits, float* write_logits, int64_t write_pos,
-                      int64_t size, float* lse_out, hipStream_t st) {
-  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part);
+static int logits_lse(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
+                      float* lse_out, hipStream_t st) {
+  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
+                     clear_pos);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part, b->nblocks, lse_out ? lse_out : b->lse,
-                     write_logits, write_pos, size);
+                     logits, write_pos, size);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -531,11 +532,8 @@ int dqz_logits_add(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_
     return fail(DQZ_ERR_INVALID, "position out of range");
   if (size < 0) return fail(DQZ_ERR_INVALID, "size must be >= 0");
   hipStream_t st = (hipStream_t)stream;
-  if (clear_pos >= 0) {
-    hipLaunchKernelGGL(logit_clear_kernel, dim3(1), dim3(64), 0, st, logits, clear_pos);
-    DQZ_HIP(hipGetLastError());
-  }
-  if (int rc = logits_lse(b, logits, logits, write_pos, size, lse_out, st)) return rc;
+  // the reservoir `replace` clear (logits[clear_pos] = -inf) happens inside pass 1
+  if (int rc = logits_lse(b, logits, clear_pos, write_pos, size, lse_out, st)) return rc;
   if (lse_out) DQZ_HIP(hipMemcpyAsync(b->lse, lse_out, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }
@@ -545,9 +543,11 @@ int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* un
   if (!b || !logits || !uniforms || !out_idx) return fail(DQZ_ERR_INVALID, "null argument");
   if (n < 1 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
   hipStream_t st = (hipStream_t)stream;
-  if (int rc = logits_lse(b, logits, nullptr, -1, 0, nullptr, st)) return rc;
-  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse,
-                     b->bsum);
+  // pass 1 never writes when clear_pos < 0
+  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
+                     b->capacity, b->part, (int64_t)-1);
+  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
+                     b->nblocks, b->lse, b->bsum);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(softmax_choice_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse, b->bsum,
                      b->nblocks, uniforms, out_idx);

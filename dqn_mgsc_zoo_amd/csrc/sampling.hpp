@@ -51,21 +51,58 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sbuf) {
   return r;
 }
 
-// Pass 1: per-block (max, sum exp) of logits[n].
-__global__ __launch_bounds__(SM_THREADS) void lse_partial_kernel(const float* __restrict__ x, int64_t n,
-                                                                 MaxSum* __restrict__ part) {
+// Pass 1: per-block (max, sum exp) of logits[n].  Each lane holds 16 logits
+// (float4 loads), takes their max, then sums exp(x - max): one expf per logit.
+// clear_pos (>= 0): that slot is set to -inf first (the reservoir replace)
+// by the block that owns it, which is the only block that reads it.
+__global__ __launch_bounds__(SM_THREADS) void lse_partial_kernel(float* __restrict__ x, int64_t n,
+                                                                 MaxSum* __restrict__ part, int64_t clear_pos) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
   const int64_t base = (int64_t)blockIdx.x * SM_CHUNK;
-  MaxSum acc{-INFINITY, 0.f};
-  for (int i = threadIdx.x; i < SM_CHUNK; i += SM_THREADS) {
-    const int64_t j = base + i;
-    if (j < n) {
-      const float v = x[j];
-      if (v != -INFINITY) acc = ms_combine(acc, MaxSum{v, 1.f});
+  float v[SM_CHUNK / SM_THREADS];
+#pragma unroll
+  for (int q = 0; q < SM_CHUNK / SM_THREADS / 4; ++q) {
+    const int64_t j = base + 4 * (threadIdx.x + SM_THREADS * q);
+    float4 f = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    if (j + 3 < n && (reinterpret_cast<uintptr_t>(x + j) & 15) == 0) {
+      f = *reinterpret_cast<const float4*>(x + j);
+    } else {
+      if (j < n) f.x = x[j];
+      if (j + 1 < n) f.y = x[j + 1];
+      if (j + 2 < n) f.z = x[j + 2];
+      if (j + 3 < n) f.w = x[j + 3];
     }
+    if (clear_pos >= j && clear_pos < j + 4) {
+      const int e = (int)(clear_pos - j);
+      if (e == 0) f.x = -INFINITY;
+      if (e == 1) f.y = -INFINITY;
+      if (e == 2) f.z = -INFINITY;
+      if (e == 3) f.w = -INFINITY;
+      x[clear_pos] = -INFINITY;
+    }
+    v[4 * q] = f.x;
+    v[4 * q + 1] = f.y;
+    v[4 * q + 2] = f.z;
+    v[4 * q + 3] = f.w;
   }
-  acc = block_reduce_ms(acc, sbuf);
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < SM_CHUNK / SM_THREADS; ++i) m = fmaxf(m, v[i]);
+  float sum = 0.f;
+  if (m != -INFINITY) {
+#pragma unroll
+    for (int i = 0; i < SM_CHUNK / SM_THREADS; ++i) sum += v[i] == -INFINITY ? 0.f : expf(v[i] - m);
+  }
+  const MaxSum acc = block_reduce_ms(MaxSum{m, sum}, sbuf);
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+// (max, sum) of all block partials, every lane combining a strided subset in
+// a fixed order: any block that calls it gets the same bits.
+__device__ __forceinline__ MaxSum combine_parts(const MaxSum* __restrict__ part, int nparts, MaxSum* sbuf) {
+  MaxSum acc{-INFINITY, 0.f};
+  for (int i = threadIdx.x; i < nparts; i += SM_THREADS) acc = ms_combine(acc, part[i]);
+  return block_reduce_ms(acc, sbuf);
 }
 
 // Pass 2 (one block): lse = m + log(s); optional logit write of a new item:
@@ -74,19 +111,12 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
                                                                float* lse_out, float* logits, int64_t write_pos,
                                                                int64_t size) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
-  MaxSum acc{-INFINITY, 0.f};
-  for (int i = threadIdx.x; i < nparts; i += SM_THREADS) acc = ms_combine(acc, part[i]);
-  acc = block_reduce_ms(acc, sbuf);
+  const MaxSum acc = combine_parts(part, nparts, sbuf);
   if (threadIdx.x == 0) {
     const float lse = acc.m == -INFINITY ? -INFINITY : acc.m + logf(acc.s);
     if (lse_out) *lse_out = lse;
     if (logits && write_pos >= 0) logits[write_pos] = size == 0 ? 0.f : lse - logf((float)size);
   }
-}
-
-// Sets logits[pos] = -inf before a log-mean-exp (MGSCReservoirDistribution.replace).
-__global__ void logit_clear_kernel(float* logits, int64_t pos) {
-  if (threadIdx.x == 0) logits[pos] = -INFINITY;
 }
 
 // Uniform doubles in [0, 1) from Philox (53-bit mantissa), counter advanced on device.
@@ -101,19 +131,25 @@ __global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, d
   if (threadIdx.x == 0) *counter = ctr + 1;
 }
 
-// Per-block float64 sums of p = exp(x - lse) (f32 p, widened like numpy's choice).
+// Per-block float64 sums of p = exp(x - lse) (f32 p, widened like numpy's
+// choice).  lse is recombined from pass 1's partials by every block (same
+// bits as lse_final_kernel); block 0 publishes it for the choice kernel.
 __global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float* __restrict__ x, int64_t n,
-                                                                    const float* __restrict__ lse,
+                                                                    const MaxSum* __restrict__ part, int nparts,
+                                                                    float* __restrict__ lse_out,
                                                                     double* __restrict__ bsum) {
-  __shared__ double sbuf[SM_THREADS / 64];
-  const float L = *lse;
+  __shared__ MaxSum sbuf[SM_THREADS / 64];
+  __shared__ double dbuf[SM_THREADS / 64];
+  const MaxSum t = combine_parts(part, nparts, sbuf);
+  const float L = t.m == -INFINITY ? -INFINITY : t.m + logf(t.s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *lse_out = L;
   const int64_t base = (int64_t)blockIdx.x * SM_CHUNK;
   double acc = 0.0;
   for (int i = threadIdx.x; i < SM_CHUNK; i += SM_THREADS) {
     const int64_t j = base + i;
     if (j < n) acc += (double)expf(x[j] - L);
   }
-  acc = block_sum_f64(acc, sbuf);
+  acc = block_sum_f64(acc, dbuf);
   if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
 }
 
