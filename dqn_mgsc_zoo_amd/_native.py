@@ -110,6 +110,7 @@ SIGNATURES = {
          _vp, _vp],
     ),
     'dqz_learner_outputs': (_int, [_vp, _vp, _vp, _vp, _vp]),
+    'dqz_learner_sync_status': (_int, [_vp, _vp]),
     'dqz_learner_profile': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,

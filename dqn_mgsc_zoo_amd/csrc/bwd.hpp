@@ -199,8 +199,14 @@ struct Conv3BwdArgs {
   float* dy2;        // [B][81][64]
   float* part;       // [B][577][64]
   int B;
+  Handoff sync;      // per-sample dy2 arrival counters (bwd_bc_kernel)
 };
 
+// PUB: dy2 is handed to conv2 dX inside the same launch (bwd_bc_kernel): every
+// dy2 store is write-through (sc1), every storing wave drains (vmcnt(0)), and
+// after the workgroup barrier one lane adds to the sample's arrival counter
+// (MI355X_MICROARCH.md visibility table, row 1; the consumer loads sc1).
+template <bool PUB>
 __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win, int b, int nq, int mh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -274,9 +280,14 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     const int p = 48 * mh + (i >> 4);
     if (p < C2M) {
       const float v = (s_red[i] + s_red[768 + i]) + (s_red[1536 + i] + s_red[2304 + i]);
-      a.dy2[((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15)] = ym[k] > 0.f ? v : 0.f;
+      float* dst = a.dy2 + ((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15);
+      if constexpr (PUB)
+        __hip_atomic_store(dst, ym[k] > 0.f ? v : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *dst = ym[k] > 0.f ? v : 0.f;
     }
   }
+  if constexpr (PUB) a.sync.arrive(b);
 }
 
 __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq) {
@@ -356,8 +367,14 @@ struct Conv2BwdArgs {
   float* dy1;        // [B][400][32]
   float* part;       // [B][513][64]
   int B;
+  Handoff sync;      // dy2 arrival counters (WAIT)
 };
 
+// WAIT: dy2 of sample b is produced by the 8 conv3 dX jobs of the same launch
+// (bwd_bc_kernel).  Weights and relu'(y1) are loaded first, then one lane
+// polls the sample's counter, and every dy2 load is an sc1 (L1-bypassing)
+// buffer load.
+template <bool WAIT>
 __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -376,13 +393,19 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   const float4* src = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * (C2M * C2CO));
   constexpr int NW4 = 121 * 16;  // 1936
+  if constexpr (WAIT) a.sync.wait(b);
   float4 r[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int i = min(t + 256 * q, NW4 - 1);
     const int pix = i >> 4, oh = pix / 11 - 1, ow = pix % 11 - 1;
     const bool in = oh >= 0 && oh < C2O && ow >= 0 && ow < C2O;
-    const float4 v = src[(in ? oh * C2O + ow : 0) * 16 + (i & 15)];
+    const int e = (in ? oh * C2O + ow : 0) * 16 + (i & 15);
+    float4 v;
+    if constexpr (WAIT)
+      v = load_sc1_f4(src, C2M * C2CO * 4, e);
+    else
+      v = src[e];
     r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
@@ -627,7 +650,7 @@ __global__ __launch_bounds__(256) void bwd_b_kernel(Conv3BwdArgs c3, Fc1BwdArgs 
     const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c3.B);
     if (!sj.valid) return;
     DQZ_STAMP(6, 0);
-    conv3_bwd_dx(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
+    conv3_bwd_dx<false>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
     DQZ_STAMP(6, 3);
   } else {
     fc1_dw_body(f1, smem, blockIdx.x - n3);
@@ -641,7 +664,7 @@ __global__ __launch_bounds__(256) void bwd_c_kernel(Conv2BwdArgs c2, Conv3BwdArg
     const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c2.B);
     if (!sj.valid) return;
     DQZ_STAMP(7, 0);
-    conv2_bwd_dx(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    conv2_bwd_dx<false>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
   } else {
     const SampleJob sj = xcd_sample_job_at(blockIdx.x - n2, 4, c3.B);
@@ -650,6 +673,53 @@ __global__ __launch_bounds__(256) void bwd_c_kernel(Conv2BwdArgs c2, Conv3BwdArg
     conv3_bwd_dw(c3, smem, sj.s, sj.job);
     DQZ_STAMP(12, 3);
   }
+}
+
+// bwd_bc_kernel = bwd_b + bwd_c in one launch.  Grid, in dispatch order:
+//   [conv3 dX 8/sample] [fc1 dW 784] [conv2 dX 8/sample] [conv3 dW 4/sample]
+// conv2 dX of sample s waits (in-launch hand-off) for the 8 conv3 dX jobs of s,
+// which have lower block indices: workgroups are dispatched in index order, so
+// every producer a consumer waits on is already resident or finished and the
+// wait always terminates.  The first two ranges fill the chip (4 workgroups
+// per CU), so conv2 dX workgroups are dispatched as conv3 dX ones retire
+// instead of spinning from the start.  Sample jobs keep the XCD-aware decode
+// (each range starts at a multiple of 8, so producer and consumer share an L2).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
+    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2) {
+  constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
+  constexpr int kW2 = C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN;
+  __shared__ __attribute__((aligned(16))) float smem[kW > kW2 ? kW : kW2];
+  const int B8 = (c3.B + 7) / 8 * 8;
+  constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
+  int i = blockIdx.x;
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(6, 0);
+    conv3_bwd_dx<true>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
+    DQZ_STAMP(6, 3);
+    return;
+  }
+  i -= 8 * B8;
+  if (i < NF) {
+    fc1_dw_body(f1, smem, i);
+    return;
+  }
+  i -= NF;
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(7, 0);
+    conv2_bwd_dx<true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    DQZ_STAMP(7, 3);
+    return;
+  }
+  i -= 8 * B8;
+  const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
+  if (!sj.valid) return;
+  DQZ_STAMP(12, 0);
+  conv3_bwd_dw(c3, smem, sj.s, sj.job);
+  DQZ_STAMP(12, 3);
 }
 
 __global__ __launch_bounds__(256) void bwd_d_kernel(Conv1DwArgs c1, Conv2BwdArgs c2) {

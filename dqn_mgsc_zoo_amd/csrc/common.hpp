@@ -178,6 +178,56 @@ __device__ __forceinline__ SampleJob xcd_sample_job(int J, int nsamp) {
 
 inline dim3 xcd_grid(int J, int nsamp) { return dim3((unsigned)(J * ((nsamp + 7) / 8) * 8)); }
 
+// In-launch per-sample hand-off (fwd_conv_kernel: conv1 -> conv2 -> conv3;
+// bwd_bc_kernel: conv3 dX -> conv2 dX), the
+// form of MI355X_MICROARCH.md's visibility table row 1: producers store the
+// payload write-through (sc1), drain (vmcnt(0)) in every storing wave, meet
+// at the workgroup barrier, and one lane adds to the sample's counter
+// (agent-scope atomic); one consumer lane polls the counter with sc1 loads,
+// the workgroup barrier releases the other waves, and every payload load is
+// an sc1 load.  The last of `consumers` consumers to pass resets the
+// sample's words, so every launch starts from zero (the learner scratch is
+// zeroed at creation).  A spin that outlives ~2^24 polls sets *err and gives
+// up rather than hang the GPU.
+struct Handoff {
+  static constexpr int kStride = 64;  // one 256-byte line pair per sample word: pollers of
+                                      // different samples never share a line
+  int* cnt;  // [B * kStride] producer arrivals
+  int* ack;  // [B * kStride] consumers past the wait
+  int* err;  // timeout word (0 = ok)
+  int need, consumers;
+  __device__ __forceinline__ void arrive(int b) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + b * kStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void wait(int b) const {
+    if (threadIdx.x == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(cnt + b * kStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (__hip_atomic_fetch_add(ack + b * kStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == consumers - 1) {
+        __hip_atomic_store(cnt + b * kStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ack + b * kStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+  }
+};
+
+// 16-byte sc1 (L1-bypassing) load of element e of a float4 array of `bytes`
+// bytes whose base is wave-uniform (buffer_load_dwordx4 ... sc1).
+__device__ __forceinline__ float4 load_sc1_f4(const float4* base, int bytes, int e) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 16));
+}
+
 // Uniform replay draw of the device sampler (replay.py:119-125 distribution):
 // draw i of step `ctr` -> live slot (base + floor(u * size)) mod capacity,
 // u from Philox(counter = (ctr, i), key = seed).

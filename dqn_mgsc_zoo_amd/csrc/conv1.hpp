@@ -115,17 +115,17 @@ struct Conv1FwdArgs {
   int B, Z;
   int linear;  // 1: write the pre-activation (no ReLU)
   float* out;  // y1 [Z][B][400][32]
+  Handoff pub;  // PUB: y1 rows handed to conv2 in the same launch (fwd_conv_kernel)
 };
 
 // grid (4 row blocks, B, Z); 256 threads; each wave owns 32 positions x 32
-// channels (the 4th wave's tile is 4/32 live).
-__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
+// channels (the 4th wave's tile is 4/32 live).  PUB: y1 stores are sc1 and
+// the block arrives on its sample's counter (common.hpp Handoff).
+template <bool PUB>
+__device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* smem, const SampleJob sj) {
   DQZ_STAMP(0, 0);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_in = smem;                  // 8064
   float* s_w = smem + C1_IN_FLOATS;    // 256 x 32
-  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.Z * a.B);
-  if (!sj.valid) return;
   const int rb = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const float bias = a.nz.p[z][a.b_off + (threadIdx.x & 31)];  // epilogue operand, loaded early
   const float4* w4 = reinterpret_cast<const float4*>(a.nz.p[z] + a.w_off);
@@ -163,10 +163,21 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
     const int pos = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (pos < C1_POS) {
       const float v = acc[r] + bias;
-      out[pos * C1CO + i] = a.linear ? v : relu(v);
+      if constexpr (PUB)
+        __hip_atomic_store(out + pos * C1CO + i, a.linear ? v : relu(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        out[pos * C1CO + i] = a.linear ? v : relu(v);
     }
   }
+  if constexpr (PUB) a.pub.arrive(sj.s);
   DQZ_STAMP(0, 3);
+}
+
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.Z * a.B);
+  if (!sj.valid) return;
+  conv1_fwd_body<false>(a, smem, sj);
 }
 
 struct Conv1DwArgs {

@@ -18,6 +18,7 @@
 // Work per launch: Z x B x 4 workgroups (256 at B = 32, Z = 2).
 #pragma once
 #include "common.hpp"
+#include "conv1.hpp"
 
 namespace dqz {
 
@@ -32,6 +33,7 @@ struct LayerFwdArgs {
   int B, Z;
   int linear;  // 1: pre-activation output, no ReLU (tangent forward)
   float* out;  // [Z][B][...]
+  Handoff wait, pub;  // fwd_conv_kernel: input produced / output consumed in the same launch
 };
 
 // ---- conv2: 20x20x32 -> 9x9x64, 4x4 stride 2 -------------------------------
@@ -39,11 +41,11 @@ struct LayerFwdArgs {
 // A read for position p = 9 oh + ow: 2*oh*RS + 2*ow*S = 2p (mod 32).
 constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
 
-__global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
+// WAIT: y1 of this sample comes from conv1 blocks of the same launch (poll,
+// then sc1 window loads).  PUB: y2 stores are sc1 and the block arrives.
+template <bool WAIT, bool PUB>
+__device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(1, 0);
-  __shared__ float s_in[C2L_WIN];
-  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
-  if (!sj.valid) return;
   const int nq = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
   const int n = lane & 15, kq = lane >> 4;
@@ -54,9 +56,15 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
   for (int kk = 0; kk < 32; ++kk) wr[kk] = W[(w * 128 + 4 * kk + kq) * C2CO + 16 * nq + n];
   const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C1M * C1CO));
   constexpr int NQ4 = C1M * C1CO / 4;  // 3200
+  if constexpr (WAIT) a.wait.wait(sj.s);
   float4 r[13];
 #pragma unroll
-  for (int q = 0; q < 13; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  for (int q = 0; q < 13; ++q) {
+    if constexpr (WAIT)
+      r[q] = load_sc1_f4(src, NQ4 * 16, min(t + 256 * q, NQ4 - 1));
+    else
+      r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  }
 #pragma unroll
   for (int q = 0; q < 13; ++q) {
     const int i = t + 256 * q;
@@ -97,9 +105,21 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   for (int i = t; i < C2M * 16; i += 256) {
     const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bv;
-    out[(i >> 4) * C2CO + (i & 15)] = a.linear ? v : relu(v);
+    if constexpr (PUB)
+      __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), a.linear ? v : relu(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      out[(i >> 4) * C2CO + (i & 15)] = a.linear ? v : relu(v);
   }
+  if constexpr (PUB) a.pub.arrive(sj.s);
   DQZ_STAMP(1, 3);
+}
+
+__global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
+  __shared__ float s_in[C2L_WIN];
+  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
+  if (!sj.valid) return;
+  conv2_fwd_body<false, false>(a, s_in, sj);
 }
 
 // ---- conv3: 9x9x64 -> 7x7x64, 3x3 stride 1 ---------------------------------
@@ -107,11 +127,9 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
 // for p = 7 oh + ow: oh*RS + ow*S = 14 oh + 2 ow = 2p (mod 32).
 constexpr int C3L_S = 66, C3L_RS = 622, C3L_WIN = 9 * C3L_RS;  // 5598 floats
 
-__global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
+template <bool WAIT>
+__device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
-  __shared__ float s_in[C3L_WIN];
-  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
-  if (!sj.valid) return;
   const int nq = sj.job, b = sj.s % a.B, z = sj.s / a.B;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -123,9 +141,15 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
     wr[kk] = W[((kk >> 2) * C3CI + 16 * w + 4 * (kk & 3) + kq) * C3CO + 16 * nq + n];
   const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C2M * C2CO));
   constexpr int NQ4 = C2M * C2CO / 4;  // 1296
+  if constexpr (WAIT) a.wait.wait(sj.s);
   float4 r[6];
 #pragma unroll
-  for (int q = 0; q < 6; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  for (int q = 0; q < 6; ++q) {
+    if constexpr (WAIT)
+      r[q] = load_sc1_f4(src, NQ4 * 16, min(t + 256 * q, NQ4 - 1));
+    else
+      r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  }
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const int i = t + 256 * q;
@@ -170,6 +194,43 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
     out[(i >> 4) * C3CO + (i & 15)] = a.linear ? v : relu(v);
   }
   DQZ_STAMP(2, 3);
+}
+
+__global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
+  __shared__ float s_in[C3L_WIN];
+  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
+  if (!sj.valid) return;
+  conv3_fwd_body<false>(a, s_in, sj);
+}
+
+// ---- conv1 -> conv2 -> conv3 forward in one launch ------------------------
+// Grid, in dispatch order, over the Z x B samples s = z B + b:
+//   [conv1 4/sample] [conv2 4/sample] [conv3 4/sample]
+// conv2 blocks of sample s wait for the 4 conv1 blocks of s (y1 hand-off),
+// conv3 blocks for the 4 conv2 blocks (y2).  Producers always have lower
+// block indices (workgroups are dispatched in index order), so every wait
+// terminates; each range starts at a multiple of 8, so a sample's producer
+// and consumer blocks share an XCD (and its L2).  Consumers stage their
+// weight slices before they poll.  Dynamic LDS = conv1's 65 KB (2 blocks/CU:
+// conv1 and conv2 are co-resident from the start, conv3 blocks dispatch as
+// conv1 blocks retire).
+__global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int zb = c1.Z * c1.B, n = 4 * ((zb + 7) / 8 * 8);
+  int i = blockIdx.x;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, zb);
+    if (sj.valid) conv1_fwd_body<true>(c1, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, zb);
+    if (sj.valid) conv2_fwd_body<true, true>(c2, smem, sj);
+    return;
+  }
+  const SampleJob sj = xcd_sample_job_at(i - n, 4, zb);
+  if (sj.valid) conv3_fwd_body<true>(c3, smem, sj);
 }
 
 // ---- fc1: [B][3136] x [3136][512] split-K partials ------------------------

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -52,6 +53,9 @@ struct dqz_learner {
   int S_fc1, S2, S3;
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
   int32_t* ga;
+  int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
+  int fused_bwd;  // 1: bwd_bc_kernel + bwd_d_kernel; 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
+  int fused_fwd;  // 1: fwd_conv_kernel; 0: conv1 / conv2 / conv3 fwd launches (DQZ_FUSED_FWD=0)
   void* block;
 };
 
@@ -60,6 +64,8 @@ static int g_attr_done = 0;
 static int init_kernel_attrs() {
   if (g_attr_done) return DQZ_OK;
   DQZ_HIP(hipFuncSetAttribute((const void*)conv1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kConv1FwdSmem));
+  DQZ_HIP(hipFuncSetAttribute((const void*)fwd_conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kConv1FwdSmem));
   DQZ_HIP(hipFuncSetAttribute((const void*)bwd_d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kBwdDSmem));
@@ -90,6 +96,12 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   L->Z = cfg->algo == DQZ_ALGO_DQN ? 2 : 3;
   L->shared_bias = cfg->algo == DQZ_ALGO_DQN ? 0 : 1;
   param_layout(cfg->num_actions, L->shared_bias, L->off, L->sz, &L->total);
+  {
+    const char* e = getenv("DQZ_FUSED_BWD");
+    L->fused_bwd = !(e && e[0] == '0');
+    e = getenv("DQZ_FUSED_FWD");
+    L->fused_fwd = !(e && e[0] == '0');
+  }
   const int B = cfg->batch, Z = L->Z, A = cfg->num_actions;
   L->S_fc1 = FC1_S;
   L->S2 = B;  // per-sample conv2 dW partials (conv2_bwd_kernel)
@@ -101,10 +113,10 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 14 * B * Handoff::kStride + 64};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
-                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec};
+                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -181,8 +193,6 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.Z = Z;
   c1.linear = 0;
   c1.out = L->y1;
-  DQZ_PHASE(0, hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
-            DQZ_HIP(hipGetLastError()));
 
   LayerFwdArgs c2;
   c2.in = L->y1;
@@ -193,16 +203,32 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c2.Z = Z;
   c2.linear = 0;
   c2.out = L->y2;
-  DQZ_PHASE(1, hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
-            DQZ_HIP(hipGetLastError()));
 
   LayerFwdArgs c3 = c2;
   c3.in = L->y2;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  DQZ_PHASE(2, hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
-            DQZ_HIP(hipGetLastError()));
+  if (L->fused_fwd) {
+    // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample (Z*B <= 3B samples)
+    int* hw = L->sync + 2 * B * Handoff::kStride;
+    int* err = L->sync + 14 * B * Handoff::kStride;
+    c1.pub = Handoff{hw, hw + 3 * B * Handoff::kStride, err, 4, 4};
+    c2.wait = c1.pub;
+    c2.pub = Handoff{hw + 6 * B * Handoff::kStride, hw + 9 * B * Handoff::kStride, err, 4, 4};
+    c3.wait = c2.pub;
+    DQZ_PHASE(0, hipLaunchKernelGGL(fwd_conv_kernel, dim3(3 * xcd_grid(4, Z * B).x), dim3(256), kConv1FwdSmem, st, c1,
+                                    c2, c3);
+              DQZ_HIP(hipGetLastError()));
+    if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
+  } else {
+    DQZ_PHASE(0, hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
+              DQZ_HIP(hipGetLastError()));
+    DQZ_PHASE(1, hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
+              DQZ_HIP(hipGetLastError()));
+    DQZ_PHASE(2, hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
+              DQZ_HIP(hipGetLastError()));
+  }
 
   Fc1FwdArgs f1;
   f1.in = L->y3;
@@ -319,6 +345,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
   c3b.B = B;
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, L->sync + 14 * B * Handoff::kStride, 8, 8};
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -326,6 +353,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
   c2b.B = B;
+  c2b.sync = c3b.sync;
   Conv1DwArgs c1dw;
   c1dw.src = src;
   c1dw.src.rec = nullptr;
@@ -334,10 +362,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
   const int B8 = (B + 7) / 8 * 8;
-  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
-            DQZ_HIP(hipGetLastError()));
-  DQZ_PHASE(7, hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
-            DQZ_HIP(hipGetLastError()));
+  if (L->fused_bwd) {
+    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(8 * B8 + 8 * B8 + 4 * B8 + 4 * (FLAT / 16)), dim3(256), 0,
+                                    st, c3b, fb, c2b);
+              DQZ_HIP(hipGetLastError()));
+    if (pe.on()) pe.ms[7] = 0.f;
+  } else {
+    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
+              DQZ_HIP(hipGetLastError()));
+    DQZ_PHASE(7, hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
+              DQZ_HIP(hipGetLastError()));
+  }
   DQZ_PHASE(8, hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
             DQZ_HIP(hipGetLastError()));
 
@@ -406,6 +441,13 @@ int dqz_learner_profile(dqz_learner* L, const dqz_params* P, const dqz_store* S,
   (void)hipEventDestroy(pe.e0);
   (void)hipEventDestroy(pe.e1);
   return rc;
+}
+
+int dqz_learner_sync_status(dqz_learner* L, int* status) {
+  if (!L || !status) return fail(DQZ_ERR_INVALID, "null argument");
+  DQZ_HIP(hipDeviceSynchronize());
+  DQZ_HIP(hipMemcpy(status, L->sync + 14 * L->cfg.batch * Handoff::kStride, sizeof(int), hipMemcpyDeviceToHost));
+  return DQZ_OK;
 }
 
 int dqz_learner_outputs(dqz_learner* L, float* q_tm1, float* td, float* loss, void* stream) {

@@ -159,6 +159,12 @@ class Learner:
         _native.ptr(self.loss), _native.stream_handle(stream)))
     return self.q_tm1, self.td, self.loss
 
+  def sync_status(self):
+    """0 if every in-launch backward hand-off completed (synchronises)."""
+    st = ctypes.c_int(0)
+    _native.check(_native.lib().dqz_learner_sync_status(self._h, ctypes.byref(st)))
+    return st.value
+
   def q_values(self, states, params=None, stream=None):
     """network.apply(params, s).q_values for uint8 [n,84,84,4] device states."""
     params = self.online if params is None else params

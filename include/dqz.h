@@ -157,6 +157,11 @@ int dqz_learner_profile(dqz_learner* learner, const dqz_params* params, const dq
  * q_tm1 [B][A] online Q(s_tm1), td [B] TD errors, loss [1] mean loss. */
 int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* loss, void* stream);
 
+/* Health of the in-launch hand-offs of the backward pass: *status = 0 when
+ * every wait completed, 1 if a wait gave up (a bounded spin expired; the
+ * step's results are then invalid).  Synchronises the device. */
+int dqz_learner_sync_status(dqz_learner* learner, int* status);
+
 /* Q-values of the NatureQNetwork for uint8 HWC states [n][84][84][4]
  * (network.apply(...).q_values, networks.py:352-363; used by select_action,
  * dqn/agent.py:121-131).  q_out: device f32 [n][A]. n <= learner batch. */

@@ -221,3 +221,53 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
   q_t = lrn.q_values(torch.from_numpy(s_t).to(device))
   q_ref, _ = learner_ref.forward(ref['params'], s_t, algo != 'dqn')
   np.testing.assert_allclose(q_t.cpu().numpy(), q_ref, atol=Q_ATOL)
+
+
+@pytest.mark.parametrize('algo,batch', [('dqn', 32), ('per', 20), ('double', 64)])
+def test_fused_handoff_kernels_bit_exact(device, algo, batch, monkeypatch):
+  """fwd_conv_kernel (conv1 -> conv2 -> conv3 hand-offs) and bwd_bc_kernel
+  (conv3 dX -> conv2 dX) give the same bits as the separate launches, over
+  many steps, under hipGraph replay and after profile-mode repeated
+  launches."""
+  monkeypatch.setenv('DQZ_FUSED_BWD', '0')
+  monkeypatch.setenv('DQZ_FUSED_FWD', '0')
+  _, ref, st, _, _, _, _, _ = _setup(algo, batch, seed=21)
+  monkeypatch.setenv('DQZ_FUSED_BWD', '1')
+  monkeypatch.setenv('DQZ_FUSED_FWD', '1')
+  _, lrn, _, _, _, _, _, _ = _setup(algo, batch, seed=21)
+  rng = np.random.default_rng(22)
+  w = torch.rand((batch,), device=device) + 0.5 if algo == 'per' else None
+  for _ in range(12):
+    slots = torch.from_numpy(
+        rng.integers(0, st.capacity, size=batch).astype(np.int32)).to(device)
+    ref.step(st, slots, w)
+    lrn.step(st, slots, w)
+  # graph replay of the fused path
+  slots = torch.from_numpy(
+      rng.integers(0, st.capacity, size=batch).astype(np.int32)).to(device)
+  side = torch.cuda.Stream(device)
+  side.wait_stream(torch.cuda.current_stream(device))
+  with torch.cuda.stream(side):
+    lrn.step(st, slots, w)
+  torch.cuda.current_stream(device).wait_stream(side)
+  ref.step(st, slots, w)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    for _ in range(4):
+      lrn.step(st, slots, w)
+  for _ in range(3):
+    g.replay()
+  for _ in range(12):
+    ref.step(st, slots, w)
+  torch.cuda.synchronize()
+  assert lrn.sync_status() == 0
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(lrn, which), getattr(ref, which)), which
+  q1, td1, _ = lrn.fetch_outputs()
+  q2, td2, _ = ref.fetch_outputs()
+  assert torch.equal(q1, q2) and torch.equal(td1, td2)
+  # profile mode repeats every launch back to back; the hand-off words must
+  # reset themselves between launches.
+  lrn.profile(st, slots, weights=w, iters=5)
+  torch.cuda.synchronize()
+  assert lrn.sync_status() == 0
