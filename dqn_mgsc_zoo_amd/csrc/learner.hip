@@ -55,7 +55,7 @@ struct dqz_learner {
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   int fused_bwd;  // 1: bwd_bc_kernel + bwd_d_kernel; 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
-  int fused_fwd;  // 1: fwd_conv_kernel; 0: conv1 / conv2 / conv3 fwd launches (DQZ_FUSED_FWD=0)
+  int fused_fwd;  // 1: fwd_conv_kernel (DQZ_FUSED_FWD=1, measured 1.5 % slower); 0: conv1 / conv2 / conv3 launches
   void* block;
 };
 
@@ -100,7 +100,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
     const char* e = getenv("DQZ_FUSED_BWD");
     L->fused_bwd = !(e && e[0] == '0');
     e = getenv("DQZ_FUSED_FWD");
-    L->fused_fwd = !(e && e[0] == '0');
+    L->fused_fwd = e && e[0] == '1';
   }
   const int B = cfg->batch, Z = L->Z, A = cfg->num_actions;
   L->S_fc1 = FC1_S;
