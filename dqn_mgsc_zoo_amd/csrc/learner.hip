@@ -626,13 +626,26 @@ int dqz_sumtree_set(double* tree, int64_t cap, const int64_t* idx, const double*
   return DQZ_OK;
 }
 
+int dqz_per_write_back(dqz_learner* L, double* tree, int64_t cap, const int32_t* slots, double alpha,
+                       double* max_seen_dev, void* stream) {
+  if (!L || !tree || !slots || !max_seen_dev) return fail(DQZ_ERR_INVALID, "null argument");
+  if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
+  const int n = L->cfg.batch;
+  const int levels = tree_levels(cap);
+  if (n > ST_FAST || levels > 32) return fail(DQZ_ERR_INVALID, "batch must be <= %d and cap <= 2^32", ST_FAST);
+  hipLaunchKernelGGL(per_write_back_kernel, dim3(1), dim3(ST_FAST), 0, (hipStream_t)stream, tree, cap, levels, slots,
+                     L->td, alpha, n, max_seen_dev);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
 int dqz_sumtree_query(const double* tree, int64_t cap, const double* targets, int n, int64_t* out, void* stream) {
   if (!tree || !targets || !out) return fail(DQZ_ERR_INVALID, "null argument");
   if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
   if (n < 0) return fail(DQZ_ERR_INVALID, "n must be >= 0");
   if (n == 0) return DQZ_OK;
-  hipLaunchKernelGGL(sumtree_query_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, tree, cap, targets,
-                     n, out);
+  hipLaunchKernelGGL(sumtree_query_kernel, dim3((n + 7) / 8), dim3(256), 0, (hipStream_t)stream, tree, cap,
+                     tree_levels(cap), targets, n, out);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -646,7 +659,8 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
   if (n < 1 || n > 1024) return fail(DQZ_ERR_INVALID, "n must be in [1, 1024]");
   if (!(beta >= 0.0 && beta <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= exponent <= 1.");
   if (!(usp >= 0.0 && usp <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= uniform_sample_probability <= 1.");
-  hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, live_base, size,
+  hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, tree_levels(cap),
+                     live_base, size,
                      capacity, n, usp, beta, normalize, seed, counter_dev, out_slots, out_weights, out_probs);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;

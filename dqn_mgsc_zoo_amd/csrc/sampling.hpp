@@ -290,16 +290,16 @@ __global__ __launch_bounds__(1024) void sumtree_set_kernel(double* tree, int64_t
 // Caller passes distinct leaves.
 constexpr int ST_FAST = 256;
 
-__global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree, int64_t cap, int levels,
-                                                                    const int64_t* idx, const double* vals, int n) {
+// Thread i < n owns leaf `leaf` (tree index, or -1: this thread sets nothing)
+// with new value v; live leaves are distinct.
+__device__ __forceinline__ void sumtree_set_small_body(double* tree, int levels, int n, int64_t leaf, double v) {
   __shared__ int64_t s_leaf[ST_FAST];
   __shared__ double s_val[ST_FAST];
   __shared__ double s_sib[32][ST_FAST];  // old sibling per level; later the new ancestor values
   __shared__ short s_rep[32][ST_FAST];   // updated leaf whose ancestor is my sibling at level l, or -1
   const int i = threadIdx.x;
-  const bool live = i < n;
-  const int64_t leaf = live ? cap + idx[i] : -1;
-  double v = live ? vals[i] : 0.0;
+  const bool live = i < n && leaf >= 0;
+  if (!live) leaf = -1;
   const double leaf_v = v;
   for (int l0 = 0; l0 < levels; l0 += 8) {  // one batch of loads per 8 levels
     double t8[8];
@@ -315,8 +315,9 @@ __global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree
   __syncthreads();
   if (live)
     for (int j = 0; j < n; ++j) {
-      const uint64_t d = (uint64_t)(leaf ^ s_leaf[j]);
-      if (d != 0) s_rep[63 - __builtin_clzll(d)][i] = (short)j;
+      const int64_t o = s_leaf[j];
+      const uint64_t d = (uint64_t)(leaf ^ o);
+      if (o >= 0 && d != 0) s_rep[63 - __builtin_clzll(d)][i] = (short)j;
     }
   __syncthreads();
   for (int l = 0; l < levels; ++l) {
@@ -336,81 +337,163 @@ __global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree
   }
 }
 
-// Descent of SumTree._query_single for each target; -1 when out of range.
-__global__ void sumtree_query_kernel(const double* __restrict__ tree, int64_t cap, const double* __restrict__ targets,
-                                     int n, int64_t* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double t = targets[i];
-  if (!(t >= 0.0 && t < tree[1])) {
-    out[i] = -1;
-    return;
+__global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree, int64_t cap, int levels,
+                                                                    const int64_t* idx, const double* vals, int n) {
+  const int i = threadIdx.x;
+  sumtree_set_small_body(tree, levels, n, i < n ? cap + idx[i] : -1, i < n ? vals[i] : 0.0);
+}
+
+// PrioritizedDqn priority write-back (prioritized/agent.py:201-206 +
+// PrioritizedDistribution.update_priorities, replay.py:620-630 + _power,
+// :336-341) for the learner's last batch, on device: p = |td|,
+// *max_seen = max(*max_seen, max p), leaf = p^alpha (0 -> 0), sum-tree
+// set.  A slot drawn twice keeps its last draw's value (numpy fancy
+// assignment order in SumTree.set).  n <= ST_FAST.
+__global__ __launch_bounds__(ST_FAST) void per_write_back_kernel(double* tree, int64_t cap, int levels,
+                                                                 const int32_t* slots, const float* td, double alpha,
+                                                                 int n, double* max_seen) {
+  __shared__ double s_max[ST_FAST / 64];
+  const int i = threadIdx.x;
+  int64_t leaf = -1;
+  double p = 0.0;
+  if (i < n) {
+    const int32_t s = slots[i];
+    p = fabs((double)td[i]);
+    bool last = true;
+    for (int j = i + 1; j < n; ++j) last &= slots[j] != s;
+    if (last) leaf = cap + s;
   }
+  double m = p;
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if ((i & 63) == 0) s_max[i >> 6] = m;
+  const double v = p == 0.0 ? 0.0 : pow(p, alpha);
+  sumtree_set_small_body(tree, levels, n, leaf, v);  // its barriers publish s_max
+  if (i == 0) {
+    double mm = *max_seen;
+    for (int w = 0; w < ST_FAST / 64; ++w) mm = fmax(mm, s_max[w]);
+    *max_seen = mm;
+  }
+}
+
+// Descent of SumTree._query_single (replay.py:539-559) by one half-wave (32
+// lanes), four tree levels per global round trip.  In the implicit layout
+// the descendants of `node` at relative depth k are the contiguous indices
+// node * 2^k .. node * 2^k + 2^k - 1, so a round loads the 2 + 4 + 8 + 16 = 30
+// nodes below the current one (lane l: depth k = floor(log2(l + 2)),
+// j = l + 2 - 2^k) and takes the four left/right decisions from registers with
+// the reference's own fp64 arithmetic (compare with the left sum, subtract it
+// on the way right): the same node sequence as the serial descent, bit for
+// bit, in ceil(levels / 4) dependent loads instead of `levels`.  The first
+// round also fetches the root (nodes 1 .. 31, lane l holds node l + 1), so
+// callers that scale their target by the root pay no extra round trip:
+// `scale` >= 0 -> t = scale * root (PER), scale < 0 -> t as given, and the
+// slot is -1 when t is not in [0, root).  Returns the slot and its leaf.
+struct Descent {
+  int64_t slot;
+  double leaf, root;
+};
+
+__device__ __forceinline__ Descent halfwave_descend(const double* tree, int64_t cap, int levels, double t,
+                                                    double scale, int l) {
+  // round 0: nodes 1..31 (depths 0..4), clamped to the tree
+  const int64_t top = min((int64_t)31, 2 * cap - 1);
+  const double v0 = l < top ? tree[1 + l] : 0.0;
+  const double root = __shfl(v0, 0, 32);
+  Descent d{-1, 0.0, root};
+  if (scale >= 0.0)
+    t = scale * root;  // u in [0, 1): u * root < root in fp64 (no range check, as the serial descent)
+  else if (!(t >= 0.0 && t < root))
+    return d;
   int64_t node = 1;
-  while (node < cap) {
-    const double left = tree[2 * node];
-    if (t < left) {
-      node = 2 * node;
-    } else {
-      t -= left;
-      node = 2 * node + 1;
+  int depth = 0;
+  double v = v0;
+  int base = -1;  // lane of relative depth k, j = 0 is base + 2^k (round 0: lane = node - 1)
+  while (true) {
+    const int K = min(4, levels - depth);
+    int64_t pos = 0;
+    for (int k = 1; k <= K; ++k) {
+      const double left = __shfl(v, base + (1 << k) + 2 * (int)pos, 32);
+      if (t < left) {
+        pos = 2 * pos;
+      } else {
+        t -= left;
+        pos = 2 * pos + 1;
+      }
     }
+    node = (node << K) + pos;
+    depth += K;
+    if (depth >= levels) {
+      d.slot = node - cap;
+      d.leaf = K > 0 ? __shfl(v, base + (1 << K) + (int)pos, 32) : root;
+      return d;
+    }
+    // next round: the 30 nodes below `node`
+    const int k = 31 - __builtin_clz(l + 2), j = l + 2 - (1 << k);
+    const int kmax = min(4, levels - depth);
+    v = (l < (2 << kmax) - 2) ? tree[(node << k) + j] : 0.0;
+    base = -2;
   }
-  out[i] = node - cap;
+}
+
+// One half-wave per target; -1 when out of range.
+__global__ __launch_bounds__(256) void sumtree_query_kernel(const double* __restrict__ tree, int64_t cap,
+                                                            int levels, const double* __restrict__ targets, int n,
+                                                            int64_t* __restrict__ out) {
+  const int i = blockIdx.x * 8 + (threadIdx.x >> 5), l = threadIdx.x & 31;
+  if (i >= n) return;  // half-wave uniform
+  const Descent d = halfwave_descend(tree, cap, levels, targets[i], -1.0, l);
+  if (l == 0) out[i] = d.slot;
 }
 
 // PrioritizedDistribution.sample + importance_sampling_weights with device
 // Philox streams (replay.py:680-716, 344-376).  Tree index == replay slot.
-// One block; n <= 1024.
-__global__ __launch_bounds__(1024) void per_sample_kernel(const double* __restrict__ tree, int64_t cap,
+// One block of 32 half-waves; half-wave h handles draws h, h + 32, ...;
+// n <= 1024.
+__global__ __launch_bounds__(1024) void per_sample_kernel(const double* __restrict__ tree, int64_t cap, int levels,
                                                           int64_t live_base, int64_t size, int64_t capacity, int n,
                                                           double usp, double beta, int normalize, uint64_t seed,
                                                           uint64_t* counter, int32_t* out_slots,
                                                           float* out_weights, double* out_probs) {
   __shared__ double s_w[1024];
   const uint64_t ctr = *counter;
-  const int i = threadIdx.x;
-  double w = 0.0;
-  if (i < n) {
+  const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
+  for (int i = h; i < n; i += 32) {
     const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
     const double u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
     const double u_mix = (double)(r.z >> 8) * 0x1.0p-24;
     const int64_t uni = (live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)size)) % capacity;
-    const double root = tree[1];
+    const bool use_uniform = u_mix < usp;
+    // t = u_target * root inside the descent (the root arrives with the first round)
+    Descent d = halfwave_descend(tree, cap, levels, 0.0, use_uniform ? 0.0 : u_target, l);
+    const double root = d.root;
     int64_t slot = uni;
-    if (root > 0.0 && !(u_mix < usp)) {
-      double t = u_target * root;
-      int64_t node = 1;
-      while (node < cap) {
-        const double left = tree[2 * node];
-        if (t < left) {
-          node = 2 * node;
-        } else {
-          t -= left;
-          node = 2 * node + 1;
-        }
-      }
-      slot = node - cap;
+    double leaf;
+    if (root > 0.0 && !use_uniform) {
+      slot = d.slot;
+      leaf = d.leaf;
+    } else {
+      leaf = tree[cap + slot];
     }
-    const double leaf = tree[cap + slot];
     const double up = 1.0 / (double)size;
     const double pp = root > 0.0 ? leaf / root : up;
     const double prob = (1.0 - usp) * pp + usp * up;
-    w = pow(up / prob, beta);
-    out_slots[i] = (int32_t)slot;
-    if (out_probs) out_probs[i] = prob;
+    const double w = pow(up / prob, beta);
+    if (l == 0) {
+      out_slots[i] = (int32_t)slot;
+      if (out_probs) out_probs[i] = prob;
+      s_w[i] = w;
+    }
   }
-  s_w[i] = w;
   __syncthreads();
-  if (i < n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
     double m = 0.0;
     if (normalize)
       for (int j = 0; j < n; ++j) m = fmax(m, s_w[j]);
-    out_weights[i] = (float)(normalize ? w / m : w);
+    out_weights[i] = (float)(normalize ? s_w[i] / m : s_w[i]);
   }
   __syncthreads();
-  if (i == 0) *counter = ctr + 1;
+  if (threadIdx.x == 0) *counter = ctr + 1;
 }
 
 }  // namespace dqz

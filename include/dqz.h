@@ -214,6 +214,14 @@ int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* 
 /* n uniform doubles in [0,1) from Philox4x32-10 (counter advanced on device). */
 int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream);
 
+/* Priority write-back of the learner's last step (prioritized/agent.py:201-206,
+ * replay.py:620-630): p = |td| (fp64 of the f32 TD errors), *max_seen_dev =
+ * max(*max_seen_dev, max p), leaf[slots[i]] = p^alpha (0 -> 0) with the sum
+ * tree's ancestors rebuilt (a slot drawn twice keeps its last draw).  All
+ * device pointers; one launch, no host synchronisation.  Batch <= 256. */
+int dqz_per_write_back(dqz_learner* learner, double* tree, int64_t cap, const int32_t* slots, double alpha,
+                       double* max_seen_dev, void* stream);
+
 /* ---- prioritized replay: fp64 sum tree in HBM (replay.py:379-559) -------
  * tree: device f64 [2*cap], cap a power of two, node i has children 2i, 2i+1,
  * root at 1, leaves at [cap, 2cap) -- the layout of the host SumTree.

@@ -271,3 +271,31 @@ def test_fused_handoff_kernels_bit_exact(device, algo, batch, monkeypatch):
   lrn.profile(st, slots, weights=w, iters=5)
   torch.cuda.synchronize()
   assert lrn.sync_status() == 0
+
+
+def test_per_write_back_device(device):
+  """dqz_per_write_back == |td| -> max_seen, _power(|td|, alpha) -> SumTree.set
+  (host mirror of replay.py:411-423), duplicates keeping the last draw."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  batch, alpha = 32, 0.6
+  _, lrn, st, _, _, _, _, _ = _setup('per', batch, seed=31)
+  rng = np.random.default_rng(32)
+  host = replay_lib.SumTree()
+  host.set_all(rng.random(st.capacity))
+  tree = torch.from_numpy(host.storage.copy()).to(device)
+  slots_np = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+  slots_np[5] = slots_np[20]  # a duplicate draw
+  slots = torch.from_numpy(slots_np).to(device)
+  w = torch.rand((batch,), device=device) + 0.5
+  lrn.step(st, slots, w)
+  max_seen = torch.tensor([0.25], dtype=torch.float64, device=device)
+  _native.check(_native.lib().dqz_per_write_back(
+      lrn._h, _native.ptr(tree), host.capacity, _native.ptr(slots), alpha,  # pylint: disable=protected-access
+      _native.ptr(max_seen), _native.stream_handle()))
+  _, td, _ = lrn.fetch_outputs()
+  torch.cuda.synchronize()
+  p = np.abs(td.cpu().numpy().astype(np.float64))
+  host.set(slots_np, replay_lib._power(p, alpha))  # pylint: disable=protected-access
+  np.testing.assert_allclose(tree.cpu().numpy()[1:], host.storage[1:], rtol=4e-16, atol=0)
+  assert max_seen.item() == max(0.25, p.max())

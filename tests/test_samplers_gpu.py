@@ -190,3 +190,37 @@ def test_per_device_sampler_distribution(device):
   np.testing.assert_allclose(probs.cpu().numpy(), expected[s], rtol=1e-12)
   want_w = replay_lib.importance_sampling_weights(expected[s], 1.0 / cap, beta, True)
   np.testing.assert_allclose(w.cpu().numpy(), want_w, rtol=1e-6)
+
+
+def test_sumtree_query_large_tree_boundaries(device):
+  """2^20-leaf tree (PER at capacity 1e6): the half-wave four-level descent
+  returns the serial descent's leaf for random targets and for targets that
+  sit exactly on left-subtree sums (where the compare flips)."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  lib = _native.lib()
+  rng = np.random.default_rng(11)
+  host = replay_lib.SumTree()
+  prios = rng.random(1_000_000) ** 3
+  prios[rng.integers(0, prios.size, 5000)] = 0.0
+  host.set_all(prios)
+  dev = _tree_dev(host)
+  st = host.storage
+  targets = list(rng.uniform(0, host.root(), 300))
+  # exact boundaries: cumulative sums along a few random root-to-leaf paths
+  for _ in range(20):
+    node, acc = 1, 0.0
+    while node < host.capacity:
+      targets.append(acc + st[2 * node])  # == left sum: must go right
+      if rng.random() < 0.5:
+        node = 2 * node
+      else:
+        acc += st[2 * node]
+        node = 2 * node + 1
+  targets = np.array([t for t in targets if 0.0 <= t < host.root()])
+  dt = torch.from_numpy(targets).to(device)
+  out = torch.empty(targets.size, dtype=torch.int64, device=device)
+  _native.check(lib.dqz_sumtree_query(_native.ptr(dev), host.capacity,
+                                      _native.ptr(dt), targets.size,
+                                      _native.ptr(out), _native.stream_handle()))
+  assert out.cpu().numpy().tolist() == list(host.query(targets))

@@ -98,21 +98,17 @@ def main():
   lrn_p = learner_lib.Learner(net_d, B, algo='per', device=dev)
   lrn_p.set_params(net_d.init(seed=2))
   p_slots = torch.zeros((B,), dtype=torch.int32, device=dev)
-  p_idx = torch.zeros((B,), dtype=torch.int64, device=dev)
   p_w = torch.zeros((B,), dtype=torch.float32, device=dev)
   p_ctr = torch.zeros((1,), dtype=torch.int64, device=dev)
-  newp = torch.zeros((B,), dtype=torch.float64, device=dev)
+  max_seen = torch.ones((1,), dtype=torch.float64, device=dev)
 
   def per_step():
     _native.check(lib.dqz_per_sample(
         _native.ptr(tree), tcap, 0, cap, cap, B, ctypes.c_double(1e-3), ctypes.c_double(0.4), 1, 11,
         _native.ptr(p_ctr), _native.ptr(p_slots), _native.ptr(p_w), None, _native.stream_handle()))
     lrn_p.step(store, p_slots, p_w)
-    _, td, _ = lrn_p.fetch_outputs()
-    torch.pow(td.abs().double(), 0.6, out=newp)
-    p_idx.copy_(p_slots)
-    _native.check(lib.dqz_sumtree_set(_native.ptr(tree), tcap, _native.ptr(p_idx), _native.ptr(newp), B,
-                                      _native.stream_handle()))
+    _native.check(lib.dqz_per_write_back(lrn_p._h, _native.ptr(tree), tcap, _native.ptr(p_slots),  # pylint: disable=protected-access
+                                         ctypes.c_double(0.6), _native.ptr(max_seen), _native.stream_handle()))
   out['per_double'] = timed(per_step, args.steps, 20, dev, graph_steps=50)
 
   # ---- MGSC learner part: softmax sample over the logits + DQN step -------
