@@ -53,6 +53,8 @@ def phase_flops(algo, batch):
       'fc1_dx': 2 * b * MAC['fc1'],
       'conv3_dx+fc1_dw': 2 * b * (MAC['conv3'] + MAC['fc1']),
       'conv2_dx+conv3_dw': 2 * b * (MAC['conv2'] + MAC['conv3']),
+      'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 2 * b * (2 * MAC['conv3'] + MAC['fc1'] +
+                                                   MAC['conv2']),
       'conv1_dw+conv2_dw': 2 * b * (MAC['conv1'] + MAC['conv2']),
       'update': 0,
   }
@@ -88,6 +90,11 @@ def phase_bytes(algo, batch):
                           b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
       'conv2_dx+conv3_dw': (b * (ACT['y2'] + 2 * ACT['y1']) + PARAM['conv2'] +
                             b * (ACT['y2'] + ACT['y3']) + PARAM['conv3']),
+      # one launch (bwd_bc_kernel): dy2 is handed off inside it, dy3 and y2
+      # are read once
+      'conv3_dx+conv2_dx+fc1_dw+conv3_dw': (
+          b * (ACT['y3'] + ACT['y2'] + 2 * ACT['y1']) + 2 * PARAM['conv3'] +
+          PARAM['conv2'] + b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
       'conv1_dw+conv2_dw': (b * (ACT['state'] + ACT['y1']) + PARAM['conv1'] +
                             b * (ACT['y1'] + ACT['y2']) + PARAM['conv2']),
       'update': rms,
@@ -100,6 +107,7 @@ PHASE_KERNEL = {
     'conv3_fwd': 'conv3_fwd_kernel', 'fc1_fwd': 'fc1_fwd_kernel',
     'head': 'head_kernel', 'fc1_dx': 'fc1_dx_kernel',
     'conv3_dx+fc1_dw': 'bwd_b_kernel', 'conv2_dx+conv3_dw': 'bwd_c_kernel',
+    'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 'bwd_bc_kernel',
     'conv1_dw+conv2_dw': 'bwd_d_kernel', 'update': 'update_kernel'}
 PMC_JSON = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
 

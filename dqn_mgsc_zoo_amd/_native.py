@@ -20,7 +20,11 @@ NUM_LEAVES = 10
 NUM_PHASES = 10
 PHASE_NAMES = (
     'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_dx',
-    'conv3_dx+fc1_dw', 'conv2_dx+conv3_dw', 'conv1_dw+conv2_dw', 'update')
+    'conv3_dx+conv2_dx+fc1_dw+conv3_dw', 'conv2_dx+conv3_dw',
+    'conv1_dw+conv2_dw', 'update')
+# Phase 6 of the split-backward debug layout (DQZ_FUSED_BWD=0), where phase 7
+# is a launch of its own.
+PHASE6_SPLIT = 'conv3_dx+fc1_dw'
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4

@@ -150,7 +150,12 @@ class Learner:
         self._h, ctypes.byref(self._params_c), store.c_ref(),
         _native.ptr(slots), _native.ptr(weights), int(iters), out,
         _native.stream_handle(stream)))
-    return dict(zip(_native.PHASE_NAMES, [float(x) for x in out]))
+    ms = [float(x) for x in out]
+    names = list(_native.PHASE_NAMES)
+    if ms[7] > 0.0:  # split-backward layout: phase 6 is conv3 dX + fc1 dW only
+      names[6] = _native.PHASE6_SPLIT
+    # phases merged into another launch report 0 and are left out
+    return {n: t for n, t in zip(names, ms) if t > 0.0}
 
   def fetch_outputs(self, stream=None):
     """Copies (q_tm1, td, loss) of the last step into self tensors."""
