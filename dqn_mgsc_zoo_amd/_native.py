@@ -84,6 +84,22 @@ class DqzMetaConfig(ctypes.Structure):
   ]
 
 
+class DqzAction(ctypes.Structure):
+  _fields_ = [('action', ctypes.c_int32), ('value', ctypes.c_float)]
+
+
+class DqzTransitionPut(ctypes.Structure):
+  _fields_ = [
+      ('slot', ctypes.c_int64),
+      ('fidx', ctypes.c_int32 * 8),
+      ('action', ctypes.c_int32),
+      ('reward', ctypes.c_float),
+      ('discount', ctypes.c_float),
+      ('num_frames', ctypes.c_int32),
+      ('frame_rows', ctypes.c_int32 * 8),
+  ]
+
+
 # name -> (restype, argtypes); must match include/dqz.h exactly.
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -124,6 +140,12 @@ SIGNATURES = {
     'dqz_forward': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
     'dqz_forward_slots': (
         _int, [_vp, _vp, ctypes.POINTER(DqzStore), _vp, _int, _int, _vp, _vp]),
+    'dqz_act': (
+        _int, [_vp, _vp, _vp, _int, ctypes.c_double, ctypes.c_uint64,
+               ctypes.c_uint64, _vp, _vp]),
+    'dqz_store_put': (
+        _int, [ctypes.POINTER(DqzStore), ctypes.POINTER(DqzTransitionPut), _vp,
+               _vp]),
     'dqz_sample_uniform': (
         _int, [_i64, _i64, _i64, _int, ctypes.c_uint64, _vp, _vp, _vp]),
     'dqz_gather_stacks': (

@@ -54,7 +54,8 @@ class DeviceDqnAgent(parts.Agent):
     self._learn_period = learn_period
     self._target_network_update_period = target_network_update_period
     seed = seed_from_key(rng_key)
-    self._rng = np.random.default_rng(seed)
+    self._act_seed = seed
+    self._act_count = 0
     self._network = network
     self._learner = learner_lib.Learner(network, batch_size, algo=self._ALGO,
                                         optimizer=optimizer,
@@ -95,10 +96,14 @@ class DeviceDqnAgent(parts.Agent):
     self._replay.add(transition)
 
   def _act(self, timestep) -> parts.Action:
-    q = self._learner.q_values_host(timestep.observation)
-    probs = parts.epsilon_greedy_probs(q, self.exploration_epsilon)
-    a = int(self._rng.choice(len(q), p=probs))
-    self._statistics['state_value'] = float(np.max(q))
+    """select_action + device_get (dqn/agent.py:169-177) as one device call:
+    eps-greedy draw number `_act_count` of the Philox stream `_act_seed`
+    (JAX's threefry keys are not reproducible here; the distribution is
+    distrax.EpsilonGreedy's)."""
+    a, v = self._learner.act(timestep.observation, self.exploration_epsilon,
+                             self._act_seed, self._act_count)
+    self._act_count += 1
+    self._statistics['state_value'] = v
     return parts.Action(a)
 
   def _learn(self) -> None:
@@ -124,7 +129,7 @@ class DeviceDqnAgent(parts.Agent):
   def get_state(self) -> Mapping[str, Any]:
     lrn = self._learner
     return {
-        'rng_key': self._rng.bit_generator.state,
+        'rng_key': {'seed': self._act_seed, 'count': self._act_count},
         'frame_t': self._frame_t,
         'opt_state': (lrn.params_tree('mu'), lrn.params_tree('nu')),
         'online_params': lrn.params_tree('online'),
@@ -133,7 +138,8 @@ class DeviceDqnAgent(parts.Agent):
     }
 
   def set_state(self, state: Mapping[str, Any]) -> None:
-    self._rng.bit_generator.state = state['rng_key']
+    self._act_seed = state['rng_key']['seed']
+    self._act_count = state['rng_key']['count']
     self._frame_t = state['frame_t']
     self._learner.set_params(state['online_params'], state['target_params'])
     self._learner.set_opt_state(*state['opt_state'])

@@ -28,7 +28,35 @@ struct HeadArgs {
   float* gq;             // [B] d loss / d q_tm1[b, a_b]
   int32_t* ga;           // [B] a_b
   float* dz1;            // [B][512] d loss / d fc1 pre-activation (online)
+  // actor mode (fwd_only): eps-greedy draw per sample into act_out (or null)
+  dqz_action* act_out;
+  double eps;
+  uint64_t act_seed, act_ctr;
 };
+
+// distrax.EpsilonGreedy(q, eps).sample as the host mirror computes it
+// (parts.epsilon_greedy_probs + numpy Generator.choice): fp64 probabilities
+// (1 - eps) [q_a == max] / #ties + eps / A, cdf = cumsum normalised by its
+// last entry, action = first a with cdf[a] > u.
+__device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double eps, double u) {
+  float v = q[0];
+  for (int a = 1; a < A; ++a) v = fmaxf(v, q[a]);
+  int ties = 0;
+  for (int a = 0; a < A; ++a) ties += q[a] == v;
+  const double greedy = 1.0 / (double)ties, floor = eps / (double)A;
+  double total = 0.0;
+  for (int a = 0; a < A; ++a) total += (1.0 - eps) * (q[a] == v ? greedy : 0.0) + floor;
+  double cum = 0.0;
+  int act = A - 1;
+  for (int a = 0; a < A; ++a) {
+    cum += (1.0 - eps) * (q[a] == v ? greedy : 0.0) + floor;
+    if (cum / total > u) {
+      act = a;
+      break;
+    }
+  }
+  return dqz_action{act, v};
+}
 
 // One workgroup (512 threads = hidden units) per sample b:
 //   h1 = relu(b1 + sum_s partial), q = h1 @ W2 + b2 for every copy z,
@@ -155,6 +183,14 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
     for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
     DQZ_STAMP(4, 2);
     h.dz1[(int64_t)b * HID + n] = hz[0] > 0.f ? s_g * wv : 0.f;
+  } else if (h.act_out) {  // actor: eps-greedy draw b of call act_ctr
+    __syncthreads();
+    if (n == 0) {
+      const uint4 r = philox4x32(make_uint4((unsigned)h.act_ctr, (unsigned)(h.act_ctr >> 32), (unsigned)b, 0xAC7u),
+                                 make_uint2((unsigned)h.act_seed, (unsigned)(h.act_seed >> 32)));
+      const double u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+      h.act_out[b] = eps_greedy(s_q[0], A, h.eps, u);
+    }
   }
   // deferred outputs: fc1 activations (fc2 dW in the update kernel), q values
 #pragma unroll
@@ -360,6 +396,32 @@ __global__ void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx,
     c[ci] = f < 0 ? 0u : frames[(int64_t)f * FB + p];
   }
   reinterpret_cast<uchar4*>(out)[i] = make_uchar4(c[0], c[1], c[2], c[3]);
+}
+
+// One replay add (dqz_store_put): block i < t.num_frames copies new frame i
+// (441 x 16 B) into its pool row; block 0 also writes the transition record.
+// `frames` may be pinned host memory (read over the fabric).
+__global__ __launch_bounds__(256) void store_put_kernel(uint8_t* pool, int32_t* fidx, int32_t* action, float* reward,
+                                                        float* discount, dqz_transition_put t,
+                                                        const uint8_t* frames) {
+  constexpr int Q = FB / 16;  // 441
+  const int f = blockIdx.x;
+  if (f < t.num_frames) {
+    const uint4* src = reinterpret_cast<const uint4*>(frames + (int64_t)f * FB);
+    uint4* dst = reinterpret_cast<uint4*>(pool + (int64_t)t.frame_rows[f] * FB);
+    uint4 v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) v[k] = src[min((int)threadIdx.x + 256 * k, Q - 1)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if ((int)threadIdx.x + 256 * k < Q) dst[threadIdx.x + 256 * k] = v[k];
+  }
+  if (f == 0) {
+    if (threadIdx.x < 8) fidx[t.slot * 8 + threadIdx.x] = t.fidx[threadIdx.x];
+    if (threadIdx.x == 8) action[t.slot] = t.action;
+    if (threadIdx.x == 9) reward[t.slot] = t.reward;
+    if (threadIdx.x == 10) discount[t.slot] = t.discount;
+  }
 }
 
 }  // namespace dqz

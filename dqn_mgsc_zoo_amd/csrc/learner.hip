@@ -182,8 +182,11 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
   } while (0)
 
 // conv1..fc1 forward of Z network copies (phases 0-3).
+// fused_conv: conv1 -> conv2 -> conv3 as one hand-off launch (fwd_conv_kernel);
+// the learner step uses it only under DQZ_FUSED_FWD=1, the actor (n <= a few
+// samples, launch-latency bound) always.
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
-                        PhaseEvents pe) {
+                        PhaseEvents pe, bool fused_conv) {
   Conv1FwdArgs c1;
   c1.src = src;
   c1.nz = nz;
@@ -209,7 +212,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  if (L->fused_fwd) {
+  if (fused_conv) {
     // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample (Z*B <= 3B samples)
     int* hw = L->sync + 2 * B * Handoff::kStride;
     int* err = L->sync + 14 * B * Handoff::kStride;
@@ -291,9 +294,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     Conv1Src fsrc = src;
     fsrc.fused = 1;
     fsrc.draw = *draw;
-    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, L->fused_fwd)) return rc;
   } else {
-    if (int rc = forward_impl(L, nz, Z, B, src, st, pe)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, src, st, pe, L->fused_fwd)) return rc;
   }
 
   Rms rms;
@@ -465,7 +468,7 @@ static int forward_q(dqz_learner* L, const float* params, const Conv1Src& src, i
   NetZ nz;
   nz.p[0] = nz.p[1] = nz.p[2] = params;
   nz.which[0] = nz.which[1] = nz.which[2] = which;
-  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile)) return rc;
+  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile, true)) return rc;
   HeadArgs h = make_head(L, nz, 1, n);
   h.fwd_only = 1;
   h.q = q_out;
@@ -490,6 +493,82 @@ int dqz_forward_slots(dqz_learner* L, const float* params, const dqz_store* S, c
   if (which != 0 && which != 1) return fail(DQZ_ERR_INVALID, "which must be 0 (s_tm1) or 1 (s_t)");
   Conv1Src src{S->frames, S->fidx, slots, nullptr, 0, UniformDraw{}};
   return forward_q(L, params, src, which, n, q_out, (hipStream_t)stream);
+}
+
+// Device address of p: device memory as is, pinned host memory through its
+// mapped device pointer.  Pageable host memory is refused (a kernel access
+// would fault).
+static int device_view(const void* p, const void** out, const char* what) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(DQZ_ERR_INVALID, "%s must be device memory or pinned host memory", what);
+  }
+  if (attr.type == hipMemoryTypeHost) {
+    void* d = attr.devicePointer;
+    if (!d && hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(DQZ_ERR_INVALID, "%s: pinned host memory without a device mapping", what);
+    }
+    *out = d;
+  } else if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged ||
+             attr.type == hipMemoryTypeUnified) {
+    *out = p;
+  } else {
+    return fail(DQZ_ERR_INVALID, "%s must be device memory or pinned host memory", what);
+  }
+  return DQZ_OK;
+}
+
+int dqz_act(dqz_learner* L, const float* params, const uint8_t* states, int n, double epsilon, uint64_t seed,
+            uint64_t counter, dqz_action* out, void* stream) {
+  if (!L || !params || !states || !out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 1 || n > L->cfg.batch) return fail(DQZ_ERR_INVALID, "n must be in [1, %d]", L->cfg.batch);
+  if (!(epsilon >= 0.0 && epsilon <= 1.0)) return fail(DQZ_ERR_INVALID, "epsilon must be in [0, 1]");
+  const void *dstates = nullptr, *dout = nullptr;
+  if (int rc = device_view(states, &dstates, "states")) return rc;
+  if (int rc = device_view(out, &dout, "out")) return rc;
+  if (reinterpret_cast<uintptr_t>(dstates) % 16) return fail(DQZ_ERR_INVALID, "states must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  NetZ nz;
+  nz.p[0] = nz.p[1] = nz.p[2] = params;
+  nz.which[0] = nz.which[1] = nz.which[2] = 0;
+  Conv1Src src{nullptr, nullptr, nullptr, static_cast<const uint8_t*>(dstates), 0, UniformDraw{}};
+  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile, true)) return rc;
+  HeadArgs h = make_head(L, nz, 1, n);
+  h.fwd_only = 1;
+  h.q = L->q;
+  h.act_out = static_cast<dqz_action*>(const_cast<void*>(dout));
+  h.eps = epsilon;
+  h.act_seed = seed;
+  h.act_ctr = counter;
+  DQZ_HIP(launch_head(h, n, st));
+  return DQZ_OK;
+}
+
+int dqz_store_put(const dqz_store* S, const dqz_transition_put* t, const uint8_t* frames, void* stream) {
+  if (int rc = check_store(S)) return rc;
+  if (!t) return fail(DQZ_ERR_INVALID, "null transition");
+  if (t->slot < 0 || t->slot >= S->capacity)
+    return fail(DQZ_ERR_INVALID, "slot %lld out of range [0, %lld)", (long long)t->slot, (long long)S->capacity);
+  if (t->num_frames < 0 || t->num_frames > 8) return fail(DQZ_ERR_INVALID, "num_frames must be in [0, 8]");
+  for (int i = 0; i < 8; ++i)
+    if (t->fidx[i] < -1 || t->fidx[i] >= S->num_frames) return fail(DQZ_ERR_INVALID, "fidx[%d] out of range", i);
+  for (int i = 0; i < t->num_frames; ++i)
+    if (t->frame_rows[i] < 0 || t->frame_rows[i] >= S->num_frames)
+      return fail(DQZ_ERR_INVALID, "frame_rows[%d] out of range", i);
+  const void* dframes = nullptr;
+  if (t->num_frames > 0) {
+    if (!frames) return fail(DQZ_ERR_INVALID, "null frames");
+    if (int rc = device_view(frames, &dframes, "frames")) return rc;
+    if (reinterpret_cast<uintptr_t>(dframes) % 16) return fail(DQZ_ERR_INVALID, "frames must be 16-byte aligned");
+  }
+  hipLaunchKernelGGL(store_put_kernel, dim3(t->num_frames > 0 ? t->num_frames : 1), dim3(256), 0,
+                     (hipStream_t)stream, const_cast<uint8_t*>(S->frames), const_cast<int32_t*>(S->fidx),
+                     const_cast<int32_t*>(S->action), const_cast<float*>(S->reward),
+                     const_cast<float*>(S->discount), *t, static_cast<const uint8_t*>(dframes));
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
 }
 
 int dqz_sample_uniform(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed, uint64_t* counter_dev,

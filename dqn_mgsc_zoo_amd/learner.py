@@ -205,6 +205,27 @@ class Learner:
     out = q.cpu().numpy()
     return out[0] if observation.ndim == 3 else out
 
+  def act(self, observation, epsilon, seed, counter, params=None):
+    """select_action on device (dqn/agent.py:121-131): (action, max_a q) for
+    one host uint8 [84,84,4] observation, the eps-greedy draw being number
+    `counter` of the Philox stream `seed` (dqz_act).  The observation is
+    read and the result written in place in pinned host buffers: one launch
+    chain and one stream synchronisation per call, no staging copies."""
+    if getattr(self, '_act_in', None) is None:
+      self._act_in = torch.empty((1, 84, 84, 4), dtype=torch.uint8,
+                                 pin_memory=True)
+      self._act_in_np = self._act_in.numpy()
+      self._act_out = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
+      self._act_out_np = self._act_out.numpy()
+    self._act_in_np[0] = observation
+    _native.check(_native.lib().dqz_act(
+        self._h, _native.ptr(self._params_tensor(params)),
+        ctypes.c_void_p(self._act_in.data_ptr()), 1, float(epsilon),
+        int(seed) & (2**64 - 1), int(counter) & (2**64 - 1),
+        ctypes.c_void_p(self._act_out.data_ptr()), _native.stream_handle()))
+    torch.cuda.current_stream(self.device).synchronize()
+    return int(self._act_out_np[0]), float(self._act_out_np.view(np.float32)[1])
+
   def q_values_slots(self, store, slots, which, params=None, stream=None):
     params = self.online if params is None else params
     n = int(slots.numel())

@@ -246,8 +246,11 @@ class EpsilonGreedyActor(Agent):
                rng_key, learner=None):
     from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
     self._preprocessor = preprocessor
-    self._rng = np.random.default_rng(np.asarray(rng_key).astype(np.uint64).tolist()
-                                      if np.ndim(rng_key) else int(rng_key))
+    key = np.asarray(rng_key).astype(np.uint64).reshape(-1).tolist()
+    self._act_seed = 0
+    for x in key:
+      self._act_seed = (self._act_seed * 1000003 + int(x)) & (2**63 - 1)
+    self._act_count = 0
     self._rng_key = rng_key
     self._action = None
     self._epsilon = exploration_epsilon
@@ -261,8 +264,11 @@ class EpsilonGreedyActor(Agent):
       if self._action is None:
         raise RuntimeError('Cannot repeat if action has never been selected.')
       return self._action
-    q = self._learner.q_values_host(timestep.observation, self.network_params)
-    self._action = Action(self._rng.choice(len(q), p=epsilon_greedy_probs(q, self._epsilon)))
+    a, _ = self._learner.act(timestep.observation, self._epsilon,
+                             self._act_seed, self._act_count,
+                             params=self.network_params)
+    self._act_count += 1
+    self._action = Action(a)
     return self._action
 
   def reset(self) -> None:
@@ -271,13 +277,12 @@ class EpsilonGreedyActor(Agent):
 
   def get_state(self) -> Mapping[str, Any]:
     return {'rng_key': self._rng_key, 'network_params': self.network_params,
-            'rng_state': self._rng.bit_generator.state}
+            'act_count': self._act_count}
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._rng_key = state['rng_key']
     self.network_params = state['network_params']
-    if 'rng_state' in state:
-      self._rng.bit_generator.state = state['rng_state']
+    self._act_count = state.get('act_count', 0)
 
   @property
   def statistics(self) -> Mapping[str, float]:

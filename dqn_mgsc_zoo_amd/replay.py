@@ -186,9 +186,10 @@ class _DeviceStorage:
   def put(self, slot, item, oldest_live_slot=None):
     s_tm1 = np.asarray(item.s_tm1, np.uint8)
     s_t = np.asarray(item.s_t, np.uint8)
-    fidx = self.allocator.allocate(slot, s_tm1, s_t, oldest_live_slot)
-    self.store.write_transition(slot, fidx, item.a_tm1, item.r_t,
-                                item.discount_t)
+    fidx, new_frames = self.allocator.allocate(slot, s_tm1, s_t,
+                                               oldest_live_slot)
+    self.store.put(slot, fidx, item.a_tm1, item.r_t, item.discount_t,
+                   new_frames)
 
   def get(self, slot):
     return self.host_batch(np.array([slot]), single=True)

@@ -18,11 +18,13 @@ import ctypes
 
 import numpy as np
 import torch
+import xxhash
 
 from dqn_mgsc_zoo_amd import _native
 
 FRAME_BYTES = _native.FRAME_BYTES
 STACK = _native.STACK
+_STAGE_SLOTS = 64
 
 
 class FrameStore:
@@ -44,6 +46,8 @@ class FrameStore:
                               device=self.device)
     self.discount = torch.zeros((self.capacity,), dtype=torch.float32,
                                 device=self.device)
+    self._stage = None  # pinned staging slots of put(), allocated on first use
+    self._stage_k = 0
     self._c = _native.DqzStore(
         self.frames.data_ptr(), self.fidx.data_ptr(), self.action.data_ptr(),
         self.reward.data_ptr(), self.discount.data_ptr(), self.capacity,
@@ -56,16 +60,39 @@ class FrameStore:
   def c_ref(self):
     return ctypes.byref(self._c)
 
-  def write_frame(self, index, frame):
-    """Copies one host [84,84] (or [7056]) uint8 frame into the pool."""
-    self.frames[index].copy_(
-        torch.from_numpy(np.ascontiguousarray(frame, np.uint8).reshape(-1)))
+  def put(self, slot, fidx8, a_tm1, r_t, discount_t, new_frames=()):
+    """One replay add in one launch (dqz_store_put): the new frames
+    [(pool row, host [84,84] uint8), ...] go through a pinned staging slot
+    that the kernel reads in place, then the record {fidx, a, r, d}.
 
-  def write_transition(self, slot, fidx8, a_tm1, r_t, discount_t):
-    self.fidx[slot].copy_(torch.as_tensor(np.asarray(fidx8, np.int32)))
-    self.action[slot] = int(a_tm1)
-    self.reward[slot] = float(r_t)
-    self.discount[slot] = float(discount_t)
+    Staging slots are reused round-robin once the launch that read them has
+    completed (one event per slot), so calls return without waiting."""
+    if self._stage is None:
+      self._stage = torch.empty((_STAGE_SLOTS, 8, FRAME_BYTES), dtype=torch.uint8,
+                                pin_memory=True)
+      self._stage_np = self._stage.numpy()
+      self._stage_ev = [None] * _STAGE_SLOTS
+    k = self._stage_k
+    self._stage_k = (k + 1) % _STAGE_SLOTS
+    if self._stage_ev[k] is not None:
+      self._stage_ev[k].synchronize()
+    t = _native.DqzTransitionPut()
+    t.slot = int(slot)
+    for i, f in enumerate(fidx8):
+      t.fidx[i] = int(f)
+    t.action = int(a_tm1)
+    t.reward = float(r_t)
+    t.discount = float(discount_t)
+    t.num_frames = len(new_frames)
+    for i, (row, frame) in enumerate(new_frames):
+      self._stage_np[k, i] = np.asarray(frame, np.uint8).reshape(-1)
+      t.frame_rows[i] = int(row)
+    _native.check(_native.lib().dqz_store_put(
+        self.c_ref(), ctypes.byref(t),
+        ctypes.c_void_p(self._stage[k].data_ptr()), _native.stream_handle()))
+    if self._stage_ev[k] is None:
+      self._stage_ev[k] = torch.cuda.Event()
+    self._stage_ev[k].record()
 
   def gather_stacks(self, slots, which, stream=None):
     """uint8 [n,84,84,4] stacks of `which` (0 = s_tm1, 1 = s_t) on device."""
@@ -89,6 +116,15 @@ class FrameAllocator:
       otherwise `allocate` raises (the pool is too small for the stream).
     * 'slot': reservoir replays; slot i owns pool indices
       [i*per_slot, (i+1)*per_slot) and only shares frames within itself.
+
+  Ring mode takes two byte-exact shortcuts before hashing a channel: the
+  accumulator hands the previous transition's s_t object back as the next
+  s_tm1 (replay.py:1183-1191), whose channels are then already placed; and
+  the frame stack shifts by one frame per step (processors.py:497-504), so
+  s_t channels 0..2 equal s_tm1 channels 1..3 whenever one vectorised
+  compare of the two stacks' 32-bit pixels says so.  Every other channel is
+  fingerprinted (xxh3 of the contiguous plane) against a window of recent
+  frames and byte-compared before it is shared.
   """
 
   def __init__(self, store, mode, per_slot=8, window=16):
@@ -98,38 +134,59 @@ class FrameAllocator:
     self._mode = mode
     self._per_slot = per_slot
     self._pos = 0  # ring: absolute position of the next frame
-    self._recent = collections.OrderedDict()  # key -> absolute position
+    self._recent = collections.OrderedDict()  # fingerprint -> (absolute position, plane)
     self._window = window
     self._min_ref = {}  # slot -> oldest absolute frame position referenced
+    self._new = []  # frames of the current allocate() still to be written
+    self._prev = None  # (last s_t object, its 4 absolute positions / -1)
 
   def allocate(self, slot, s_tm1, s_t, oldest_live_slot=None):
-    """Writes the unique frames of the two stacks; returns 8 pool indices."""
-    channels = [s_tm1[..., c] for c in range(STACK)] + [
-        s_t[..., c] for c in range(STACK)]
+    """Assigns pool rows to the channels of the two stacks.
+
+    Returns (8 pool indices, [(pool row, frame plane), ...] of the frames
+    that are new and still have to be written, in order)."""
+    self._new = []
     if self._mode == 'slot':
-      return self._allocate_slot(slot, channels)
-    out = []
-    refs = []
-    for ch in channels:
-      if not ch.any():
-        out.append(-1)
-        continue
-      raw = ch.tobytes()
-      key = hash(raw)
-      hit = self._recent.get(key)
-      if (hit is not None and hit[1] == raw and
-          self._pos - hit[0] <= self._store.num_frames):
-        pos = hit[0]
-        self._recent.move_to_end(key)
-      else:
-        pos = self._append(ch, oldest_live_slot)
-        self._recent[key] = (pos, raw)
-        while len(self._recent) > self._window:
-          self._recent.popitem(last=False)
-      refs.append(pos)
-      out.append(pos % self._store.num_frames)
+      return self._allocate_slot(slot, s_tm1, s_t), self._new
+    nf = self._store.num_frames
+    prev = self._prev
+    if (prev is not None and prev[0] is s_tm1 and
+        all(p < 0 or self._pos - p <= nf for p in prev[1])):
+      first = list(prev[1])
+    else:
+      first = [self._place(s_tm1, c, oldest_live_slot) for c in range(STACK)]
+    second = [None] * STACK
+    if (s_tm1.flags.c_contiguous and s_t.flags.c_contiguous and
+        s_tm1.shape == (84, 84, STACK) and s_t.shape == (84, 84, STACK)):
+      u_tm1 = s_tm1.view(np.uint32).reshape(-1)
+      u_t = s_t.view(np.uint32).reshape(-1)
+      if np.array_equal(u_t & np.uint32(0x00FFFFFF), u_tm1 >> np.uint32(8)):
+        second[:STACK - 1] = first[1:]
+    for c in range(STACK):
+      if second[c] is None:
+        second[c] = self._place(s_t, c, oldest_live_slot)
+    self._prev = (s_t, second)
+    positions = first + second
+    refs = [p for p in positions if p >= 0]
     self._min_ref[slot] = min(refs) if refs else self._pos
-    return out
+    return [p % nf if p >= 0 else -1 for p in positions], self._new
+
+  def _place(self, stack, c, oldest_live_slot):
+    """Absolute pool position of channel c of `stack` (-1: all zero)."""
+    ch = np.ascontiguousarray(stack[..., c]).reshape(-1)
+    if not ch.any():
+      return -1
+    key = xxhash.xxh3_64_intdigest(ch)
+    hit = self._recent.get(key)
+    if (hit is not None and self._pos - hit[0] <= self._store.num_frames and
+        np.array_equal(hit[1], ch)):
+      self._recent.move_to_end(key)
+      return hit[0]
+    pos = self._append(ch, oldest_live_slot)
+    self._recent[key] = (pos, ch)
+    while len(self._recent) > self._window:
+      self._recent.popitem(last=False)
+    return pos
 
   def _append(self, ch, oldest_live_slot):
     pos = self._pos
@@ -140,29 +197,31 @@ class FrameAllocator:
             'Frame pool of %d frames is too small for this transition stream: '
             'overwriting frame %d still referenced by a live transition. '
             'Increase num_frames.' % (self._store.num_frames, victim))
-    self._store.write_frame(pos % self._store.num_frames, ch)
+    self._new.append((pos % self._store.num_frames, ch))
     self._pos += 1
     return pos
 
-  def _allocate_slot(self, slot, channels):
+  def _allocate_slot(self, slot, s_tm1, s_t):
     base = slot * self._per_slot
     seen = {}
     out = []
     used = 0
-    for ch in channels:
-      if not ch.any():
-        out.append(-1)
-        continue
-      key = ch.tobytes()
-      if key not in seen:
-        if used == self._per_slot:
-          raise RuntimeError(
-              'transition has more than %d distinct frames; construct the '
-              'replay with frames_per_slot=8.' % self._per_slot)
-        self._store.write_frame(base + used, ch)
-        seen[key] = base + used
-        used += 1
-      out.append(seen[key])
+    for stack in (s_tm1, s_t):
+      for c in range(STACK):
+        ch = np.ascontiguousarray(stack[..., c]).reshape(-1)
+        if not ch.any():
+          out.append(-1)
+          continue
+        key = ch.tobytes()
+        if key not in seen:
+          if used == self._per_slot:
+            raise RuntimeError(
+                'transition has more than %d distinct frames; construct the '
+                'replay with frames_per_slot=8.' % self._per_slot)
+          self._new.append((base + used, ch))
+          seen[key] = base + used
+          used += 1
+        out.append(seen[key])
     return out
 
   def forget(self, slot):
@@ -170,12 +229,14 @@ class FrameAllocator:
 
   def get_state(self):
     return {'mode': self._mode, 'per_slot': self._per_slot, 'pos': self._pos,
-            'recent': list(self._recent.items()),
+            'recent': [(k, (p, ch.tobytes())) for k, (p, ch) in self._recent.items()],
             'min_ref': dict(self._min_ref)}
 
   def set_state(self, state):
     self._mode = state['mode']
     self._per_slot = state['per_slot']
     self._pos = state['pos']
-    self._recent = collections.OrderedDict(state['recent'])
+    self._recent = collections.OrderedDict(
+        (k, (p, np.frombuffer(raw, np.uint8))) for k, (p, raw) in state['recent'])
     self._min_ref = dict(state['min_ref'])
+    self._prev = None

@@ -175,6 +175,39 @@ int dqz_forward(dqz_learner* learner, const float* params, const uint8_t* states
 int dqz_forward_slots(dqz_learner* learner, const float* params, const dqz_store* store,
                       const int32_t* slots, int n, int which, float* q_out, void* stream);
 
+/* ---- actor path (dqn/agent.py:121-131, 169-177) -------------------------
+ * select_action on device: q = Q(params, states[i]), v = max_a q,
+ * a ~ distrax.EpsilonGreedy(q, epsilon): P(a) = (1 - eps) [q_a == v] / #ties
+ * + eps / A (fp64, as parts.epsilon_greedy_probs), drawn by inverting the
+ * CDF the way numpy's Generator.choice does (cumsum, normalised by its last
+ * entry, first entry > u) with u = Philox4x32-10(key = seed, counter =
+ * (counter, i)).  `states` (uint8 [n][84][84][4]) and `out` may be device
+ * memory or pinned (hipHostMalloc / torch pin_memory) host memory, which
+ * the kernels read and write in place: one call, no staging copies.  Host
+ * results are valid after the stream is synchronised.  n <= learner batch. */
+typedef struct dqz_action {
+  int32_t action;
+  float value; /* max_a q: the agent's statistics['state_value'] */
+} dqz_action;
+int dqz_act(dqz_learner* learner, const float* params, const uint8_t* states, int n, double epsilon,
+            uint64_t seed, uint64_t counter, dqz_action* out, void* stream);
+
+/* One replay add into the HBM store in one launch (TransitionReplay.add,
+ * replay.py:182-192): copies `num_frames` new frames (uint8 [num_frames][7056]
+ * at `frames`, device or pinned host memory) into pool rows frame_rows[i],
+ * then writes the transition record {fidx, a, r, d} at `slot`.  Writes
+ * through the store's (caller-owned, writable) buffers. */
+typedef struct dqz_transition_put {
+  int64_t slot;
+  int32_t fidx[8];       /* pool rows of s_tm1 / s_t channels, -1 = zero padding */
+  int32_t action;
+  float reward, discount;
+  int32_t num_frames;    /* <= 8 */
+  int32_t frame_rows[8]; /* destination pool row of each new frame */
+} dqz_transition_put;
+int dqz_store_put(const dqz_store* store, const dqz_transition_put* t, const uint8_t* frames,
+                  void* stream);
+
 /* Uniform sampling with replacement over live transitions, on device
  * (UniformDistribution.sample, replay.py:119-125; replay_circular.py:283-289).
  * Live slots are (base + j) mod capacity for j in [0, size).  FIFO replay:
