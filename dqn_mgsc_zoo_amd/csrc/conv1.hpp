@@ -157,16 +157,24 @@ __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* sme
   }
   DQZ_STAMP(0, 2);
   // C/D map of 32x32x2: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+  // (fields read once: inside the store loop they could alias `out`, and the
+  // compiler would re-read them behind a vmcnt(0) per store)
   float* out = a.out + (((int64_t)z * a.B + b) * C1M + rb * C1_POS) * C1CO;
+  const bool linear = a.linear;
+  // Materialise the bias before the store loop: otherwise its (long landed)
+  // load is waited for with a vmcnt(0) inside every exec-masked store group,
+  // and vmcnt counts the stores issued so far too.
+  float bias_r = bias;
+  asm volatile("" : "+v"(bias_r));
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int pos = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (pos < C1_POS) {
-      const float v = acc[r] + bias;
+      const float v = acc[r] + bias_r;
       if constexpr (PUB)
-        __hip_atomic_store(out + pos * C1CO + i, a.linear ? v : relu(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(out + pos * C1CO + i, linear ? v : relu(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
-        out[pos * C1CO + i] = a.linear ? v : relu(v);
+        out[pos * C1CO + i] = linear ? v : relu(v);
     }
   }
   if constexpr (PUB) a.pub.arrive(sj.s);

@@ -103,13 +103,14 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1536 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
+  const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < C2M * 16; i += 256) {
     const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bv;
     if constexpr (PUB)
-      __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), a.linear ? v : relu(v), __ATOMIC_RELAXED,
+      __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     else
-      out[(i >> 4) * C2CO + (i & 15)] = a.linear ? v : relu(v);
+      out[(i >> 4) * C2CO + (i & 15)] = linear ? v : relu(v);
   }
   if constexpr (PUB) a.pub.arrive(sj.s);
   DQZ_STAMP(1, 3);
@@ -189,9 +190,10 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1024 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
+  const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < C3M * 16; i += 256) {
     const float v = ((s_red[i] + s_red[1024 + i]) + (s_red[2048 + i] + s_red[3072 + i])) + bv;
-    out[(i >> 4) * C3CO + (i & 15)] = a.linear ? v : relu(v);
+    out[(i >> 4) * C3CO + (i & 15)] = linear ? v : relu(v);
   }
   DQZ_STAMP(2, 3);
 }
