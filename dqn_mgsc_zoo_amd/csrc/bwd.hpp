@@ -25,7 +25,35 @@ struct Fc1BwdArgs {
   Rms rms;
   int B;
   float* dy3;  // [B][3136]
+  // fc1_dx_kernel also writes the B-operand-ordered copies of W3 and W2 that
+  // the conv3 / conv2 dX jobs of this step load as whole float4 lines
+  // (permute_dx_weights below); null in launches that do not need them.
+  const float *w3, *w2;
+  float *w3p, *w2p;
 };
+
+// Permuted copies of the current W3 / W2 for the dX jobs.  A dX job's lane
+// (n, kq) of wave w needs, per tap t, the four values W[t][ci = 16 q + n]
+// [co = 16 w + 4 j + kq], j = 0..3 (v_mfma_f32_16x16x4 B operand, k = co):
+// 64-byte-strided dwords in W's HWIO layout (one 64-lane load touches 16
+// lines; 36 such loads per conv3 dX lane were the bulk of its staging
+// time).  The copies store them as [job group][t][w][n][kq][j], so a wave
+// reads one contiguous 1 KB run per tap (one float4 per lane).
+//   w3p: [nq 4][t' 9][w 4][n 16][kq 4][j 4], t' = flipped tap (8 - t)
+//   w2p: [ph 2][pw 2][hh 2][t 4][w 4][n 16][kq 4][j 4], t = (u, v): kh = ph +
+//        2 (1 - u), kw = pw + 2 (1 - v)
+__device__ __forceinline__ int w3p_src(int i) {
+  const int j = i & 3, kq = (i >> 2) & 3, n = (i >> 4) & 15, w = (i >> 8) & 3, r = i >> 10;
+  const int tp = r % 9, nq = r / 9;
+  return ((8 - tp) * C3CI + 16 * nq + n) * C3CO + 16 * w + 4 * j + kq;
+}
+__device__ __forceinline__ int w2p_src(int i) {
+  const int j = i & 3, kq = (i >> 2) & 3, n = (i >> 4) & 15, w = (i >> 8) & 3, tp = (i >> 10) & 3;
+  const int hh = (i >> 12) & 1, pw = (i >> 13) & 1, ph = (i >> 14) & 1;
+  const int kh = ph + 2 * (1 - (tp >> 1)), kw = pw + 2 * (1 - (tp & 1));
+  return ((kh * C2K + kw) * C2CI + 16 * hh + n) * C2CO + 16 * w + 4 * j + kq;
+}
+constexpr int W3P_N = 4 * 9 * 1024, W2P_N = 8 * 4 * 1024;  // 36864, 32768
 
 constexpr int FC1B_LD = 528;  // LDS row stride of the dz1 chunk: 528 = 16 (mod 32) banks apart
 
@@ -196,6 +224,7 @@ struct Conv3BwdArgs {
   const float* dy3;  // [B][49][64]
   const float* y2;   // [B][81][64] online
   const float* w3;   // online W3 [3][3][64][64]
+  const float* w3p;  // its dX-ordered copy (permute_dx_weights)
   float* dy2;        // [B][81][64]
   float* part;       // [B][577][64]
   int B;
@@ -211,11 +240,17 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   // B operand: flipped kernel, k = (tap' = kh'*3 + kw', co), wave w owns co [16w, 16w + 16)
-  float wr[36];
+  float wr[36];  // wr[4 t' + j] = W3[8 - t'][16 nq + n][16 w + 4 j + kq]
+  {
+    const float4* wp = reinterpret_cast<const float4*>(a.w3p) + ((nq * 9 * 4 + w) * 16 + n) * 4 + kq;
 #pragma unroll
-  for (int kk = 0; kk < 36; ++kk) {
-    const int tap = 8 - (kk >> 2);  // (2 - kh')*3 + (2 - kw')
-    wr[kk] = a.w3[(tap * C3CI + 16 * nq + n) * C3CO + 16 * w + 4 * (kk & 3) + kq];
+    for (int tp = 0; tp < 9; ++tp) {
+      const float4 v = wp[tp * 256];
+      wr[4 * tp] = v.x;
+      wr[4 * tp + 1] = v.y;
+      wr[4 * tp + 2] = v.z;
+      wr[4 * tp + 3] = v.w;
+    }
   }
   float ym[3];  // relu'(y2) operands of the epilogue, loaded early
 #pragma unroll
@@ -364,6 +399,7 @@ struct Conv2BwdArgs {
   const float* dy2;  // [B][81][64]
   const float* y1;   // [B][400][32] online
   const float* w2;   // online W2 [4][4][32][64]
+  const float* w2p;  // its dX-ordered copy (permute_dx_weights)
   float* dy1;        // [B][400][32]
   float* part;       // [B][513][64]
   int B;
@@ -378,12 +414,18 @@ template <bool WAIT>
 __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
-  float wr[16];
+  float wr[16];  // wr[4 t + j] = W2[kh(t)][kw(t)][16 hh + n][16 w + 4 j + kq]
+  {
+    const float4* wp =
+        reinterpret_cast<const float4*>(a.w2p) + (((((ph * 2 + pw) * 2 + hh) * 4) * 4 + w) * 16 + n) * 4 + kq;
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    const int tp = kk >> 2, u = tp >> 1, v = tp & 1;
-    const int kh = ph + 2 * (1 - u), kw = pw + 2 * (1 - v);
-    wr[kk] = a.w2[((kh * C2K + kw) * C2CI + 16 * hh + n) * C2CO + 16 * w + 4 * (kk & 3) + kq];
+    for (int tp = 0; tp < 4; ++tp) {
+      const float4 v = wp[tp * 256];
+      wr[4 * tp] = v.x;
+      wr[4 * tp + 1] = v.y;
+      wr[4 * tp + 2] = v.z;
+      wr[4 * tp + 3] = v.w;
+    }
   }
   float ym[7];  // relu'(y1) operands of the epilogue, loaded early
 #pragma unroll
@@ -639,7 +681,19 @@ constexpr size_t kBwdDSmem = (C2W_WIN * sizeof(float) > kConv1DwSmem) ? C2W_WIN 
 
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[FC1B_SMEM];
+  // W3 / W2 dX copies: element i of the 69,632 is thread i of the grid (the
+  // gathers are issued first and land under the block's own work)
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  float v3 = 0.f, v2 = 0.f;
+  if (a.w3p) {
+    if (g < W3P_N) v3 = a.w3[w3p_src(g)];
+    if (g < W2P_N) v2 = a.w2[w2p_src(g)];
+  }
   fc1_bwd_body<true, false>(a, smem, blockIdx.x);
+  if (a.w3p) {
+    if (g < W3P_N) a.w3p[g] = v3;
+    if (g < W2P_N) a.w2p[g] = v2;
+  }
   DQZ_STAMP(5, 3);
 }
 

@@ -52,6 +52,7 @@ struct dqz_learner {
   int64_t off[10], sz[10], total;
   int S_fc1, S2, S3;
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
+  float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   int fused_bwd;  // 1: bwd_bc_kernel + bwd_d_kernel; 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
@@ -113,10 +114,10 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 14 * B * Handoff::kStride + 64};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 14 * B * Handoff::kStride + 64, W3P_N, W2P_N};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
-                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync)};
+                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -338,6 +339,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.rms = rms;
   fb.B = B;
   fb.dy3 = L->dy3;
+  fb.w3 = P->online + L->off[4];
+  fb.w2 = P->online + L->off[2];
+  fb.w3p = L->w3p;
+  fb.w2p = L->w2p;
   DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
             DQZ_HIP(hipGetLastError()));
 
@@ -345,6 +350,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.dy3 = L->dy3;
   c3b.y2 = L->y2;
   c3b.w3 = P->online + L->off[4];
+  c3b.w3p = L->w3p;
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
   c3b.B = B;
@@ -353,6 +359,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
   c2b.w2 = P->online + L->off[2];
+  c2b.w2p = L->w2p;
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
   c2b.B = B;

@@ -15,7 +15,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')
 subprocess.check_call(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC',
-                       '-DDQZ_TRACE', '-I' + os.path.join(ROOT, 'include'), '-o', LIB,
+                       '-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split(),
+                       '-I' + os.path.join(ROOT, 'include'), '-o', LIB,
                        os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'csrc', 'learner.hip')])
 os.environ['DQZ_LIB'] = LIB
 sys.path.insert(0, ROOT)
