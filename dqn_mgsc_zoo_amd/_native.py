@@ -146,6 +146,9 @@ SIGNATURES = {
     'dqz_store_put': (
         _int, [ctypes.POINTER(DqzStore), ctypes.POINTER(DqzTransitionPut), _vp,
                _vp]),
+    'dqz_frame_plan_create': (_int, [_int, _int, _int, _int, ctypes.POINTER(_vp)]),
+    'dqz_frame_plan_destroy': (_int, [_vp]),
+    'dqz_atari_frame': (_int, [_vp, _vp, _int, _vp, _vp]),
     'dqz_sample_uniform': (
         _int, [_i64, _i64, _i64, _int, ctypes.c_uint64, _vp, _vp, _vp]),
     'dqz_gather_stacks': (

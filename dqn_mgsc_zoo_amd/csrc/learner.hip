@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <vector>
 #include <cstdlib>
 #include <cstring>
 
@@ -24,6 +26,7 @@
 #include "meta.hpp"
 #include "hvp.hpp"
 #include "sampling.hpp"
+#include "preprocess.hpp"
 
 namespace dqz {
 
@@ -1120,4 +1123,115 @@ extern "C" int dqz_debug_trace(unsigned long long* host_out, int clear) {
   return DQZ_OK;
 }
 #endif
+
+// ---------------------------------------------------------------------------
+// Atari observation preprocessing (processors.py:488-497)
+
+struct dqz_frame_plan {
+  FramePlan p;
+  void* block;
+};
+
+// Pillow's precompute_coeffs + normalize_coeffs_8bpc for the BILINEAR
+// filter (support 1) on one axis with box (0, in_size): bounds[2 * o] =
+// first source index, bounds[2 * o + 1] = count; k[o * ksize + i] = int32
+// weights with 22 fractional bits.
+static int pil_bilinear_coeffs(int in_size, int out_size, std::vector<int32_t>& bounds, std::vector<int32_t>& k) {
+  const double scale = (double)((float)in_size - 0.0f) / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;
+  const int ksize = (int)std::ceil(support) * 2 + 1;
+  const double ss = 1.0 / filterscale;
+  bounds.assign(2 * out_size, 0);
+  k.assign((size_t)out_size * ksize, 0);
+  std::vector<double> w(ksize);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = 0.0 + (xx + 0.5) * scale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      double t = (x + xmin - center + 0.5) * ss;
+      if (t < 0.0) t = -t;
+      w[x] = t < 1.0 ? 1.0 - t : 0.0;
+      ww += w[x];
+    }
+    for (int x = 0; x < xmax; ++x) {
+      const double v = ww != 0.0 ? w[x] / ww : w[x];
+      k[(size_t)xx * ksize + x] = v < 0 ? (int32_t)(-0.5 + v * (1 << FR_PREC)) : (int32_t)(0.5 + v * (1 << FR_PREC));
+    }
+    bounds[2 * xx] = xmin;
+    bounds[2 * xx + 1] = xmax;
+  }
+  return ksize;
+}
+
+extern "C" {
+
+int dqz_frame_plan_create(int in_h, int in_w, int out_h, int out_w, dqz_frame_plan** out) {
+  if (!out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (in_h < 1 || in_w < 1 || out_h < 1 || out_w < 1 || in_h > 4096 || in_w > 4096 || out_h > 4096 || out_w > 4096)
+    return fail(DQZ_ERR_INVALID, "frame sizes must be in [1, 4096]");
+  std::vector<int32_t> hb, hk, vb, vk;
+  const int kh = pil_bilinear_coeffs(in_w, out_w, hb, hk);
+  const int kv = pil_bilinear_coeffs(in_h, out_h, vb, vk);
+  int max_band = 0;
+  for (int yy0 = 0; yy0 < out_h; yy0 += FR_ROWS) {
+    const int yy1 = std::min(yy0 + FR_ROWS, out_h);
+    max_band = std::max(max_band, vb[2 * (yy1 - 1)] + vb[2 * (yy1 - 1) + 1] - vb[2 * yy0]);
+  }
+  const size_t smem = (size_t)max_band * (in_w + out_w);
+  if (smem > 64 * 1024) return fail(DQZ_ERR_INVALID, "frame too large for one workgroup's band (%zu B of LDS)", smem);
+  const size_t n = hb.size() + hk.size() + vb.size() + vk.size();
+  dqz_frame_plan* P = new dqz_frame_plan();
+  if (hipMalloc(&P->block, n * sizeof(int32_t)) != hipSuccess) {
+    delete P;
+    return fail(DQZ_ERR_HIP, "hipMalloc of the resize tables failed");
+  }
+  std::vector<int32_t> all;
+  all.reserve(n);
+  all.insert(all.end(), hb.begin(), hb.end());
+  all.insert(all.end(), hk.begin(), hk.end());
+  all.insert(all.end(), vb.begin(), vb.end());
+  all.insert(all.end(), vk.begin(), vk.end());
+  if (hipMemcpy(P->block, all.data(), n * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(P->block);
+    delete P;
+    return fail(DQZ_ERR_HIP, "upload of the resize tables failed");
+  }
+  const int32_t* d = static_cast<const int32_t*>(P->block);
+  P->p = FramePlan{in_h, in_w, out_h, out_w, kh, kv, max_band, d, d + hb.size(), d + hb.size() + hk.size(),
+                   d + hb.size() + hk.size() + vb.size()};
+  *out = P;
+  return DQZ_OK;
+}
+
+int dqz_frame_plan_destroy(dqz_frame_plan* P) {
+  if (!P) return DQZ_OK;
+  if (P->block) (void)hipFree(P->block);
+  delete P;
+  return DQZ_OK;
+}
+
+int dqz_atari_frame(const dqz_frame_plan* P, const uint8_t* rgb, int n, uint8_t* out, void* stream) {
+  if (!P || !rgb || !out) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 1 || n > 8) return fail(DQZ_ERR_INVALID, "n must be in [1, 8]");
+  const void *drgb = nullptr, *dout = nullptr;
+  if (int rc = device_view(rgb, &drgb, "rgb")) return rc;
+  if (int rc = device_view(out, &dout, "out")) return rc;
+  if (P->p.in_w % 4 == 0 && reinterpret_cast<uintptr_t>(drgb) % 4)
+    return fail(DQZ_ERR_INVALID, "rgb must be 4-byte aligned");
+  const int64_t stride = (int64_t)P->p.in_h * P->p.in_w * 3;
+  const size_t smem = (size_t)P->p.max_band * (P->p.in_w + P->p.out_w);
+  hipLaunchKernelGGL(atari_frame_kernel, dim3((P->p.out_h + FR_ROWS - 1) / FR_ROWS), dim3(256), smem,
+                     (hipStream_t)stream, P->p, static_cast<const uint8_t*>(drgb), n, stride,
+                     static_cast<uint8_t*>(const_cast<void*>(dout)));
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+}  // extern "C"
 

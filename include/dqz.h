@@ -327,6 +327,20 @@ int dqz_meta_update(dqz_meta* meta, const dqz_params* params, const dqz_store* s
 int dqz_meta_outputs(dqz_meta* meta, float* probs, float* dlogits, float* td, float* loss,
                      void* stream);
 
+/* ---- Atari observation preprocessing (processors.py:421-505) -----------
+ * The observation branch of processors.atari on device: element-wise max of
+ * the last n RGB frames (np.max over the pooled frames), rgb2y
+ * (processors.py:367-371, numpy's float64 evaluation, truncated to uint8)
+ * and PIL's BILINEAR resize (processors.py:374-387; Pillow's 8-bit
+ * fixed-point two-pass resampler), in one launch.  A dqz_frame_plan holds
+ * the resize coefficient tables of one (in_h, in_w) -> (out_h, out_w). */
+typedef struct dqz_frame_plan dqz_frame_plan;
+int dqz_frame_plan_create(int in_h, int in_w, int out_h, int out_w, dqz_frame_plan** out);
+int dqz_frame_plan_destroy(dqz_frame_plan* plan);
+/* rgb: n frames uint8 [n][in_h][in_w][3], contiguous; out: uint8
+ * [out_h][out_w].  Either may be device memory or pinned host memory. */
+int dqz_atari_frame(const dqz_frame_plan* plan, const uint8_t* rgb, int n, uint8_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
