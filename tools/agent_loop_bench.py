@@ -29,6 +29,42 @@ from dqn_mgsc_zoo_amd import replay as replay_lib  # noqa: E402
 from tests import fake_env  # noqa: E402
 
 
+class FakeRGBAtari:
+  """Raw-Atari-shaped env: (rgb uint8 [210,160,3], lives) observations,
+  env discount 1 (0 at LAST), a life lost now and then."""
+
+  def __init__(self, episode_len=2000, seed=1):
+    self._rng = np.random.default_rng(seed)
+    self._len = episode_len
+    # a pool of frames: drawing 100 KB of random bytes per step would cost
+    # more host time than the agent itself
+    self._pool = self._rng.integers(0, 256, (64, 210, 160, 3), dtype=np.uint8)
+
+  def _obs(self):
+    return (self._pool[self._t % 64], self._lives)
+
+  def reset(self):
+    self._t, self._lives = 0, 5
+    return parts.TimeStep(parts.StepType.FIRST, None, None, self._obs())
+
+  def step(self, action):
+    del action
+    self._t += 1
+    if self._t % 97 == 0 and self._lives > 1:
+      self._lives -= 1
+    last = self._t >= self._len
+    return parts.TimeStep(parts.StepType.LAST if last else parts.StepType.MID,
+                          float(self._t % 7 == 0), 0.0 if last else 1.0, self._obs())
+
+
+def host_atari_frame(obs):
+  """The reference's host observation math (processors.py:488-497)."""
+  from PIL import Image  # pylint: disable=g-import-not-at-top
+  pooled = np.max(np.stack(list(obs)[-2:], axis=0), axis=0)
+  y = np.tensordot(pooled, [0.299, 0.587, 1 - (0.299 + 0.587)], (-1, 0)).astype(np.uint8)
+  return np.array(Image.fromarray(y).resize((84, 84), Image.Resampling.BILINEAR), dtype=np.uint8)
+
+
 class RepeatStacker(fake_env.FrameStacker):
   """FrameStacker that emits every `repeat`-th frame (None in between)."""
 
@@ -46,7 +82,7 @@ class RepeatStacker(fake_env.FrameStacker):
     return super().__call__(timestep)
 
 
-def make_agent(kind, capacity, seed=0):
+def make_agent(kind, capacity, seed=0, preprocessor=None):
   rs = np.random.RandomState(seed)
   structure = replay_lib.Transition(None, None, None, None, None)
   if kind == 'double':
@@ -57,7 +93,7 @@ def make_agent(kind, capacity, seed=0):
     cls, net = agent_lib.Dqn, networks.dqn_atari_network(6)
   replay = replay_lib.TransitionReplay(capacity, structure, rs)
   return cls(
-      preprocessor=RepeatStacker(),
+      preprocessor=preprocessor or RepeatStacker(),
       sample_network_input=np.zeros((84, 84, 4), np.uint8),
       network=net,
       optimizer=learner_lib.rmsprop(2.5e-4, 0.95, 0.01 / 32**2, centered=True),
@@ -75,8 +111,15 @@ def main():
   ap.add_argument('--frames', type=int, default=8000)
   ap.add_argument('--capacity', type=int, default=20_000)
   ap.add_argument('--kind', default='dqn', choices=['dqn', 'double'])
+  ap.add_argument('--env', default='stacked', choices=['stacked', 'atari-device', 'atari-host'],
+                  help='stacked: pre-stacked 84x84 frames; atari-*: raw RGB frames through '
+                       'processors.atari with the observation math on device or on the host')
   args = ap.parse_args()
-  agent = make_agent(args.kind, args.capacity)
+  pre = None
+  if args.env != 'stacked':
+    from dqn_mgsc_zoo_amd import processors  # pylint: disable=g-import-not-at-top
+    pre = processors.atari(observation_frame=host_atari_frame if args.env == 'atari-host' else None)
+  agent = make_agent(args.kind, args.capacity, preprocessor=pre)
   times = {'act': 0.0, 'add': 0.0, 'learn': 0.0}
   counts = {'act': 0, 'add': 0, 'learn': 0}
 
@@ -92,7 +135,8 @@ def main():
   agent._act = wrap('act', agent._act)  # pylint: disable=protected-access
   agent._add = wrap('add', agent._add)  # pylint: disable=protected-access
   agent._learn = wrap('learn', agent._learn)  # pylint: disable=protected-access
-  env = fake_env.FakeAtari(episode_len=2000, seed=1)
+  env = (fake_env.FakeAtari(episode_len=2000, seed=1) if args.env == 'stacked' else
+         FakeRGBAtari(episode_len=2000, seed=1))
   loop = parts.run_loop(agent, env, max_steps_per_episode=0)
   warm = 4 * int(0.05 * args.capacity) + 256
   for _ in range(warm):
@@ -105,7 +149,7 @@ def main():
     next(loop)
   torch.cuda.synchronize()
   dt = time.perf_counter() - t0
-  out = {'kind': args.kind, 'frames': args.frames, 'seconds': round(dt, 3),
+  out = {'kind': args.kind, 'env': args.env, 'frames': args.frames, 'seconds': round(dt, 3),
          'frames_per_s': round(args.frames / dt, 1),
          'learner_steps_per_s': round(counts['learn'] / dt, 1),
          'us_per_frame': round(1e6 * dt / args.frames, 1)}
