@@ -35,6 +35,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 STEP_FLOP = {'dqn': 2182873088, 'double': 2781020160}
 STEP_BYTES = {'dqn': 49048488, 'double': 49048488}
 
+ALL_BWD = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw'
+
 # Algorithmic MACs per sample of each forward layer.
 MAC = dict(conv1=400 * 256 * 32, conv2=81 * 512 * 64, conv3=49 * 576 * 64,
            fc1=3136 * 512, fc2=512 * NUM_ACTIONS)
@@ -56,6 +58,7 @@ def phase_flops(algo, batch):
       'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 2 * b * (2 * MAC['conv3'] + MAC['fc1'] +
                                                    MAC['conv2']),
       'conv1_dw+conv2_dw': 2 * b * (MAC['conv1'] + MAC['conv2']),
+      ALL_BWD: 2 * b * (2 * MAC['conv3'] + MAC['fc1'] + 2 * MAC['conv2'] + MAC['conv1']),
       'update': 0,
   }
 
@@ -97,6 +100,11 @@ def phase_bytes(algo, batch):
           PARAM['conv2'] + b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
       'conv1_dw+conv2_dw': (b * (ACT['state'] + ACT['y1']) + PARAM['conv1'] +
                             b * (ACT['y1'] + ACT['y2']) + PARAM['conv2']),
+      # the whole backward after fc1 dX in one launch: dy2 and dy1 are handed
+      # off inside it; dy3, y2, y1 and the state are read once
+      ALL_BWD: (b * (ACT['y3'] + ACT['y2'] + ACT['y1'] + ACT['state']) +
+                2 * PARAM['conv3'] + 2 * PARAM['conv2'] + PARAM['conv1'] +
+                b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
       'update': rms,
   }
 
@@ -108,7 +116,8 @@ PHASE_KERNEL = {
     'head': 'head_kernel', 'fc1_dx': 'fc1_dx_kernel',
     'conv3_dx+fc1_dw': 'bwd_b_kernel', 'conv2_dx+conv3_dw': 'bwd_c_kernel',
     'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 'bwd_bc_kernel',
-    'conv1_dw+conv2_dw': 'bwd_d_kernel', 'update': 'update_kernel'}
+    'conv1_dw+conv2_dw': 'bwd_d_kernel', ALL_BWD: 'bwd_bc_kernel',
+    'update': 'update_kernel'}
 PMC_JSON = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
 
 

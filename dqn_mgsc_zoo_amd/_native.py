@@ -20,11 +20,13 @@ NUM_LEAVES = 10
 NUM_PHASES = 10
 PHASE_NAMES = (
     'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_dx',
-    'conv3_dx+conv2_dx+fc1_dw+conv3_dw', 'conv2_dx+conv3_dw',
+    'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw', 'conv2_dx+conv3_dw',
     'conv1_dw+conv2_dw', 'update')
 # Phase 6 of the split-backward debug layout (DQZ_FUSED_BWD=0), where phase 7
-# is a launch of its own.
+# is a launch of its own, and of the late-dW layout (DQZ_DW_LATE=1), where
+# phase 8 is.
 PHASE6_SPLIT = 'conv3_dx+fc1_dw'
+PHASE6_LATE_DW = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw'
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4

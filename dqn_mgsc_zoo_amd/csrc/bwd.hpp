@@ -404,13 +404,15 @@ struct Conv2BwdArgs {
   float* part;       // [B][513][64]
   int B;
   Handoff sync;      // dy2 arrival counters (WAIT)
+  Handoff sync1;     // dy1 arrival counters (PUB)
 };
 
 // WAIT: dy2 of sample b is produced by the 8 conv3 dX jobs of the same launch
 // (bwd_bc_kernel).  Weights and relu'(y1) are loaded first, then one lane
 // polls the sample's counter, and every dy2 load is an sc1 (L1-bypassing)
-// buffer load.
-template <bool WAIT>
+// buffer load.  PUB: dy1 is handed on to the conv1 dW jobs of the same launch
+// (sc1 stores + arrival on sync1).
+template <bool WAIT, bool PUB = false>
 __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -494,10 +496,14 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     if (i < 1600) {
       const int p = i >> 4, ah = p / 10, cw = p % 10;
       const float v = (s_red[i] + s_red[1792 + i]) + (s_red[3584 + i] + s_red[5376 + i]);
-      a.dy1[((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15)] =
-          ym[k] > 0.f ? v : 0.f;
+      float* dst = a.dy1 + ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15);
+      if constexpr (PUB)
+        __hip_atomic_store(dst, ym[k] > 0.f ? v : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *dst = ym[k] > 0.f ? v : 0.f;
     }
   }
+  if constexpr (PUB) a.sync1.arrive(b);
 }
 
 __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win, int b, int nq) {
@@ -554,6 +560,89 @@ __device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win
     sb += __shfl_xor(sb, 16, 64);
     sb += __shfl_xor(sb, 32, 64);
     if (kq == 0) part[C2KK * C2CO] = sb;
+  }
+}
+
+// conv2 dW as 8 jobs per sample for the merged backward launch: job (kh, ch)
+// computes part[b][(kh*4 + kw)*32 + ci][32 ch + co'] for all kw (wave w = kw),
+// ci and its 32 output channels, K = the 81 positions in conv2_bwd_dw's k
+// order (the same bits).  Only the 9 input rows 2 oh + kh are staged (29 KB
+// of LDS instead of 64 KB, so the job fits beside the other backward jobs);
+// dy2 comes from this launch's conv3 dX jobs (wait + sc1 loads).
+constexpr int C2V_WIN = 9 * C2W_RS;  // 7272 floats
+
+__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kw
+  const int n = lane & 15, kq = lane >> 4;
+  // y1 rows 2 oh + kh, oh = 0..8 (not handed off: plain loads, issued first)
+  const float4* src = reinterpret_cast<const float4*>(a.y1 + (int64_t)b * (C1M * C1CO));
+  constexpr int NV4 = 9 * C1O * C1CO / 4;  // 1440
+  float4 r[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int i = min(t + 256 * q, NV4 - 1);
+    const int oh = i / (C1O * 8), rem = i % (C1O * 8);  // 8 float4 per pixel
+    r[q] = src[((2 * oh + kh) * C1O) * 8 + rem];
+  }
+  a.sync.wait(b);
+  float dr[21][2];
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk) {
+    const int p = 4 * kk + kq;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const float* g = a.dy2 + ((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 32 * ch + 16 * ct + n;
+      const float v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dr[kk][ct] = p < C2M ? v : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NV4) {
+      const int oh = i / (C1O * 8), rem = i % (C1O * 8), iw = rem >> 3;
+      *reinterpret_cast<float4*>(s_win + oh * C2W_RS + iw * C2W_S + (rem & 7) * 4) = r[q];
+    }
+  }
+  __syncthreads();
+  DQZ_STAMP(13, 1);
+  int pb[21];
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk) {
+    const int p = min(4 * kk + kq, C2M - 1);
+    pb[kk] = (p / C2O) * C2W_RS + (2 * (p % C2O) + w) * C2W_S + n;
+  }
+  f32x4 acc[2][2];  // [ci tile][co tile]
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const float av = s_win[pb[kk] + 16 * mt];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = mfma4(av, dr[kk][ct], acc[mt][ct]);
+    }
+  float* part = a.part + (int64_t)b * (C2KK + 1) * C2CO + 32 * ch + n;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        part[((kh * C2K + w) * C2CI + 16 * mt + 4 * kq + rr) * C2CO + 16 * ct] = acc[mt][ct][rr];
+  if (kh == 0 && w == 0) {  // bias row (conv2_bwd_dw's order: per lane over kk, then over kq)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float sb = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 21; ++kk) sb += dr[kk][ct];
+      sb += __shfl_xor(sb, 16, 64);
+      sb += __shfl_xor(sb, 32, 64);
+      if (kq == 0) part[C2KK * C2CO + 16 * ct] = sb;
+    }
   }
 }
 
@@ -729,22 +818,30 @@ __global__ __launch_bounds__(256) void bwd_c_kernel(Conv2BwdArgs c2, Conv3BwdArg
   }
 }
 
-// bwd_bc_kernel = bwd_b + bwd_c in one launch.  Grid, in dispatch order:
+// bwd_bc_kernel: the whole backward after fc1 dX in one launch.  Grid, in
+// dispatch order:
 //   [conv3 dX 8/sample] [fc1 dW 784] [conv2 dX 8/sample] [conv3 dW 4/sample]
-// conv2 dX of sample s waits (in-launch hand-off) for the 8 conv3 dX jobs of s,
-// which have lower block indices: workgroups are dispatched in index order, so
-// every producer a consumer waits on is already resident or finished and the
-// wait always terminates.  The first two ranges fill the chip (4 workgroups
-// per CU), so conv2 dX workgroups are dispatched as conv3 dX ones retire
-// instead of spinning from the start.  Sample jobs keep the XCD-aware decode
-// (each range starts at a multiple of 8, so producer and consumer share an L2).
+//   [conv2 dW 8/sample] [conv1 dW 8/sample]
+// (the last two ranges only when c1.B > 0; otherwise conv1 / conv2 dW run in
+// bwd_d_kernel).  Hand-offs inside the launch (common.hpp Handoff): dy2 from
+// the 8 conv3 dX jobs of a sample to its 8 conv2 dX and 8 conv2 dW jobs, dy1
+// from the 8 conv2 dX jobs to its 8 conv1 dW jobs.  Every consumer has a
+// higher block index than its producers and workgroups are dispatched in
+// index order, so every wait terminates.  The first two ranges fill the chip
+// (4 workgroups per CU), so consumers are dispatched as conv3 dX blocks
+// retire instead of spinning from the start.  Sample jobs keep the XCD-aware
+// decode (each range starts at a multiple of 8, so producer and consumer
+// share an L2).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
-    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2) {
+    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1) {
   constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
   constexpr int kW2 = C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN;
-  __shared__ __attribute__((aligned(16))) float smem[kW > kW2 ? kW : kW2];
+  constexpr int kW3 = C2V_WIN > C1H_SMEM ? C2V_WIN : C1H_SMEM;
+  constexpr int kWA = kW > kW2 ? kW : kW2;
+  __shared__ __attribute__((aligned(16))) float smem[kWA > kW3 ? kWA : kW3];
   const int B8 = (c3.B + 7) / 8 * 8;
   constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
+  const bool all_dw = c1.B > 0;
   int i = blockIdx.x;
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
@@ -764,16 +861,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
     DQZ_STAMP(7, 0);
-    conv2_bwd_dx<true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    if (all_dw)
+      conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    else
+      conv2_bwd_dx<true, false>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
     return;
   }
   i -= 8 * B8;
-  const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
+  if (i < 4 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(12, 0);
+    conv3_bwd_dw(c3, smem, sj.s, sj.job);
+    DQZ_STAMP(12, 3);
+    return;
+  }
+  i -= 4 * B8;
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(13, 0);
+    conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
+    DQZ_STAMP(13, 3);
+    return;
+  }
+  i -= 8 * B8;
+  const SampleJob sj = xcd_sample_job_at(i, 8, c1.B);
   if (!sj.valid) return;
-  DQZ_STAMP(12, 0);
-  conv3_bwd_dw(c3, smem, sj.s, sj.job);
-  DQZ_STAMP(12, 3);
+  conv1_dw_half(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
 }
 
 __global__ __launch_bounds__(256) void bwd_d_kernel(Conv1DwArgs c1, Conv2BwdArgs c2) {

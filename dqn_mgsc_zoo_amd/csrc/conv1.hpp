@@ -193,6 +193,7 @@ struct Conv1DwArgs {
   int which, B;
   const float* dy1;  // [B][400][32] (online copy)
   float* part;       // [B*4][257][32]: dW rows 0..255 (HWIO order), db row 256
+  Handoff sync1;     // dy1 arrival counters (conv1_dw_half in bwd_bc_kernel)
 };
 
 // Partial dW/db of one 100-position block: part[k][co] = sum_p x(p,k) dy(p,co).
@@ -242,6 +243,73 @@ __device__ __forceinline__ void conv1_dw_body(const Conv1DwArgs& a, float* smem,
       const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
       part[(kh * 32 + row) * C1CO + i] = acc[r];
     }
+  }
+  DQZ_STAMP(8, 3);
+}
+
+// Half-channel job of conv1 dW for the merged backward launch (bwd_bc_kernel):
+// rows block rb of sample b, input channels {2 ch, 2 ch + 1}.  Its 128 dW rows
+// (kh 8 x kw 8 x ci 2) are four 32-row MFMA tiles, one per wave (wave w: kh
+// 2w, 2w + 1; tile row m = 16 (kh - 2w) + 2 kw + ci'), each accumulated over
+// the 100 positions in conv1_dw_body's k order, so the partials are the
+// same bits.  LDS: two input planes + the 100 x 32 dy1 block (29 KB).  dy1
+// comes from this launch's conv2 dX jobs: the block waits for its sample's
+// counter and loads dy1 with sc1 loads.
+constexpr int C1H_SMEM = 2 * C1_PLANE + C1_POS * C1CO;  // 7232 floats
+
+__device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem, int rb, int ch, int b) {
+  DQZ_STAMP(8, 0);
+  float* s_in = smem;                 // 2 planes x 2016
+  float* s_dy = smem + 2 * C1_PLANE;  // 100 x 32
+  // frames of the two channels: slot -> fidx -> 2 x 126 16-byte pieces
+  const int row0 = rb * C1S * C1_ROWS;
+  constexpr int QPC = C1_PLANE / 16;  // 126
+  const int slot = a.src.slots[b];
+  const int32_t* fr = a.src.fidx + (int64_t)slot * 8 + a.which * 4 + 2 * ch;
+  const int fa = fr[0], fb = fr[1];
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  const int tid = threadIdx.x;
+  const int cl = tid / QPC, j = tid % QPC;  // threads 0..251: channel cl, piece j
+  const int f = cl == 0 ? fa : fb;
+  if (tid < 2 * QPC && f >= 0)
+    v = reinterpret_cast<const uint4*>(a.src.frames + (int64_t)f * FB + row0 * FW)[j];
+  a.sync1.wait(b);
+  const float4* dy4 = reinterpret_cast<const float4*>(a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO);
+  constexpr int ND4 = C1_POS * C1CO / 4;  // 800
+  float4 dv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dv[q] = load_sc1_f4(dy4, ND4 * 16, min(tid + 256 * q, ND4 - 1));
+  if (tid < 2 * QPC) store_bytes_as_f32(s_in + cl * C1_PLANE + j * 16, v);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (tid + 256 * q < ND4) reinterpret_cast<float4*>(s_dy)[tid + 256 * q] = dv[q];
+  __syncthreads();
+  DQZ_STAMP(8, 1);
+  const int lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, i = lane & 31;
+  const int kh = 2 * wave + (i >> 4), kw = (i >> 1) & 7, cp = i & 1;
+  float* part = a.part + ((int64_t)b * C1_BLOCKS + rb) * (C1KK + 1) * C1CO;
+  if (ch == 0 && tid < C1CO) {  // bias row (conv1_dw_body's order)
+    float sb = 0.f;
+    for (int p = 0; p < C1_POS; ++p) sb += s_dy[p * C1CO + tid];
+    part[C1KK * C1CO + tid] = sb;
+  }
+  const float* pa = s_in + cp * C1_PLANE + kh * FW + kw + 4 * h;
+  const float* pb = s_dy + h * C1CO + i;
+  f32x16 acc = {};
+#pragma unroll
+  for (int jj = 0; jj < C1_POS / 2; ++jj) {
+    const int p0 = 2 * jj;  // positions p0 + h share an output row
+    const float av = pa[(C1S * (p0 / C1O)) * FW + C1S * (p0 % C1O)];
+    const float bv = pb[64 * jj];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  }
+  // C row m = (r & 3) + 8 (r >> 2) + 4 h -> kh = 2 wave + (m >> 4), kw = (m >> 1) & 7, ci = 2 ch + (m & 1)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int row = (2 * wave + (m >> 4)) * 32 + ((m >> 1) & 7) * 4 + 2 * ch + (m & 1);
+    part[row * C1CO + i] = acc[r];
   }
   DQZ_STAMP(8, 3);
 }

@@ -58,7 +58,8 @@ struct dqz_learner {
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
-  int fused_bwd;  // 1: bwd_bc_kernel + bwd_d_kernel; 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
+  int fused_bwd;  // 1: bwd_bc_kernel (+ bwd_d_kernel if dw_late); 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
+  int dw_late;    // 1: conv1 / conv2 dW in bwd_d_kernel after the merged launch (DQZ_DW_LATE=1)
   int fused_fwd;  // 1: fwd_conv_kernel (DQZ_FUSED_FWD=1, measured 1.5 % slower); 0: conv1 / conv2 / conv3 launches
   void* block;
 };
@@ -103,6 +104,8 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   {
     const char* e = getenv("DQZ_FUSED_BWD");
     L->fused_bwd = !(e && e[0] == '0');
+    e = getenv("DQZ_DW_LATE");
+    L->dw_late = e && e[0] == '1';
     e = getenv("DQZ_FUSED_FWD");
     L->fused_fwd = e && e[0] == '1';
   }
@@ -117,7 +120,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 14 * B * Handoff::kStride + 64, W3P_N, W2P_N};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 16 * B * Handoff::kStride + 64, W3P_N, W2P_N};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p};
@@ -219,7 +222,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   if (fused_conv) {
     // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample (Z*B <= 3B samples)
     int* hw = L->sync + 2 * B * Handoff::kStride;
-    int* err = L->sync + 14 * B * Handoff::kStride;
+    int* err = L->sync + 16 * B * Handoff::kStride;
     c1.pub = Handoff{hw, hw + 3 * B * Handoff::kStride, err, 4, 4};
     c2.wait = c1.pub;
     c2.pub = Handoff{hw + 6 * B * Handoff::kStride, hw + 9 * B * Handoff::kStride, err, 4, 4};
@@ -357,7 +360,11 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
   c3b.B = B;
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, L->sync + 14 * B * Handoff::kStride, 8, 8};
+  // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
+  // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
+  int* const herr = L->sync + 16 * B * Handoff::kStride;
+  const bool all_dw = L->fused_bwd && !L->dw_late;  // conv1 / conv2 dW inside bwd_bc_kernel
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, all_dw ? 16 : 8};
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -374,10 +381,14 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
+  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8};
+  c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
   if (L->fused_bwd) {
-    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(8 * B8 + 8 * B8 + 4 * B8 + 4 * (FLAT / 16)), dim3(256), 0,
-                                    st, c3b, fb, c2b);
+    Conv1DwArgs c1k = c1dw;
+    if (!all_dw) c1k.B = 0;  // bwd_bc_kernel stops after the conv3 dW range
+    const int grid = 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + (all_dw ? 16 * B8 : 0);
+    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1k);
               DQZ_HIP(hipGetLastError()));
     if (pe.on()) pe.ms[7] = 0.f;
   } else {
@@ -386,8 +397,12 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     DQZ_PHASE(7, hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
               DQZ_HIP(hipGetLastError()));
   }
-  DQZ_PHASE(8, hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
-            DQZ_HIP(hipGetLastError()));
+  if (all_dw) {
+    if (pe.on()) pe.ms[8] = 0.f;
+  } else {
+    DQZ_PHASE(8, hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
+              DQZ_HIP(hipGetLastError()));
+  }
 
   UpdArgs u;
   u.th = P->online;
@@ -459,7 +474,7 @@ int dqz_learner_profile(dqz_learner* L, const dqz_params* P, const dqz_store* S,
 int dqz_learner_sync_status(dqz_learner* L, int* status) {
   if (!L || !status) return fail(DQZ_ERR_INVALID, "null argument");
   DQZ_HIP(hipDeviceSynchronize());
-  DQZ_HIP(hipMemcpy(status, L->sync + 14 * L->cfg.batch * Handoff::kStride, sizeof(int), hipMemcpyDeviceToHost));
+  DQZ_HIP(hipMemcpy(status, L->sync + 16 * L->cfg.batch * Handoff::kStride, sizeof(int), hipMemcpyDeviceToHost));
   return DQZ_OK;
 }
 

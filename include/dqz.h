@@ -137,11 +137,13 @@ int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_s
  *  2 conv3 fwd   3 fc1 fwd (split-K)
  *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample)
  *  5 fc1 dX
- *  6 conv3 dX -> conv2 dX (in-launch per-sample hand-off) + fc1 dW and
- *    RMSProp of fc1/w + conv3 dW partials (one launch, bwd_bc_kernel)
+ *  6 conv3 dX -> conv2 dX -> conv1 dW and conv3 dX -> conv2 dW (in-launch
+ *    per-sample hand-offs of dy2 / dy1) + fc1 dW and RMSProp of fc1/w +
+ *    conv3 dW partials (one launch, bwd_bc_kernel)
  *  7 0 (merged into 6); in the DQZ_FUSED_BWD=0 debug layout 6 is conv3 dX +
  *    fc1 dW and 7 is conv2 dX + conv3 dW partials
- *  8 conv1 dW partials (frame gather fused) + conv2 dW partials
+ *  8 0 (merged into 6); with DQZ_FUSED_BWD=0 or DQZ_DW_LATE=1: conv1 dW
+ *    partials (frame gather fused) + conv2 dW partials
  *  9 gradient reductions + RMSProp (all leaves but fc1/w) */
 #define DQZ_NUM_PHASES 10
 
