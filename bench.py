@@ -53,6 +53,7 @@ def phase_flops(algo, batch):
       'fc1_fwd': 2 * z * b * MAC['fc1'],
       'head': 2 * z * b * MAC['fc2'],
       'fc1_dx': 2 * b * MAC['fc1'],
+      'head+fc1_dx': 2 * z * b * MAC['fc2'] + 2 * b * MAC['fc1'],
       'conv3_dx+fc1_dw': 2 * b * (MAC['conv3'] + MAC['fc1']),
       'conv2_dx+conv3_dw': 2 * b * (MAC['conv2'] + MAC['conv3']),
       'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 2 * b * (2 * MAC['conv3'] + MAC['fc1'] +
@@ -89,6 +90,9 @@ def phase_bytes(algo, batch):
       'fc1_fwd': z * b * (ACT['y3'] + ACT['h']) + z * PARAM['fc1'],
       'head': z * b * ACT['h'] + z * PARAM['fc2'],
       'fc1_dx': b * (ACT['h'] + 2 * ACT['y3']) + PARAM['fc1'],
+      # one launch (head_dx_kernel): dz1 is handed off inside it
+      'head+fc1_dx': (z * b * ACT['h'] + z * PARAM['fc2'] + 2 * b * ACT['y3'] +
+                      PARAM['fc1']),
       'conv3_dx+fc1_dw': (b * (ACT['y3'] + 2 * ACT['y2']) + PARAM['conv3'] +
                           b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
       'conv2_dx+conv3_dw': (b * (ACT['y2'] + 2 * ACT['y1']) + PARAM['conv2'] +
@@ -114,6 +118,7 @@ PHASE_KERNEL = {
     'conv1_fwd': 'conv1_fwd_kernel', 'conv2_fwd': 'conv2_fwd_kernel',
     'conv3_fwd': 'conv3_fwd_kernel', 'fc1_fwd': 'fc1_fwd_kernel',
     'head': 'head_kernel', 'fc1_dx': 'fc1_dx_kernel',
+    'head+fc1_dx': 'head_dx_kernel',
     'conv3_dx+fc1_dw': 'bwd_b_kernel', 'conv2_dx+conv3_dw': 'bwd_c_kernel',
     'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 'bwd_bc_kernel',
     'conv1_dw+conv2_dw': 'bwd_d_kernel', ALL_BWD: 'bwd_bc_kernel',

@@ -26,6 +26,8 @@ PHASE_NAMES = (
 # is a launch of its own, and of the late-dW layout (DQZ_DW_LATE=1), where
 # phase 8 is.
 PHASE6_SPLIT = 'conv3_dx+fc1_dw'
+# Phase 4 when the head and fc1 dX are one launch (DQZ_FUSED_HEAD=1).
+PHASE4_FUSED = 'head+fc1_dx'
 PHASE6_LATE_DW = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw'
 FRAME_H = 84
 FRAME_W = 84

@@ -3,6 +3,7 @@
 #include "common.hpp"
 #include "conv1.hpp"
 #include "fwd.hpp"
+#include "head.hpp"
 
 namespace dqz {
 
@@ -784,6 +785,112 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
     if (g < W2P_N) a.w2p[g] = v2;
   }
   DQZ_STAMP(5, 3);
+}
+
+// ---- head + fc1 dX in one launch ---------------------------------------------
+// head_dx_kernel: grid [B head blocks][FLAT / 32 fc1 dX blocks], 512 threads.
+// The head blocks run head_body with dz1 published (write-through stores,
+// then one arrival each on Handoff word 0).  A dX block owns 32 rows of W1:
+// waves 0-3 rows [k0, k0 + 16), waves 4-7 rows [k0 + 16, k0 + 32), wave
+// w & 3 one 128-wide quarter of the hidden units, so every dy3 element is the
+// same MFMA chain and the same four-way sum as in fc1_dx_kernel (bit-exact).
+// What does not depend on dz1 (the block's W1 rows, the dX-ordered W3 / W2
+// copies) is loaded before the block waits for the B arrivals; dz1 is then
+// loaded sc1.  Head blocks never wait and precede every dX block in dispatch
+// order, so the wait terminates.  Saves one kernel boundary and moves the W1
+// fetch of fc1 dX under the head.
+constexpr int HDX_ROWS = 32, HDX_BLOCKS = FLAT / HDX_ROWS;  // 98
+constexpr int HDX_SMEM = 32 * FC1B_LD + 2 * 4 * 2 * 256;   // dz1 chunk + dX partials of both row groups
+
+template <int AMAX>
+__global__ __launch_bounds__(512) void head_dx_kernel(HeadArgs h, Fc1BwdArgs a, Handoff hand) {
+  if ((int)blockIdx.x < h.B) {
+    head_body<AMAX, 7, true>(h, blockIdx.x, hand);
+    return;
+  }
+  DQZ_STAMP(5, 0);
+  __shared__ __attribute__((aligned(16))) float smem[HDX_SMEM];
+  float* s_dz = smem;
+  float(*s_red)[4][2][256] = reinterpret_cast<float(*)[4][2][256]>(smem + 32 * FC1B_LD);
+  const int blk = blockIdx.x - h.B;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wq = w & 3, rg = w >> 2, tt = t & 255;
+  const int n = lane & 15, kq = lane >> 4;
+  const int k0 = HDX_ROWS * blk + 16 * rg;  // first W1 row of this thread's row group
+  // W3 / W2 dX copies: element g of the 69,632 is thread g of the dX range
+  const int g = blk * 512 + t;
+  float v3 = 0.f, v2 = 0.f;
+  if (a.w3p) {
+    if (g < W3P_N) v3 = a.w3[w3p_src(g)];
+    if (g < W2P_N) v2 = a.w2[w2p_src(g)];
+  }
+  const float* W1 = a.th + a.w_off;
+  float4 wv[8];  // dX B operand: W1[k0 + n][128 wq + 16 j + 4 kq + e]
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * wq + 16 * j + 4 * kq);
+  hand.wait(0);
+  DQZ_STAMP(5, 1);
+  const float4* dz4 = reinterpret_cast<const float4*>(a.dz1);
+  const int dz_bytes = a.B * HID * 4;
+  for (int c = 0; c < a.B; c += 32) {
+    if (c > 0) __syncthreads();  // previous chunk's s_dz / s_red readers are done
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = t + 512 * i, row = f >> 7;
+      const float4 x = load_sc1_f4(dz4, dz_bytes, min(c + row, a.B - 1) * (HID / 4) + (f & 127));
+      v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float ym[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      ym[hh] = a.y3[(int64_t)min(c + 16 * hh + (tt >> 4), a.B - 1) * FLAT + k0 + (tt & 15)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = t + 512 * i;
+      *reinterpret_cast<float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127)) = v[i];
+    }
+    __syncthreads();
+    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const float* d = s_dz + (16 * mt + n) * FC1B_LD + 128 * wq + 4 * kq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
+        xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
+        xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
+        xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
+        xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_red[rg][wq][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
+    __syncthreads();
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int sample = c + 16 * hh + (tt >> 4);
+      const float s = (s_red[rg][0][hh][tt] + s_red[rg][1][hh][tt]) + (s_red[rg][2][hh][tt] + s_red[rg][3][hh][tt]);
+      if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (tt & 15)] = ym[hh] > 0.f ? s : 0.f;
+    }
+  }
+  if (a.w3p) {
+    if (g < W3P_N) a.w3p[g] = v3;
+    if (g < W2P_N) a.w2p[g] = v2;
+  }
+  DQZ_STAMP(5, 3);
+}
+
+inline hipError_t launch_head_dx(const HeadArgs& h, const Fc1BwdArgs& f, const Handoff& hand, hipStream_t st) {
+  if (h.S > 7) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(h.B + HDX_BLOCKS));
+  if (h.A <= 8)
+    hipLaunchKernelGGL((head_dx_kernel<8>), grid, dim3(HID), 0, st, h, f, hand);
+  else
+    hipLaunchKernelGGL((head_dx_kernel<MAXA>), grid, dim3(HID), 0, st, h, f, hand);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void bwd_b_kernel(Conv3BwdArgs c3, Fc1BwdArgs f1) {

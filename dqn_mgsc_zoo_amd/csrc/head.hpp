@@ -66,14 +66,17 @@ __device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double e
 //   the cotangent at td is clip(w td / B, +-bound) because rlax.clip_gradient
 //   clips the incoming gradient; dq[b, a_b] = -that; dz1 = dq W2[:, a_b] relu'.
 // Cross-sample sums (fc2/fc1-bias grads, mean loss) happen in update_kernel.
-template <int AMAX, int SMAX>
-__global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
+// PUB (head_dx_kernel): dz1 is handed to the fc1 dX blocks of the same launch
+// — its stores are write-through (agent-scope relaxed atomic stores) and the
+// block arrives on the batch counter `pub` (common.hpp Handoff, word 0).
+template <int AMAX, int SMAX, bool PUB>
+__device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handoff& pub) {
   DQZ_STAMP(4, 0);
   __shared__ float s_red[8][3 * AMAX];
   __shared__ float s_q[3][AMAX];
   __shared__ float s_g;
   __shared__ int s_a;
-  const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = n >> 6;
+  const int n = threadIdx.x, lane = n & 63, wave = n >> 6;
   const int A = h.A, B = h.B, Z = h.Z, S = h.S;
   // Every global load is issued up front: the batch record chain
   // (slot -> action/reward/discount), the Z x S fc1 partials, fc1 biases,
@@ -182,7 +185,13 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
 #pragma unroll
     for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
     DQZ_STAMP(4, 2);
-    h.dz1[(int64_t)b * HID + n] = hz[0] > 0.f ? s_g * wv : 0.f;
+    const float dz = hz[0] > 0.f ? s_g * wv : 0.f;
+    if constexpr (PUB) {
+      __hip_atomic_store(h.dz1 + (int64_t)b * HID + n, dz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pub.arrive(0);
+    } else {
+      h.dz1[(int64_t)b * HID + n] = dz;
+    }
   } else if (h.act_out) {  // actor: eps-greedy draw b of call act_ctr
     __syncthreads();
     if (n == 0) {
@@ -201,6 +210,11 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   if (h.advance && b == 0 && n == 0)
     __hip_atomic_fetch_add(h.advance, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   DQZ_STAMP(4, 3);
+}
+
+template <int AMAX, int SMAX>
+__global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
+  head_body<AMAX, SMAX, false>(h, blockIdx.x, Handoff{});
 }
 
 // Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.

@@ -6,6 +6,8 @@
 //   1 conv2 fwd  2 conv3 fwd  3 fc1 fwd (split-K)                fwd.hpp
 //   4 head: fc1 reduce + fc2 + TD loss + dq + dz1, per sample    head.hpp
 //   5 fc1 dX -> dy3                                              bwd.hpp
+//     (DQZ_FUSED_HEAD=1: 4 + 5 as one launch with an in-launch dz1 hand-off,
+//     head_dx_kernel; measured slower)
 //   6 {conv3 dX -> dy2, fc1 dW + fused RMSProp}                  bwd_b_kernel
 //   7 {conv2 dX (stride-phase split) -> dy1, conv3 dW partials}  bwd_c_kernel
 //   8 {conv1 dW partials (frame gather fused), conv2 dW partials} bwd_d_kernel
@@ -60,6 +62,7 @@ struct dqz_learner {
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   int fused_bwd;  // 1: bwd_bc_kernel (+ bwd_d_kernel if dw_late); 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
   int dw_late;    // 1: conv1 / conv2 dW in bwd_d_kernel after the merged launch (DQZ_DW_LATE=1)
+  int fused_head;  // 1: head + fc1 dX in one launch (head_dx_kernel, DQZ_FUSED_HEAD=1, measured 2-3 % slower); 0: two launches
   int fused_fwd;  // 1: fwd_conv_kernel (DQZ_FUSED_FWD=1, measured 1.5 % slower); 0: conv1 / conv2 / conv3 launches
   void* block;
 };
@@ -106,6 +109,8 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
     L->fused_bwd = !(e && e[0] == '0');
     e = getenv("DQZ_DW_LATE");
     L->dw_late = e && e[0] == '1';
+    e = getenv("DQZ_FUSED_HEAD");
+    L->fused_head = e && e[0] == '1';
     e = getenv("DQZ_FUSED_FWD");
     L->fused_fwd = e && e[0] == '1';
   }
@@ -120,7 +125,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, 16 * B * Handoff::kStride + 64, W3P_N, W2P_N};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p};
@@ -331,10 +336,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.gq = L->gq;
   h.ga = L->ga;
   h.dz1 = L->dz1;
-  DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
 
-  // Backward: fc1 dX, then three launches that each pair the next dX job set
-  // of the critical path with an independent dW job set (bwd.hpp).
+  // Backward: fc1 dX (in the head's launch), then the merged launch that pairs
+  // the dX chain with the independent dW job sets (bwd.hpp).
   Fc1BwdArgs fb;
   fb.dz1 = L->dz1;
   fb.y3 = L->y3;
@@ -349,8 +353,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w2 = P->online + L->off[2];
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
-  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
-            DQZ_HIP(hipGetLastError()));
+  if (L->fused_head) {
+    // dz1 hand-off words: err at 16B, batch counter at 16B + 1, ack at 16B + 2 (x kStride)
+    int* const hw = L->sync + 16 * B * Handoff::kStride;
+    const Handoff hand{hw + Handoff::kStride, hw + 2 * Handoff::kStride, hw, B, HDX_BLOCKS};
+    DQZ_PHASE(4, DQZ_HIP(launch_head_dx(h, fb, hand, st)));
+    if (pe.on()) pe.ms[5] = 0.f;
+  } else {
+    DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
+    DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+              DQZ_HIP(hipGetLastError()));
+  }
 
   Conv3BwdArgs c3b;
   c3b.dy3 = L->dy3;

@@ -152,6 +152,8 @@ class Learner:
         _native.stream_handle(stream)))
     ms = [float(x) for x in out]
     names = list(_native.PHASE_NAMES)
+    if ms[5] == 0.0:  # head and fc1 dX as one launch
+      names[4] = _native.PHASE4_FUSED
     if ms[7] > 0.0:  # split-backward layout: phase 6 is conv3 dX + fc1 dW only
       names[6] = _native.PHASE6_SPLIT
     elif ms[8] > 0.0:  # late-dW layout: conv2 / conv1 dW in a launch of their own

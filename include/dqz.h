@@ -135,7 +135,9 @@ int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_s
 /* Phases of one learner step, in launch order (dqz_learner_profile):
  *  0 conv1 fwd (uniform draw + frame gather fused)   1 conv2 fwd
  *  2 conv3 fwd   3 fc1 fwd (split-K)
- *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample)
+ *  4 head: fc1 reduce + fc2 + TD loss + dq + dz1 (one workgroup per sample);
+ *    with DQZ_FUSED_HEAD=1 also fc1 dX behind an in-launch dz1 hand-off
+ *    (one launch, head_dx_kernel) and 5 reports 0
  *  5 fc1 dX
  *  6 conv3 dX -> conv2 dX -> conv1 dW and conv3 dX -> conv2 dW (in-launch
  *    per-sample hand-offs of dy2 / dy1) + fc1 dW and RMSProp of fc1/w +

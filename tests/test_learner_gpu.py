@@ -226,16 +226,19 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
 @pytest.mark.parametrize('algo,batch,dw_late', [('dqn', 32, False), ('per', 20, False),
                                                 ('double', 64, False), ('dqn', 32, True)])
 def test_fused_handoff_kernels_bit_exact(device, algo, batch, dw_late, monkeypatch):
-  """fwd_conv_kernel (conv1 -> conv2 -> conv3 hand-offs) and bwd_bc_kernel
+  """fwd_conv_kernel (conv1 -> conv2 -> conv3 hand-offs), head_dx_kernel
+  (head -> fc1 dX hand-off of dz1) and bwd_bc_kernel
   (conv3 dX -> conv2 dX / conv2 dW, conv2 dX -> conv1 dW hand-offs; or with
   the dW jobs in bwd_d_kernel) give the same bits as the separate launches,
   over many steps, under hipGraph replay and after profile-mode repeated
   launches."""
   monkeypatch.setenv('DQZ_FUSED_BWD', '0')
   monkeypatch.setenv('DQZ_FUSED_FWD', '0')
+  monkeypatch.setenv('DQZ_FUSED_HEAD', '0')
   _, ref, st, _, _, _, _, _ = _setup(algo, batch, seed=21)
   monkeypatch.setenv('DQZ_FUSED_BWD', '1')
   monkeypatch.setenv('DQZ_FUSED_FWD', '1')
+  monkeypatch.setenv('DQZ_FUSED_HEAD', '1')
   monkeypatch.setenv('DQZ_DW_LATE', '1' if dw_late else '0')
   _, lrn, _, _, _, _, _, _ = _setup(algo, batch, seed=21)
   rng = np.random.default_rng(22)
