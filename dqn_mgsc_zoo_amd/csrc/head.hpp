@@ -101,9 +101,22 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) w2v[z][a] = w2[min(a, A - 1)];
   }
-  float b2v = 0.f;  // fc2 bias of output (z, a) = (n / AMAX, n % AMAX)
-  if (n < 3 * AMAX) {
-    const int zc = min(n / AMAX, Z - 1), a = min(n % AMAX, A - 1);
+  // fc2 (q = h1 W2 + b2).  AMAX <= 8: an LDS transpose-reduce — thread n
+  // writes its K = Z A products h1[z][n] W2[n][a] to s_p[k = z A + a][n];
+  // output k is summed by T adjacent lanes (T = 32 for K <= 16, else 16),
+  // 512 / T terms each in a fixed order, then a butterfly over the T lanes:
+  // one reduction chain per lane instead of one full-wave chain per output.
+  // Larger action sets keep per-output wave sums.
+  constexpr bool kTr = AMAX <= 8;
+  constexpr int kPS = HID + 16;  // s_p row stride: rows of adjacent 16-lane groups 16 banks apart
+  __shared__ float s_p[kTr ? 3 * AMAX : 1][kTr ? kPS : 1];
+  const int K = Z * A, lgT = K <= 16 ? 5 : 4, T = 1 << lgT;
+  const int kk = n >> lgT, jj = n & (T - 1);
+  const bool qthread = kTr ? (kk < K && jj == 0) : (n < 3 * AMAX && n / AMAX < Z && n % AMAX < A);
+  const int zq = kTr ? min(kk / A, 2) : n / AMAX, aq = kTr ? kk % A : n % AMAX;  // output of this q thread
+  float b2v = 0.f;  // fc2 bias of output (zq, aq)
+  if (kTr ? kk < K : n < 3 * AMAX) {
+    const int zc = min(zq, Z - 1), a = min(aq, A - 1);
     b2v = h.nz.p[zc][h.b2_off + (h.shared_bias ? 0 : a)];
   }
   if (!h.fwd_only && n == 0) {  // second hop of the batch record chain, needed only for the TD
@@ -129,39 +142,74 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
       for (int s = 0; s < SMAX; ++s) acc += s < S ? pv[z][s] : 0.f;
       hz[z] = relu(acc);
       if (z == 0) DQZ_STAMP(15, 0);  // fc1 partials of copy 0 have landed
+      if constexpr (kTr) {
 #pragma unroll
-      for (int a = 0; a < AMAX; ++a) {
-        const float sa = wave_sum(hz[z] * w2v[z][a]);
-        if (lane == 0) s_red[wave][z * AMAX + a] = sa;
+        for (int a = 0; a < AMAX; ++a)
+          if (a < A) s_p[z * A + a][n] = hz[z] * w2v[z][a];
+      } else {
+#pragma unroll
+        for (int a = 0; a < AMAX; ++a) {
+          const float sa = wave_sum(hz[z] * w2v[z][a]);
+          if (lane == 0) s_red[wave][z * AMAX + a] = sa;
+        }
       }
     }
   }
-  DQZ_STAMP(15, 1);  // wave sums done
+  DQZ_STAMP(15, 1);  // products / wave sums done
   __syncthreads();
   float qv = 0.f;
-  const bool qthread = n < 3 * AMAX && n / AMAX < Z && n % AMAX < A;
-  if (qthread) {
+  if constexpr (kTr) {
+    if (kk < K) {  // every lane of output kk's group
+      const float* row = &s_p[kk][jj];
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < (HID >> lgT); i += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a4[u] += row[(i + u) << lgT];
+      }
+      float v = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      qv = v + b2v;
+      if (jj == 0) s_q[zq][aq] = qv;
+    }
+  } else if (qthread) {
     float sa = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) sa += s_red[ww][n];
     qv = sa + b2v;
-    s_q[n / AMAX][n % AMAX] = qv;
+    s_q[zq][aq] = qv;
   }
   if (!h.fwd_only) {
     __syncthreads();
     DQZ_STAMP(15, 2);  // q values in LDS
     if (n == 0) {
-      float v;
+      float q0[AMAX], q1[AMAX], q2[AMAX];  // every LDS read issued before the first use
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a) {
+        q0[a] = s_q[0][min(a, A - 1)];
+        q1[a] = s_q[1][min(a, A - 1)];
+        q2[a] = s_q[min(2, Z - 1)][min(a, A - 1)];
+      }
+      float v, qa = q0[0];
+#pragma unroll
+      for (int a = 1; a < AMAX; ++a) qa = a == a_tm1 ? q0[a] : qa;
       if (h.algo == DQZ_ALGO_DQN) {
-        v = s_q[1][0];
-        for (int a = 1; a < A; ++a) v = fmaxf(v, s_q[1][a]);
+        v = q1[0];
+#pragma unroll
+        for (int a = 1; a < AMAX; ++a) v = fmaxf(v, q1[a]);  // entries past A repeat q1[A - 1]
       } else {
         int am = 0;  // online Q(s_t) selects, jnp.argmax: first maximum
-        for (int a = 1; a < A; ++a)
-          if (s_q[2][a] > s_q[2][am]) am = a;
-        v = s_q[1][am];
+        float best = q2[0];
+#pragma unroll
+        for (int a = 1; a < AMAX; ++a)
+          if (a < A && q2[a] > best) {
+            best = q2[a];
+            am = a;
+          }
+        v = q1[0];
+#pragma unroll
+        for (int a = 1; a < AMAX; ++a) v = a == am ? q1[a] : v;
       }
-      const float td = (r + d * v) - s_q[0][a_tm1];
+      const float td = (r + d * v) - qa;
       float g;
       if (h.unit) {
         g = -1.f;  // gq = d q[a] / d q[a] = 1
@@ -205,7 +253,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
 #pragma unroll
   for (int z = 0; z < 3; ++z)
     if (z < Z) h.h1[((int64_t)z * B + b) * HID + n] = hz[z];
-  if (qthread) h.q[((int64_t)(n / AMAX) * B + b) * A + n % AMAX] = qv;
+  if (qthread) h.q[((int64_t)zq * B + b) * A + aq] = qv;
   // the fused sampler's step counter: every conv1 block of this step has read it
   if (h.advance && b == 0 && n == 0)
     __hip_atomic_fetch_add(h.advance, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
