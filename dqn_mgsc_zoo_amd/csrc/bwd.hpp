@@ -192,17 +192,10 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
       *reinterpret_cast<float4*>(R.gout + e) = g;
     } else {
       float4 th4 = o_th[i], mu4 = o_mu[i], nu4 = o_nu[i];
-      auto one = [&](float gg, float& th, float& mu, float& nu) {
-        const float m = R.c1 * gg + R.decay * mu;
-        const float v = R.c1 * (gg * gg) + R.decay * nu;
-        mu = m;
-        nu = v;
-        th = th + (-R.lr) * (gg * rsqrtf(v - m * m + R.eps));
-      };
-      one(g.x, th4.x, mu4.x, nu4.x);
-      one(g.y, th4.y, mu4.y, nu4.y);
-      one(g.z, th4.z, mu4.z, nu4.z);
-      one(g.w, th4.w, mu4.w, nu4.w);
+      R.step(g.x, th4.x, mu4.x, nu4.x);
+      R.step(g.y, th4.y, mu4.y, nu4.y);
+      R.step(g.z, th4.z, mu4.z, nu4.z);
+      R.step(g.w, th4.w, mu4.w, nu4.w);
       *reinterpret_cast<float4*>(a.th + e) = th4;
       *reinterpret_cast<float4*>(a.mu + e) = mu4;
       *reinterpret_cast<float4*>(a.nu + e) = nu4;
@@ -744,13 +737,11 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
       }
       *reinterpret_cast<float4*>(R.gout + e) = o;
     } else {
-      float4 m, vv, th;
-#define DQZ_RMS1(X)                                            \
-  m.X = R.c1 * g.X + R.decay * o_mu[h].X;                      \
-  vv.X = R.c1 * (g.X * g.X) + R.decay * o_nu[h].X;             \
-  th.X = o_th[h].X + (-R.lr) * (g.X * rsqrtf(vv.X - m.X * m.X + R.eps));
-      DQZ_RMS1(x) DQZ_RMS1(y) DQZ_RMS1(z) DQZ_RMS1(w)
-#undef DQZ_RMS1
+      float4 m = o_mu[h], vv = o_nu[h], th = o_th[h];
+      R.step(g.x, th.x, m.x, vv.x);
+      R.step(g.y, th.y, m.y, vv.y);
+      R.step(g.z, th.z, m.z, vv.z);
+      R.step(g.w, th.w, m.w, vv.w);
       *reinterpret_cast<float4*>(a.mu + e) = m;
       *reinterpret_cast<float4*>(a.nu + e) = vv;
       *reinterpret_cast<float4*>(a.th + e) = th;

@@ -88,16 +88,26 @@ struct Rms {
   float lr, decay, c1, eps;
   float* gout;
   int gacc;  // gradient-output mode: 1 adds into gout (meta-batch chunks), 0 overwrites
+  // One centered RMSProp step (optax 0.1.2 scale_by_stddev, eps inside the
+  // sqrt).  Every multiply-add is an explicit fma: hipcc contracts a*b + c*d
+  // either way round depending on the surrounding code, and fc1/w is updated
+  // by this function in different kernels of the launch layouts, which must
+  // agree bit for bit.
+  __device__ __forceinline__ void step(float g, float& th, float& mu, float& nu) const {
+    mu = __fmaf_rn(c1, g, decay * mu);
+    nu = __fmaf_rn(c1, g * g, decay * nu);
+    th = __fmaf_rn(-lr, g * rsqrtf(__fmaf_rn(-mu, mu, nu) + eps), th);
+  }
   __device__ __forceinline__ void apply(float* th, float* mu, float* nu, int64_t i, float g) const {
     if (gout) {
       gout[i] = gacc ? gout[i] + g : g;
       return;
     }
-    const float m = c1 * g + decay * mu[i];
-    const float v = c1 * (g * g) + decay * nu[i];
+    float t = th[i], m = mu[i], v = nu[i];
+    step(g, t, m, v);
     mu[i] = m;
     nu[i] = v;
-    th[i] = th[i] + (-lr) * (g * rsqrtf(v - m * m + eps));
+    th[i] = t;
   }
 };
 

@@ -209,7 +209,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
 #pragma unroll
         for (int a = 1; a < AMAX; ++a) v = a == am ? q1[a] : v;
       }
-      const float td = (r + d * v) - qa;
+      const float td = __fmaf_rn(d, v, r) - qa;  // explicit fma: the same bits in every kernel using head_body
       float g;
       if (h.unit) {
         g = -1.f;  // gq = d q[a] / d q[a] = 1
@@ -423,11 +423,11 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
       if (R.gout) {
         R.gout[i] = R.gacc ? R.gout[i] + gv[h] : gv[h];
       } else {
-        const float m = R.c1 * gv[h] + R.decay * o_mu[h];
-        const float v = R.c1 * (gv[h] * gv[h]) + R.decay * o_nu[h];
+        float t = o_th[h], m = o_mu[h], v = o_nu[h];
+        R.step(gv[h], t, m, v);
         u.mu[i] = m;
         u.nu[i] = v;
-        u.th[i] = o_th[h] + (-R.lr) * (gv[h] * rsqrtf(v - m * m + R.eps));
+        u.th[i] = t;
       }
     }
   }
