@@ -578,6 +578,16 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
     const int oh = i / (C1O * 8), rem = i % (C1O * 8);  // 8 float4 per pixel
     r[q] = src[((2 * oh + kh) * C1O) * 8 + rem];
   }
+  // the y1 rows go to LDS before the wait: held in registers across the spin
+  // loop they were kept in scratch (112 bytes per lane, stored and reloaded)
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NV4) {
+      const int oh = i / (C1O * 8), rem = i % (C1O * 8), iw = rem >> 3;
+      *reinterpret_cast<float4*>(s_win + oh * C2W_RS + iw * C2W_S + (rem & 7) * 4) = r[q];
+    }
+  }
   a.sync.wait(b);
   float dr[21][2];
 #pragma unroll
@@ -588,14 +598,6 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
       const float* g = a.dy2 + ((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 32 * ch + 16 * ct + n;
       const float v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dr[kk][ct] = p < C2M ? v : 0.f;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    const int i = t + 256 * q;
-    if (i < NV4) {
-      const int oh = i / (C1O * 8), rem = i % (C1O * 8), iw = rem >> 3;
-      *reinterpret_cast<float4*>(s_win + oh * C2W_RS + iw * C2W_S + (rem & 7) * 4) = r[q];
     }
   }
   __syncthreads();
