@@ -1,14 +1,17 @@
 """Learner grad-steps/s at batch 32 on synthetic 84x84x4 uint8 replay.
 
-`python bench.py --gpus N --steps K --warmup W` (N>1 under
-torch.distributed.run, one process per GPU).  A *step* is one pass of the
+`python bench.py --gpus N --steps K --warmup W`: one process per GPU.  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank; without it
+and N > 1, this process starts the N rank processes itself (before touching
+the GPU) and exits with the worst of their exit codes.  A *step* is one pass of the
 hot path on device: uniform sample of 32 slots from a 1M-transition frame
 replay (Philox on device) -> frame gather + /255 fused into conv1 ->
 NatureQNetwork forward of online(s_tm1) and target(s_t) -> q_learning TD
 loss with clip_gradient -> backward -> centered RMSProp; the target copy
 runs every 2,500 steps (40,000 frames / learn_period 16) inside the timed
 loop.  Replicas are independent seeds (no gradient all-reduce); RCCL only
-all-gathers per-rank statistics after the timed region.
+all-gathers a per-rank statistics vector every 1,000 steps (SURVEY.md §8(d)
+config 4) and after the timed region.
 
 Prints ONE JSON line on rank 0.
 """
@@ -16,6 +19,8 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -142,39 +147,165 @@ def pmc_traffic(phase):
 
 
 def cpu_baseline(seconds, algo):
-  """Times the oracle's fp64 learner step (a CPU *port*) on this host."""
-  from threadpoolctl import threadpool_info, threadpool_limits  # pylint: disable=g-import-not-at-top
-  from oracle import learner_ref  # pylint: disable=g-import-not-at-top
+  """torch-CPU fp32 learner step on this host's cores.
+
+  The reference's --jax_platform_name=cpu path cannot run (no JAX stack), so
+  the same update is timed as an fp32 torch-CPU port (`oracle/torch_cpu.py`,
+  pinned to the fp64 oracle by tests/test_oracle.py) at every thread this
+  process is allotted and at 2 threads (run_dqn_normal.sh:9
+  --cpus-per-task=2), about seconds/2 each.
+  """
+  from oracle import torch_cpu  # pylint: disable=g-import-not-at-top
   from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
-  threads = min(16, os.cpu_count() or 1)
   net = (networks.dqn_atari_network(NUM_ACTIONS) if algo == 'dqn' else
          networks.double_dqn_atari_network(NUM_ACTIONS))
-  rng = np.random.default_rng(0)
-  params = net.init(0)
-  mu = learner_ref.zeros_like_tree(params)
-  nu = learner_ref.zeros_like_tree(params)
-  with threadpool_limits(limits=threads):
-    blas = [i.get('num_threads') for i in threadpool_info()]
-    used = max([t for t in blas if t] + [1])
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-      s_tm1 = rng.integers(0, 256, (BATCH, 84, 84, 4), dtype=np.uint8)
-      s_t = rng.integers(0, 256, (BATCH, 84, 84, 4), dtype=np.uint8)
-      a = rng.integers(0, NUM_ACTIONS, BATCH)
-      r = rng.choice([-1.0, 0.0, 1.0], BATCH, p=[0.01, 0.98, 0.01])
-      d = np.full(BATCH, 0.99)
-      out = learner_ref.learner_step(params, params, mu, nu, s_tm1, a, r, d,
-                                     s_t, algo=algo)
-      params, mu, nu = out['params'], out['mu'], out['nu']
+  allotted = int(os.environ.get('OMP_NUM_THREADS', '0') or 0)
+  if allotted <= 0:
+    allotted = len(os.sched_getaffinity(0))
+  prev = torch.get_num_threads()
+  gen = torch.Generator().manual_seed(0)
+  rates = {}
+  samples = {}
+  for threads in (allotted, 2):
+    torch.set_num_threads(threads)
+    lrn = torch_cpu.TorchCpuLearner(net.init(0), algo=algo)
+    n, t0 = 0, None
+    while True:
+      s_tm1 = torch.randint(0, 256, (BATCH, 84, 84, 4), generator=gen, dtype=torch.uint8)
+      s_t = torch.randint(0, 256, (BATCH, 84, 84, 4), generator=gen, dtype=torch.uint8)
+      a = torch.randint(0, NUM_ACTIONS, (BATCH,), generator=gen)
+      r = torch.zeros(BATCH)
+      d = torch.full((BATCH,), 0.99)
+      lrn.step(s_tm1, a, r, d, s_t)
+      if t0 is None:  # the first step pays one-off allocation; not timed
+        t0 = time.perf_counter()
+        continue
       n += 1
-    dt = time.perf_counter() - t0
-  return {'value': n / dt, 'unit': 'steps/s', 'cores': used, 'kind': 'port',
-          'sample': '%d oracle fp64 numpy learner steps (B=32, 84x84x4 uint8, '
-                    '%s) in %.1f s, BLAS threads=%d' % (n, algo, dt, used)}
+      dt = time.perf_counter() - t0
+      if dt >= seconds / 2 and n >= 2:
+        break
+    rates[threads] = n / dt
+    samples[threads] = '%d steps in %.1f s' % (n, dt)
+  torch.set_num_threads(prev)
+  return {'value': round(rates[allotted], 3), 'unit': 'steps/s',
+          'cores': allotted, 'kind': 'port',
+          'value_2_threads': round(rates[2], 3),
+          'sample': 'torch-CPU fp32 learner update (oracle/torch_cpu.py: %s, '
+                    'B=32, 84x84x4 uint8, A=%d, centered RMSProp), one '
+                    'untimed step then %s at %d threads; %s at 2 threads '
+                    '(run_dqn_normal.sh:9 --cpus-per-task=2)' % (
+                        algo, NUM_ACTIONS, samples[allotted], allotted,
+                        samples[2])}
 
 
-def main():
+def plan_chunks(steps, graph_steps, use_graph):
+  """Graph sizes (g, rem) so that the timed steps are EXACTLY `steps`.
+
+  `steps // g` replays of a g-step graph then, if rem > 0, one replay of a
+  rem-step graph; g = 1 and rem = 0 means eager launches.
+  """
+  if steps < 1:
+    raise ValueError('--steps must be >= 1, got %d' % steps)
+  if not use_graph:
+    return 1, 0
+  if graph_steps < 1:
+    raise ValueError('--graph-steps must be >= 1')
+  g = min(graph_steps, steps)
+  return g, steps % g
+
+
+class StepRunner:
+  """Runs `n` learner steps through the captured graphs (or eagerly).
+
+  Host-side bookkeeping between replays: the target hard copy whenever the
+  global step count crosses a multiple of target_period (dqn/agent.py:155-156:
+  the copy follows the learn of that step) and the statistics gather every
+  stats_every steps.
+  """
+
+  def __init__(self, one_step, graphs, target_period, sync_target,
+               stats_every=0, on_stats=None):
+    self.one_step = one_step
+    self.graphs = graphs  # {size: graph}
+    self.target_period = target_period
+    self.sync_target = sync_target
+    self.stats_every = stats_every
+    self.on_stats = on_stats
+    self.done = 0
+
+  def _advance(self, k):
+    before, self.done = self.done, self.done + k
+    if self.done // self.target_period > before // self.target_period:
+      self.sync_target()
+    if self.stats_every and self.on_stats is not None and (
+        self.done // self.stats_every > before // self.stats_every):
+      self.on_stats(self.done)
+
+  def run(self, n, g, rem):
+    """n == reps * g + rem steps: full graphs first, then the remainder."""
+    i = 0
+    while i < n:
+      left = n - i
+      if g > 1 and left >= g:
+        self.graphs[g].replay()
+        k = g
+      elif rem > 1 and left == rem:
+        self.graphs[rem].replay()
+        k = rem
+      else:
+        self.one_step()
+        k = 1
+      i += k
+      self._advance(k)
+    return i
+
+
+def free_port():
+  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+    s.bind(('127.0.0.1', 0))
+    return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+  """Starts n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE set,
+  rendezvous on 127.0.0.1) and returns the worst exit code.  Called before
+  anything touches the GPU; children are started, never exec'd into."""
+  port = free_port()
+  procs = []
+  for r in range(n):
+    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(port))
+    procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] +
+                                  list(argv), env=env))
+  rcs = [None] * n
+  while any(rc is None for rc in rcs):
+    for i, p in enumerate(procs):
+      if rcs[i] is None:
+        rcs[i] = p.poll()
+    bad = [rc for rc in rcs if rc not in (None, 0)]
+    if bad:  # one rank failed: the others would wait forever at a collective
+      for i, p in enumerate(procs):
+        if rcs[i] is None:
+          p.terminate()
+      for i, p in enumerate(procs):
+        if rcs[i] is None:
+          try:
+            rcs[i] = p.wait(timeout=30)
+          except subprocess.TimeoutExpired:
+            p.kill()
+            rcs[i] = p.wait()
+      break
+    time.sleep(0.05)
+  worst = 0
+  for rc in rcs:
+    if rc != 0:
+      worst = rc if rc > 0 else 1
+      break
+  return worst
+
+
+def parse_args(argv=None):
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=5000)
@@ -184,15 +315,112 @@ def main():
   ap.add_argument('--graph', type=int, default=1, help='hipGraph-replay steps')
   ap.add_argument('--graph-steps', type=int, default=50)
   ap.add_argument('--target-period', type=int, default=2500)
+  ap.add_argument('--stats-every', type=int, default=1000)
   ap.add_argument('--profile-iters', type=int, default=100)
-  ap.add_argument('--cpu-seconds', type=float, default=15.0)
-  args = ap.parse_args()
+  ap.add_argument('--cpu-seconds', type=float, default=20.0)
+  ap.add_argument('--selftest-cpu', action='store_true',
+                  help='orchestration self-test on CPU (gloo, no GPU, a '
+                       'stand-in step): exercises rank launch, timing and '
+                       'the statistics gathers only')
+  return ap.parse_args(argv)
 
+
+def main(argv=None):
+  argv = sys.argv[1:] if argv is None else argv
+  args = parse_args(argv)
+  if args.gpus < 1:
+    print('--gpus must be >= 1', file=sys.stderr)
+    return 2
+  if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+    return spawn_ranks(args.gpus, argv)
+  world_env = int(os.environ.get('WORLD_SIZE', '1'))
+  if world_env != args.gpus:
+    print('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world_env),
+          file=sys.stderr)
+    return 2
+  try:
+    g, rem = plan_chunks(args.steps, args.graph_steps, bool(args.graph))
+  except ValueError as e:
+    print('bench.py: %s' % e, file=sys.stderr)
+    return 2
+  if args.selftest_cpu:
+    return selftest_cpu(args, g, rem)
+  return run_gpu(args, g, rem)
+
+
+def _timed(reps, runner, steps, g, rem, sync):
+  reps.barrier()
+  sync()
+  t0 = time.perf_counter()
+  n = runner.run(steps, g, rem)
+  sync()
+  elapsed = time.perf_counter() - t0
+  reps.barrier()
+  if n != steps:
+    raise RuntimeError('timed %d steps, asked for %d' % (n, steps))
+  return elapsed
+
+
+def selftest_cpu(args, g, rem):
+  """The orchestration of run_gpu with a CPU stand-in step (tests only)."""
+  from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
+  reps = replicas_lib.Replicas('gloo')
+  x = torch.ones((64, 64))
+  counters = {'steps': 0, 'syncs': 0, 'gathers': 0}
+
+  def one_step():
+    x.copy_(torch.tanh(x @ x / 64.0))
+    counters['steps'] += 1
+
+  class _Graph:  # stand-in for a captured k-step graph
+    def __init__(self, k):
+      self.k = k
+
+    def replay(self):
+      for _ in range(self.k):
+        one_step()
+
+  def sync_target():
+    counters['syncs'] += 1
+
+  def on_stats(done):
+    reps.gather_stats([float(done), float(x[0, 0])])
+    counters['gathers'] += 1
+
+  graphs = {k: _Graph(k) for k in (g, rem) if k > 1}
+  runner = StepRunner(one_step, graphs, args.target_period, sync_target,
+                      args.stats_every, on_stats)
+  # the timed gathers are collectives: every rank runs the same step counts
+  runner.run(args.warmup, 1, 0)
+  warm = counters['steps']
+  elapsed = _timed(reps, runner, args.steps, g, rem, lambda: None)
+  elapsed_max = reps.max_over_ranks(elapsed)
+  per_rank = reps.gather_stats([counters['steps'] - warm, elapsed,
+                                counters['syncs'], counters['gathers']])
+  if reps.rank == 0:
+    print(json.dumps({
+        'metric': METRIC + ' [CPU orchestration self-test]',
+        'value': round(reps.world * args.steps / elapsed_max, 2),
+        'unit': 'steps/s', 'n_gpus': reps.world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed_max / args.steps,
+        'chunks': [g, rem],
+        'per_rank_steps': [int(v) for v in per_rank[:, 0]],
+        'per_rank_target_syncs': [int(v) for v in per_rank[:, 2]],
+        'per_rank_stats_gathers': [int(v) for v in per_rank[:, 3]]}),
+          flush=True)
+  reps.close()
+  return 0
+
+
+def run_gpu(args, g, rem):
   from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
   torch.cuda.set_device(local_rank)
   reps = replicas_lib.Replicas('nccl')  # RCCL; replicas only, no grad exchange
   world, rank = reps.world, reps.rank
+  if world != args.gpus:
+    print('bench.py: world %d != --gpus %d' % (world, args.gpus), file=sys.stderr)
+    return 2
   dev = torch.device('cuda', local_rank)
 
   from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
@@ -219,8 +447,7 @@ def main():
     lrn.step_uniform(store, 0, args.capacity, args.capacity, seed, counter,
                      slots)
 
-  g = args.graph_steps if args.graph else 1
-  graph = None
+  graphs = {}
   if args.graph:
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -228,54 +455,53 @@ def main():
       for _ in range(3):
         one_step()
     torch.cuda.current_stream(dev).wait_stream(side)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-      for _ in range(g):
-        one_step()
+    for k in sorted({g, rem}):
+      if k > 1:
+        graphs[k] = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graphs[k]):
+          for _ in range(k):
+            one_step()
 
-  def run(n_steps, done):
-    i = 0
-    while i < n_steps:
-      if graph is not None and n_steps - i >= g:
-        graph.replay()
-        k = g
-      else:
-        one_step()
-        k = 1
-      before = done + i
-      i += k
-      # target sync each time the step count crosses a period boundary
-      if (done + i) // args.target_period > before // args.target_period:
-        lrn.sync_target()
-    return done + i
+  # statistics vector [steps done, last loss], all-gathered over RCCL every
+  # stats_every steps (enqueued, never waited on inside the timed region)
+  stats_vec = torch.zeros((2,), dtype=torch.float64, device=dev)
+  gathered = torch.zeros((world, 2), dtype=torch.float64, device=dev)
+  pending = []
 
-  done = run(args.warmup, 0)
-  steps = (args.steps // g) * g if graph is not None else args.steps
-  reps.barrier()
-  torch.cuda.synchronize(dev)
-  ev0 = torch.cuda.Event(enable_timing=True)
-  ev1 = torch.cuda.Event(enable_timing=True)
-  t0 = time.perf_counter()
-  ev0.record()
-  done = run(steps, done)
-  ev1.record()
-  torch.cuda.synchronize(dev)
-  elapsed = time.perf_counter() - t0
-  reps.barrier()
-  gpu_ms = ev0.elapsed_time(ev1)
+  def on_stats(done):
+    lrn.fetch_outputs()
+    stats_vec[0].fill_(float(done))
+    stats_vec[1].copy_(lrn.loss[0])
+    if reps.dist is not None:
+      pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
+                                                      async_op=True))
+
+  runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
+                      args.stats_every, on_stats)
+  runner.run(args.warmup, 1, 0)
+  for k in graphs:  # first replay of each graph uploads it: keep it untimed
+    runner.run(k, k, 0)
+  warm_steps = runner.done
+  elapsed = _timed(reps, runner, args.steps, g, rem,
+                   lambda: torch.cuda.synchronize(dev))
+  steps = args.steps
+  for w in pending:
+    w.wait()
+  status = lrn.sync_status()  # in-launch hand-off health over every step run
   elapsed_max = reps.max_over_ranks(elapsed, device=dev)
-  per_rank = reps.gather_stats([steps / elapsed, elapsed, gpu_ms / 1e3],
-                               device=dev)
+  status_max = reps.max_over_ranks(float(status), device=dev)
+  per_rank = reps.gather_stats([steps / elapsed, elapsed], device=dev)
 
   # Per-phase device time (HIP events on the launch stream) for the roofline.
   phases = lrn.profile(store, slots, iters=args.profile_iters)
   q_tm1, td, loss = lrn.fetch_outputs()
   torch.cuda.synchronize(dev)
   finite = bool(torch.isfinite(lrn.online).all().item())
+  status_after = lrn.sync_status()
 
   if rank != 0:
     reps.close()
-    return
+    return 0 if (status == 0 and status_after == 0) else 3
 
   value = world * steps / elapsed_max
   flops = phase_flops(algo, BATCH)
@@ -318,12 +544,14 @@ def main():
       'dtype': 'f32',
       'data': 'synthetic (uint8 U{0..255} frames, 1000-transition episodes, '
               'random-init NatureQNetwork)',
-      'config': {'workload': 'dqn agent learner-only loop, synthetic 84x84x4 '
-                             'uint8 replay pre-filled to %d, batch=32, A=%d, '
-                             'algo=%s' % (args.capacity, NUM_ACTIONS, algo),
+      'config': {'workload': 'BASELINE config 2: dqn agent learner-only loop, '
+                             'synthetic 84x84x4 uint8 replay pre-filled to %d, '
+                             'batch=32, A=%d, algo=%s' % (
+                                 args.capacity, NUM_ACTIONS, algo),
                  'global_batch': BATCH * world, 'replay_capacity': args.capacity,
                  'parallelism': 'independent-seed replicas x%d' % world,
-                 'hipgraph_steps': g},
+                 'hipgraph_chunks': [g, rem],
+                 'warmup_steps_run': warm_steps},
       'roofline': roof,
       'step_roofline': {
           'achieved_tflops': round(step_tflops, 3),
@@ -333,7 +561,9 @@ def main():
           'flop_per_step': STEP_FLOP[algo], 'bytes_per_step': STEP_BYTES[algo]},
       'phase_ms': {k: round(v, 5) for k, v in phases.items()},
       'per_rank_steps_per_s': [round(float(x), 2) for x in per_rank[:, 0]],
-      'gpu_event_s': round(gpu_ms / 1e3, 4),
+      'per_gpu_min_steps_per_s': round(float(per_rank[:, 0].min()), 2),
+      'stats_gathers': len(pending),
+      'handoff_status': int(max(status_max, status_after)),
       'fill_s': round(t_fill, 2),
       'last_loss': float(loss.item()),
       'params_finite': finite,
@@ -344,7 +574,12 @@ def main():
     out['cpu_baseline'] = None
   print(json.dumps(out), flush=True)
   reps.close()
+  if out['handoff_status'] != 0 or not finite:
+    print('bench.py: hand-off status %d, params finite %s: the timed steps are '
+          'invalid' % (out['handoff_status'], finite), file=sys.stderr)
+    return 3
+  return 0
 
 
 if __name__ == '__main__':
-  main()
+  sys.exit(main())

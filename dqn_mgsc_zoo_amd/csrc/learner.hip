@@ -488,6 +488,15 @@ int dqz_learner_sync_status(dqz_learner* L, int* status) {
   if (!L || !status) return fail(DQZ_ERR_INVALID, "null argument");
   DQZ_HIP(hipDeviceSynchronize());
   DQZ_HIP(hipMemcpy(status, L->sync + 16 * L->cfg.batch * Handoff::kStride, sizeof(int), hipMemcpyDeviceToHost));
+  if (*status != 0) {
+    // A wait gave up: its consumers ran on partial payloads and producers may
+    // have arrived after the last consumer reset the words, which would let
+    // later launches pass their waits early.  Clear every hand-off word (and
+    // the error word) so the next step starts clean; the caller must treat
+    // the steps since the previous check as invalid.
+    DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
+    DQZ_HIP(hipDeviceSynchronize());
+  }
   return DQZ_OK;
 }
 

@@ -165,7 +165,9 @@ int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* lo
 
 /* Health of the in-launch hand-offs of the backward pass: *status = 0 when
  * every wait completed, 1 if a wait gave up (a bounded spin expired; the
- * step's results are then invalid).  Synchronises the device. */
+ * step's results are then invalid).  Synchronises the device.  A non-zero
+ * status also clears every hand-off word, so the next step starts clean;
+ * callers treat the steps since their previous check as invalid. */
 int dqz_learner_sync_status(dqz_learner* learner, int* status);
 
 /* Q-values of the NatureQNetwork for uint8 HWC states [n][84][84][4]

@@ -1,0 +1,99 @@
+"""CPU: bench.py's step arithmetic and rank orchestration (no GPU).
+
+The driver runs `bench.py --gpus N --steps K --warmup W` for N in 1,2,4,8;
+round 1's bench rounded K down to a multiple of the graph size and timed 0
+steps at K = 20.  These tests pin that exactly K steps are timed for any K,
+that target syncs / stats gathers fire at their step boundaries, and that
+`--gpus 2` starts two ranks by itself (gloo stand-in step, no GPU).
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # pylint: disable=g-import-not-at-top,wrong-import-position
+
+
+@pytest.mark.parametrize('steps', [1, 20, 49, 50, 51, 5000])
+@pytest.mark.parametrize('graph_steps', [1, 50])
+def test_exact_step_count(steps, graph_steps):
+  g, rem = bench.plan_chunks(steps, graph_steps, True)
+  assert 1 <= g <= graph_steps and 0 <= rem < g
+  assert (steps // g) * g + rem == steps
+  calls = []
+
+  class G:
+    def __init__(self, k):
+      self.k = k
+
+    def replay(self):
+      calls.append(self.k)
+
+  graphs = {k: G(k) for k in (g, rem) if k > 1}
+  runner = bench.StepRunner(lambda: calls.append(1), graphs, 10**9,
+                            lambda: None)
+  assert runner.run(steps, g, rem) == steps
+  assert sum(calls) == steps
+  # at most one eager / remainder chunk after the full graphs
+  assert len(calls) <= steps // g + max(rem, 1)
+
+
+def test_eager_and_invalid():
+  assert bench.plan_chunks(20, 50, False) == (1, 0)
+  with pytest.raises(ValueError):
+    bench.plan_chunks(0, 50, True)
+
+
+@pytest.mark.parametrize('g', [1, 7, 50])
+def test_target_sync_and_stats_boundaries(g):
+  syncs, stats = [], []
+  rem = 1000 % g
+  graph = type('G', (), {'replay': lambda self: None})()
+  runner = bench.StepRunner(lambda: None, {g: graph, rem: graph}, 100,
+                            lambda: syncs.append(runner.done), 250,
+                            stats.append)
+  runner.run(1000, g, rem)
+  # every crossing of a period boundary syncs once, right after that chunk
+  assert len(syncs) == 10
+  assert all(0 <= s - 100 * (i + 1) < max(g, 1) for i, s in enumerate(syncs))
+  assert len(stats) == 4
+
+
+def _run_bench(args, env=None, timeout=240):
+  e = dict(os.environ)
+  for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+    e.pop(k, None)
+  e.update(env or {})
+  return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args,
+                        capture_output=True, text=True, timeout=timeout, env=e,
+                        cwd=ROOT)
+
+
+def test_gpus2_spawns_two_ranks_gloo():
+  p = _run_bench(['--gpus', '2', '--steps', '20', '--warmup', '5',
+                  '--stats-every', '8', '--target-period', '10',
+                  '--graph-steps', '6', '--selftest-cpu'])
+  assert p.returncode == 0, p.stderr[-2000:]
+  lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+  assert len(lines) == 1  # rank 0 only
+  out = json.loads(lines[0])
+  assert out['n_gpus'] == 2 and out['steps'] == 20
+  assert out['per_rank_steps'] == [20, 20]
+  assert out['chunks'] == [6, 2]
+  # warmup 5 + 20 timed: target-period 10 crossed at 10 and 20 (and 25 is
+  # not a multiple), stats-every 8 crossed at 8, 16, 24
+  assert out['per_rank_target_syncs'] == [2, 2]
+  assert out['per_rank_stats_gathers'] == [3, 3]
+  assert out['value'] > 0
+
+
+def test_world_mismatch_fails():
+  p = _run_bench(['--gpus', '2', '--steps', '4', '--warmup', '0',
+                  '--selftest-cpu'], env={'WORLD_SIZE': '1'}, timeout=120)
+  assert p.returncode != 0
+  assert 'WORLD_SIZE=1' in p.stderr

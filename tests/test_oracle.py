@@ -311,3 +311,41 @@ def test_oracle_second_order_meta_update_matches_torch_autograd():
     np.testing.assert_allclose(ref['dlogits'], want, rtol=1e-6,
                                atol=1e-6 * np.abs(want).max(), err_msg='bound=%g' % bound)
     assert np.abs(want).max() > 0
+
+
+@pytest.mark.parametrize('algo', ['dqn', 'double', 'per'])
+def test_torch_cpu_baseline_matches_oracle(algo):
+  """bench.py's CPU baseline (oracle/torch_cpu.py) computes the same update."""
+  from oracle import torch_cpu
+  shared = algo != 'dqn'
+  a = 6
+  online = _init(a, shared, 11)
+  target = helpers.perturbed_tree(online, 12)
+  rng = np.random.default_rng(13)
+  b = 8
+  s_tm1 = rng.integers(0, 256, (b, 84, 84, 4), dtype=np.uint8)
+  s_t = rng.integers(0, 256, (b, 84, 84, 4), dtype=np.uint8)
+  act = rng.integers(0, a, b)
+  r = rng.choice([-1.0, 0.0, 1.0], b)
+  d = np.where(rng.random(b) < 0.2, 0.0, 0.99)
+  w = rng.uniform(0.3, 1.0, b) if algo == 'per' else None
+  lrn = torch_cpu.TorchCpuLearner(online, target, algo=algo)
+  mu = learner_ref.zeros_like_tree(online)
+  nu = learner_ref.zeros_like_tree(online)
+  params = online
+  for _ in range(2):
+    ref = learner_ref.learner_step(params, target, mu, nu, s_tm1, act, r, d,
+                                   s_t, algo=algo, weights=w)
+    q, td, loss = lrn.step(
+        torch.from_numpy(s_tm1), torch.from_numpy(act), torch.from_numpy(r).float(),
+        torch.from_numpy(d).float(), torch.from_numpy(s_t),
+        None if w is None else torch.from_numpy(w).float())
+    np.testing.assert_allclose(q.numpy(), ref['q_tm1'], atol=1e-4)
+    np.testing.assert_allclose(td.numpy(), ref['td'], atol=1e-4)
+    np.testing.assert_allclose(float(loss), ref['loss'], rtol=1e-4)
+    params, mu, nu = ref['params'], ref['mu'], ref['nu']
+  got = lrn.params_tree()
+  for m in params:
+    for n in params[m]:
+      np.testing.assert_allclose(got[m][n], params[m][n], atol=2e-6,
+                                 err_msg=m + '/' + n)
