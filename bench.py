@@ -56,16 +56,11 @@ def phase_flops(algo, batch):
       'conv2_fwd': 2 * z * b * MAC['conv2'],
       'conv3_fwd': 2 * z * b * MAC['conv3'],
       'fc1_fwd': 2 * z * b * MAC['fc1'],
-      'head': 2 * z * b * MAC['fc2'],
+      # fc2 forward + fc2 dX (dz1 = dq W2^T)
+      'head': 2 * z * b * MAC['fc2'] + 2 * b * MAC['fc2'],
       'fc1_dx': 2 * b * MAC['fc1'],
-      'head+fc1_dx': 2 * z * b * MAC['fc2'] + 2 * b * MAC['fc1'],
-      'conv3_dx+fc1_dw': 2 * b * (MAC['conv3'] + MAC['fc1']),
-      'conv2_dx+conv3_dw': 2 * b * (MAC['conv2'] + MAC['conv3']),
-      'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 2 * b * (2 * MAC['conv3'] + MAC['fc1'] +
-                                                   MAC['conv2']),
-      'conv1_dw+conv2_dw': 2 * b * (MAC['conv1'] + MAC['conv2']),
       ALL_BWD: 2 * b * (2 * MAC['conv3'] + MAC['fc1'] + 2 * MAC['conv2'] + MAC['conv1']),
-      'update': 0,
+      'update': 2 * b * MAC['fc2'],  # fc2 dW (the rest is the optimizer)
   }
 
 
@@ -82,8 +77,9 @@ def phase_bytes(algo, batch):
 
   Every tensor the phase consumes is read once and every tensor it produces
   is written once; implementation scratch (split-K partials, per-sample dW
-  partials) is excluded.  Centered RMSProp reads and writes theta, mu, nu
-  (6 x 4 B per parameter); fc1's update runs inside conv3_dx+fc1_dw.
+  partials, hand-off payloads) is excluded.  Centered RMSProp reads and
+  writes theta, mu, nu (6 x 4 B per parameter); fc1's update runs inside the
+  merged backward launch.
   """
   z = 2 if algo == 'dqn' else 3
   b = batch
@@ -93,22 +89,9 @@ def phase_bytes(algo, batch):
       'conv2_fwd': z * b * (ACT['y1'] + ACT['y2']) + z * PARAM['conv2'],
       'conv3_fwd': z * b * (ACT['y2'] + ACT['y3']) + z * PARAM['conv3'],
       'fc1_fwd': z * b * (ACT['y3'] + ACT['h']) + z * PARAM['fc1'],
-      'head': z * b * ACT['h'] + z * PARAM['fc2'],
+      # fc1 reduce -> h1 (read once as the split sum, written), W2, dz1 out
+      'head': z * b * ACT['h'] + z * PARAM['fc2'] + b * ACT['h'],
       'fc1_dx': b * (ACT['h'] + 2 * ACT['y3']) + PARAM['fc1'],
-      # one launch (head_dx_kernel): dz1 is handed off inside it
-      'head+fc1_dx': (z * b * ACT['h'] + z * PARAM['fc2'] + 2 * b * ACT['y3'] +
-                      PARAM['fc1']),
-      'conv3_dx+fc1_dw': (b * (ACT['y3'] + 2 * ACT['y2']) + PARAM['conv3'] +
-                          b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
-      'conv2_dx+conv3_dw': (b * (ACT['y2'] + 2 * ACT['y1']) + PARAM['conv2'] +
-                            b * (ACT['y2'] + ACT['y3']) + PARAM['conv3']),
-      # one launch (bwd_bc_kernel): dy2 is handed off inside it, dy3 and y2
-      # are read once
-      'conv3_dx+conv2_dx+fc1_dw+conv3_dw': (
-          b * (ACT['y3'] + ACT['y2'] + 2 * ACT['y1']) + 2 * PARAM['conv3'] +
-          PARAM['conv2'] + b * (ACT['y3'] + ACT['h']) + 6 * PARAM['fc1']),
-      'conv1_dw+conv2_dw': (b * (ACT['state'] + ACT['y1']) + PARAM['conv1'] +
-                            b * (ACT['y1'] + ACT['y2']) + PARAM['conv2']),
       # the whole backward after fc1 dX in one launch: dy2 and dy1 are handed
       # off inside it; dy3, y2, y1 and the state are read once
       ALL_BWD: (b * (ACT['y3'] + ACT['y2'] + ACT['y1'] + ACT['state']) +
@@ -122,11 +105,8 @@ def phase_bytes(algo, batch):
 PHASE_KERNEL = {
     'conv1_fwd': 'conv1_fwd_kernel', 'conv2_fwd': 'conv2_fwd_kernel',
     'conv3_fwd': 'conv3_fwd_kernel', 'fc1_fwd': 'fc1_fwd_kernel',
-    'head': 'head_kernel', 'fc1_dx': 'fc1_dx_kernel',
-    'head+fc1_dx': 'head_dx_kernel',
-    'conv3_dx+fc1_dw': 'bwd_b_kernel', 'conv2_dx+conv3_dw': 'bwd_c_kernel',
-    'conv3_dx+conv2_dx+fc1_dw+conv3_dw': 'bwd_bc_kernel',
-    'conv1_dw+conv2_dw': 'bwd_d_kernel', ALL_BWD: 'bwd_bc_kernel',
+    'head': 'head_kernel',
+    'fc1_dx': 'fc1_dx_kernel', ALL_BWD: 'bwd_bc_kernel',
     'update': 'update_kernel'}
 PMC_JSON = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
 

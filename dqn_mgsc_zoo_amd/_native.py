@@ -18,17 +18,12 @@ ALGO_DOUBLE = 1
 ALGO_PER = 2
 NUM_LEAVES = 10
 NUM_PHASES = 10
+# dqz_learner_profile's phase slots; slots 7 and 8 are merged into
+# bwd_bc_kernel and report 0.
 PHASE_NAMES = (
     'conv1_fwd', 'conv2_fwd', 'conv3_fwd', 'fc1_fwd', 'head', 'fc1_dx',
-    'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw', 'conv2_dx+conv3_dw',
-    'conv1_dw+conv2_dw', 'update')
-# Phase 6 of the split-backward debug layout (DQZ_FUSED_BWD=0), where phase 7
-# is a launch of its own, and of the late-dW layout (DQZ_DW_LATE=1), where
-# phase 8 is.
-PHASE6_SPLIT = 'conv3_dx+fc1_dw'
-# Phase 4 when the head and fc1 dX are one launch (DQZ_FUSED_HEAD=1).
-PHASE4_FUSED = 'head+fc1_dx'
-PHASE6_LATE_DW = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw'
+    'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw', 'unused7',
+    'unused8', 'update')
 FRAME_H = 84
 FRAME_W = 84
 STACK = 4

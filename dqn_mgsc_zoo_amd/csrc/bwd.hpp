@@ -500,67 +500,10 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   if constexpr (PUB) a.sync1.arrive(b);
 }
 
-__device__ __forceinline__ void conv2_bwd_dw(const Conv2BwdArgs& a, float* s_win, int b, int nq) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
-  const int n = lane & 15, kq = lane >> 4;
-  float dr[21];
-#pragma unroll
-  for (int kk = 0; kk < 21; ++kk) {
-    const int p = 4 * kk + kq;
-    const float v = a.dy2[((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 16 * nq + n];
-    dr[kk] = p < C2M ? v : 0.f;
-  }
-  const float4* src = reinterpret_cast<const float4*>(a.y1 + (int64_t)b * (C1M * C1CO));
-  constexpr int NQ4 = C1M * C1CO / 4;  // 3200
-  float4 r[13];
-#pragma unroll
-  for (int q = 0; q < 13; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
-#pragma unroll
-  for (int q = 0; q < 13; ++q) {
-    const int i = t + 256 * q;
-    if (i < NQ4) {
-      const int pix = i >> 3;
-      *reinterpret_cast<float4*>(s_win + (pix / C1O) * C2W_RS + (pix % C1O) * C2W_S + (i & 7) * 4) = r[q];
-    }
-  }
-  __syncthreads();
-  DQZ_STAMP(13, 1);
-  int pb[21];
-#pragma unroll
-  for (int kk = 0; kk < 21; ++kk) {
-    const int p = min(4 * kk + kq, C2M - 1);
-    pb[kk] = (2 * (p / C2O) + w) * C2W_RS + 2 * (p % C2O) * C2W_S + n;
-  }
-  f32x4 acc[8];  // tile = (kw, ci half)
-#pragma unroll
-  for (int m = 0; m < 8; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 21; ++kk)
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int off = (m >> 1) * C2W_S + 16 * (m & 1);
-      acc[m] = mfma4(s_win[pb[kk] + off], dr[kk], acc[m]);
-    }
-  float* part = a.part + (int64_t)b * (C2KK + 1) * C2CO + 16 * nq + n;
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-      part[((w * C2K + (m >> 1)) * C2CI + 16 * (m & 1) + 4 * kq + rr) * C2CO] = acc[m][rr];
-  if (w == 0) {
-    float sb = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 21; ++kk) sb += dr[kk];
-    sb += __shfl_xor(sb, 16, 64);
-    sb += __shfl_xor(sb, 32, 64);
-    if (kq == 0) part[C2KK * C2CO] = sb;
-  }
-}
-
 // conv2 dW as 8 jobs per sample for the merged backward launch: job (kh, ch)
 // computes part[b][(kh*4 + kw)*32 + ci][32 ch + co'] for all kw (wave w = kw),
-// ci and its 32 output channels, K = the 81 positions in conv2_bwd_dw's k
-// order (the same bits).  Only the 9 input rows 2 oh + kh are staged (29 KB
+// ci and its 32 output channels, K = the 81 positions in a fixed k
+// order.  Only the 9 input rows 2 oh + kh are staged (29 KB
 // of LDS instead of 64 KB, so the job fits beside the other backward jobs);
 // dy2 comes from this launch's conv3 dX jobs (wait + sc1 loads).
 constexpr int C2V_WIN = 9 * C2W_RS;  // 7272 floats
@@ -629,7 +572,7 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
         part[((kh * C2K + w) * C2CI + 16 * mt + 4 * kq + rr) * C2CO + 16 * ct] = acc[mt][ct][rr];
-  if (kh == 0 && w == 0) {  // bias row (conv2_bwd_dw's order: per lane over kk, then over kq)
+  if (kh == 0 && w == 0) {  // bias row (per lane over kk, then over kq)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       float sb = 0.f;
@@ -753,14 +696,9 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
 }
 
 // ---- backward launches ----------------------------------------------------
-// Each launch pairs a critical-path dX job set with an independent dW job set
-// so the latency-bound dX workgroups and the dW workgroups share the CUs
-// (one launch, no cross-stream dependency edges):
-//   fc1_dx_kernel                  fc1 dX
-//   bwd_b_kernel  = conv3 dX (8 jobs/sample)  + fc1 dW + RMSProp (784 blocks)
-//   bwd_c_kernel  = conv2 dX (8 jobs/sample)  + conv3 dW (4 jobs/sample)
-//   bwd_d_kernel  = conv1 dW (4 jobs/sample)  + conv2 dW (4 jobs/sample)
-constexpr size_t kBwdDSmem = (C2W_WIN * sizeof(float) > kConv1DwSmem) ? C2W_WIN * sizeof(float) : kConv1DwSmem;
+// fc1_dx_kernel (fc1 dX), then bwd_bc_kernel: the critical-path dX job chain
+// and the independent dW job sets share one launch, so the latency-bound dX
+// workgroups and the dW workgroups share the CUs (no cross-stream edges).
 
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[FC1B_SMEM];
@@ -780,150 +718,11 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   DQZ_STAMP(5, 3);
 }
 
-// ---- head + fc1 dX in one launch ---------------------------------------------
-// head_dx_kernel: grid [B head blocks][FLAT / 32 fc1 dX blocks], 512 threads.
-// The head blocks run head_body with dz1 published (write-through stores,
-// then one arrival each on Handoff word 0).  A dX block owns 32 rows of W1:
-// waves 0-3 rows [k0, k0 + 16), waves 4-7 rows [k0 + 16, k0 + 32), wave
-// w & 3 one 128-wide quarter of the hidden units, so every dy3 element is the
-// same MFMA chain and the same four-way sum as in fc1_dx_kernel (bit-exact).
-// What does not depend on dz1 (the block's W1 rows, the dX-ordered W3 / W2
-// copies) is loaded before the block waits for the B arrivals; dz1 is then
-// loaded sc1.  Head blocks never wait and precede every dX block in dispatch
-// order, so the wait terminates.  Saves one kernel boundary and moves the W1
-// fetch of fc1 dX under the head.
-constexpr int HDX_ROWS = 32, HDX_BLOCKS = FLAT / HDX_ROWS;  // 98
-constexpr int HDX_SMEM = 32 * FC1B_LD + 2 * 4 * 2 * 256;   // dz1 chunk + dX partials of both row groups
-
-template <int AMAX>
-__global__ __launch_bounds__(512) void head_dx_kernel(HeadArgs h, Fc1BwdArgs a, Handoff hand) {
-  if ((int)blockIdx.x < h.B) {
-    head_body<AMAX, 7, true>(h, blockIdx.x, hand);
-    return;
-  }
-  DQZ_STAMP(5, 0);
-  __shared__ __attribute__((aligned(16))) float smem[HDX_SMEM];
-  float* s_dz = smem;
-  float(*s_red)[4][2][256] = reinterpret_cast<float(*)[4][2][256]>(smem + 32 * FC1B_LD);
-  const int blk = blockIdx.x - h.B;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wq = w & 3, rg = w >> 2, tt = t & 255;
-  const int n = lane & 15, kq = lane >> 4;
-  const int k0 = HDX_ROWS * blk + 16 * rg;  // first W1 row of this thread's row group
-  // W3 / W2 dX copies: element g of the 69,632 is thread g of the dX range
-  const int g = blk * 512 + t;
-  float v3 = 0.f, v2 = 0.f;
-  if (a.w3p) {
-    if (g < W3P_N) v3 = a.w3[w3p_src(g)];
-    if (g < W2P_N) v2 = a.w2[w2p_src(g)];
-  }
-  const float* W1 = a.th + a.w_off;
-  float4 wv[8];  // dX B operand: W1[k0 + n][128 wq + 16 j + 4 kq + e]
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * wq + 16 * j + 4 * kq);
-  hand.wait(0);
-  DQZ_STAMP(5, 1);
-  const float4* dz4 = reinterpret_cast<const float4*>(a.dz1);
-  const int dz_bytes = a.B * HID * 4;
-  for (int c = 0; c < a.B; c += 32) {
-    if (c > 0) __syncthreads();  // previous chunk's s_dz / s_red readers are done
-    float4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = t + 512 * i, row = f >> 7;
-      const float4 x = load_sc1_f4(dz4, dz_bytes, min(c + row, a.B - 1) * (HID / 4) + (f & 127));
-      v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float ym[2];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-      ym[hh] = a.y3[(int64_t)min(c + 16 * hh + (tt >> 4), a.B - 1) * FLAT + k0 + (tt & 15)];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = t + 512 * i;
-      *reinterpret_cast<float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127)) = v[i];
-    }
-    __syncthreads();
-    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const float* d = s_dz + (16 * mt + n) * FC1B_LD + 128 * wq + 4 * kq;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
-        xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
-        xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
-        xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
-        xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s_red[rg][wq][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
-    __syncthreads();
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int sample = c + 16 * hh + (tt >> 4);
-      const float s = (s_red[rg][0][hh][tt] + s_red[rg][1][hh][tt]) + (s_red[rg][2][hh][tt] + s_red[rg][3][hh][tt]);
-      if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (tt & 15)] = ym[hh] > 0.f ? s : 0.f;
-    }
-  }
-  if (a.w3p) {
-    if (g < W3P_N) a.w3p[g] = v3;
-    if (g < W2P_N) a.w2p[g] = v2;
-  }
-  DQZ_STAMP(5, 3);
-}
-
-inline hipError_t launch_head_dx(const HeadArgs& h, const Fc1BwdArgs& f, const Handoff& hand, hipStream_t st) {
-  if (h.S > 7) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(h.B + HDX_BLOCKS));
-  if (h.A <= 8)
-    hipLaunchKernelGGL((head_dx_kernel<8>), grid, dim3(HID), 0, st, h, f, hand);
-  else
-    hipLaunchKernelGGL((head_dx_kernel<MAXA>), grid, dim3(HID), 0, st, h, f, hand);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(256) void bwd_b_kernel(Conv3BwdArgs c3, Fc1BwdArgs f1) {
-  __shared__ __attribute__((aligned(16))) float smem[C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM];
-  const int n3 = 8 * ((c3.B + 7) / 8) * 8;
-  if ((int)blockIdx.x < n3) {
-    const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c3.B);
-    if (!sj.valid) return;
-    DQZ_STAMP(6, 0);
-    conv3_bwd_dx<false>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
-    DQZ_STAMP(6, 3);
-  } else {
-    fc1_dw_body(f1, smem, blockIdx.x - n3);
-  }
-}
-
-__global__ __launch_bounds__(256) void bwd_c_kernel(Conv2BwdArgs c2, Conv3BwdArgs c3) {
-  __shared__ __attribute__((aligned(16))) float smem[C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN];
-  const int n2 = 8 * ((c2.B + 7) / 8) * 8;
-  if ((int)blockIdx.x < n2) {
-    const SampleJob sj = xcd_sample_job_at(blockIdx.x, 8, c2.B);
-    if (!sj.valid) return;
-    DQZ_STAMP(7, 0);
-    conv2_bwd_dx<false>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-    DQZ_STAMP(7, 3);
-  } else {
-    const SampleJob sj = xcd_sample_job_at(blockIdx.x - n2, 4, c3.B);
-    if (!sj.valid) return;
-    DQZ_STAMP(12, 0);
-    conv3_bwd_dw(c3, smem, sj.s, sj.job);
-    DQZ_STAMP(12, 3);
-  }
-}
-
 // bwd_bc_kernel: the whole backward after fc1 dX in one launch.  Grid, in
 // dispatch order:
 //   [conv3 dX 8/sample] [fc1 dW 784] [conv2 dX 8/sample] [conv3 dW 4/sample]
 //   [conv1 dW 8/sample] [conv2 dW 8/sample]
-// (the last two ranges only when c1.B > 0; otherwise conv1 / conv2 dW run in
-// bwd_d_kernel).  Hand-offs inside the launch (common.hpp Handoff): dy2 from
+// Hand-offs inside the launch (common.hpp Handoff): dy2 from
 // the 8 conv3 dX jobs of a sample to its 8 conv2 dX and 8 conv2 dW jobs, dy1
 // from the 8 conv2 dX jobs to its 8 conv1 dW jobs.  Every consumer has a
 // higher block index than its producers and workgroups are dispatched in
@@ -941,7 +740,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   __shared__ __attribute__((aligned(16))) float smem[kWA > kW3 ? kWA : kW3];
   const int B8 = (c3.B + 7) / 8 * 8;
   constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
-  const bool all_dw = c1.B > 0;
   int i = blockIdx.x;
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
@@ -961,10 +759,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
     DQZ_STAMP(7, 0);
-    if (all_dw)
-      conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-    else
-      conv2_bwd_dx<true, false>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
     return;
   }
@@ -993,22 +788,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   DQZ_STAMP(13, 0);
   conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
   DQZ_STAMP(13, 3);
-}
-
-__global__ __launch_bounds__(256) void bwd_d_kernel(Conv1DwArgs c1, Conv2BwdArgs c2) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int n1 = 4 * ((c1.B + 7) / 8) * 8;
-  if ((int)blockIdx.x < n1) {
-    const SampleJob sj = xcd_sample_job_at(blockIdx.x, C1_BLOCKS, c1.B);
-    if (!sj.valid) return;
-    conv1_dw_body(c1, smem, sj.job, sj.s);
-  } else {
-    const SampleJob sj = xcd_sample_job_at(blockIdx.x - n1, 4, c2.B);
-    if (!sj.valid) return;
-    DQZ_STAMP(13, 0);
-    conv2_bwd_dw(c2, smem, sj.s, sj.job);
-    DQZ_STAMP(13, 3);
-  }
 }
 
 }  // namespace dqz

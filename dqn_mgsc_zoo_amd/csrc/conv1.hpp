@@ -196,63 +196,11 @@ struct Conv1DwArgs {
   Handoff sync1;     // dy1 arrival counters (conv1_dw_half in bwd_bc_kernel)
 };
 
-// Partial dW/db of one 100-position block: part[k][co] = sum_p x(p,k) dy(p,co).
-// grid (4 row blocks, B); wave w owns kernel rows [64w, 64w+64) (two 32-row
-// MFMA tiles; row = kh*32 + kw*4 + ci), K' = 100 positions.
-__device__ __forceinline__ void conv1_dw_body(const Conv1DwArgs& a, float* smem, int rb, int b) {
-  DQZ_STAMP(8, 0);
-  float* s_in = smem;                 // 8064
-  float* s_dy = smem + C1_IN_FLOATS;  // 100 x 32
-  const float4* dy4 = reinterpret_cast<const float4*>(a.dy1 + ((int64_t)b * C1M + rb * C1_POS) * C1CO);
-  constexpr int ND4 = C1_POS * C1CO / 4;  // 800
-  float4 dv[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) dv[q] = dy4[min((int)threadIdx.x + 256 * q, ND4 - 1)];
-  stage_conv1_input(s_in, a.src, b, a.which, rb);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if ((int)threadIdx.x + 256 * q < ND4) reinterpret_cast<float4*>(s_dy)[threadIdx.x + 256 * q] = dv[q];
-  __syncthreads();
-  DQZ_STAMP(8, 1);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, i = lane & 31;
-  const int kw = i >> 2, ci = i & 3;
-  float* part = a.part + ((int64_t)b * C1_BLOCKS + rb) * (C1KK + 1) * C1CO;
-  if (threadIdx.x < C1CO) {  // bias row
-    float s = 0.f;
-    for (int p = 0; p < C1_POS; ++p) s += s_dy[p * C1CO + threadIdx.x];
-    part[C1KK * C1CO + threadIdx.x] = s;
-  }
-  const float* pa = s_in + ci * C1_PLANE + kw + 4 * h;
-  const float* pb = s_dy + h * C1CO + i;
-#pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
-    const int kh = 2 * wave + t2;  // 32-row tile index == kh
-    const float* pat = pa + kh * FW;
-    f32x16 acc = {};
-#pragma unroll
-    for (int j = 0; j < C1_POS / 2; ++j) {
-      const int p0 = 2 * j;  // positions p0 + h share an output row
-      const float av = pat[(C1S * (p0 / C1O)) * FW + C1S * (p0 % C1O)];
-      const float bv = pb[64 * j];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      part[(kh * 32 + row) * C1CO + i] = acc[r];
-    }
-  }
-  DQZ_STAMP(8, 3);
-}
-
 // Half-channel job of conv1 dW for the merged backward launch (bwd_bc_kernel):
 // rows block rb of sample b, input channels {2 ch, 2 ch + 1}.  Its 128 dW rows
 // (kh 8 x kw 8 x ci 2) are four 32-row MFMA tiles, one per wave (wave w: kh
 // 2w, 2w + 1; tile row m = 16 (kh - 2w) + 2 kw + ci'), each accumulated over
-// the 100 positions in conv1_dw_body's k order, so the partials are the
-// same bits.  LDS: two input planes + the 100 x 32 dy1 block (29 KB).  dy1
+// the 100 positions in a fixed order.  LDS: two input planes + the 100 x 32 dy1 block (29 KB).  dy1
 // comes from this launch's conv2 dX jobs: the block waits for its sample's
 // counter and loads dy1 with sc1 loads.
 constexpr int C1H_SMEM = 2 * C1_PLANE + C1_POS * C1CO;  // 7232 floats
@@ -289,7 +237,7 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
   const int h = lane >> 5, i = lane & 31;
   const int kh = 2 * wave + (i >> 4), kw = (i >> 1) & 7, cp = i & 1;
   float* part = a.part + ((int64_t)b * C1_BLOCKS + rb) * (C1KK + 1) * C1CO;
-  if (ch == 0 && tid < C1CO) {  // bias row (conv1_dw_body's order)
+  if (ch == 0 && tid < C1CO) {  // bias row
     float sb = 0.f;
     for (int p = 0; p < C1_POS; ++p) sb += s_dy[p * C1CO + tid];
     part[C1KK * C1CO + tid] = sb;
@@ -315,6 +263,5 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
 }
 
 constexpr size_t kConv1FwdSmem = (C1_IN_FLOATS + C1KK * C1CO) * sizeof(float);
-constexpr size_t kConv1DwSmem = (C1_IN_FLOATS + C1_POS * C1CO) * sizeof(float);
 
 }  // namespace dqz

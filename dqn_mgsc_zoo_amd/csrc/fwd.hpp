@@ -250,16 +250,21 @@ struct Fc1FwdArgs {
   float* part;      // [Z][FC1_S][B][512]
 };
 
-__global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
-  DQZ_STAMP(3, 0);
-  __shared__ float s_red[4][2][256];
+// The MFMA body of one fc1 block: its (z, split s, column tile nt, row group
+// mg) and the four waves' [2][256] K-quarter tiles in s_red[w * 512 ..]
+// (row 16 mt + 4 kq + rr, column n at [mt * 256 + (4 kq + rr) * 16 + n]).
+__device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int& z, int& s, int& nt, int& mg) {
   // Block -> tile map: the two 16-column tiles that share W1's 128-byte lines
   // (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
   // dispatch places on the same XCD, so each line is fetched into one L2.
   const int i = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const int slot = i >> 3, pair = (i & 7) + 8 * (slot >> 1);
-  const int nt = 2 * (pair % 16) + (slot & 1), rest = pair / 16;
-  const int s = rest % FC1_S, zm = rest / FC1_S, z = zm / a.MG, mg = zm % a.MG;
+  nt = 2 * (pair % 16) + (slot & 1);
+  const int rest = pair / 16;
+  s = rest % FC1_S;
+  const int zm = rest / FC1_S;
+  z = zm / a.MG;
+  mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = s * FC1_KS + w * FC1_KW;
@@ -292,14 +297,23 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w][mt][(4 * kq + rr) * 16 + n] = acc[mt][rr];
-  DQZ_STAMP(3, 2);
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 512 + mt * 256 + (4 * kq + rr) * 16 + n] = acc[mt][rr];
   __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
+  DQZ_STAMP(3, 0);
+  __shared__ float s_red[4 * 2 * 256];
+  int z, s, nt, mg;
+  fc1_fwd_tile(a, s_red, z, s, nt, mg);
+  DQZ_STAMP(3, 2);
+  const int t = threadIdx.x;
   // 512 outputs (32 rows x 16 cols), 2 per thread
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = 32 * mg + 16 * h + (t >> 4);
-    const float v = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
+    const float* sr = s_red + h * 256 + t;
+    const float v = (sr[0] + sr[512]) + (sr[1024] + sr[1536]);
     if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
   }
   DQZ_STAMP(3, 3);

@@ -5,12 +5,10 @@
 //                 [, online(s_t) for double-Q])                  conv1.hpp
 //   1 conv2 fwd  2 conv3 fwd  3 fc1 fwd (split-K)                fwd.hpp
 //   4 head: fc1 reduce + fc2 + TD loss + dq + dz1, per sample    head.hpp
-//   5 fc1 dX -> dy3                                              bwd.hpp
-//     (DQZ_FUSED_HEAD=1: 4 + 5 as one launch with an in-launch dz1 hand-off,
-//     head_dx_kernel; measured slower)
-//   6 {conv3 dX -> dy2, fc1 dW + fused RMSProp}                  bwd_b_kernel
-//   7 {conv2 dX (stride-phase split) -> dy1, conv3 dW partials}  bwd_c_kernel
-//   8 {conv1 dW partials (frame gather fused), conv2 dW partials} bwd_d_kernel
+//   5 fc1 dX -> dy3 (+ the dX-ordered W3 / W2 copies)            bwd.hpp
+//   6 the rest of the backward in one launch (bwd_bc_kernel): conv3 dX ->
+//     conv2 dX -> conv1 dW hand-offs, fc1 dW + fused RMSProp, conv3 / conv2
+//     dW partials                                                 bwd.hpp
 //   9 reduce of every cross-sample / split-K gradient + centered RMSProp
 #include <hip/hip_runtime.h>
 
@@ -60,10 +58,6 @@ struct dqz_learner {
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
-  int fused_bwd;  // 1: bwd_bc_kernel (+ bwd_d_kernel if dw_late); 0: bwd_b / bwd_c / bwd_d (DQZ_FUSED_BWD=0)
-  int dw_late;    // 1: conv1 / conv2 dW in bwd_d_kernel after the merged launch (DQZ_DW_LATE=1)
-  int fused_head;  // 1: head + fc1 dX in one launch (head_dx_kernel, DQZ_FUSED_HEAD=1, measured 2-3 % slower); 0: two launches
-  int fused_fwd;  // 1: fwd_conv_kernel (DQZ_FUSED_FWD=1, measured 1.5 % slower); 0: conv1 / conv2 / conv3 launches
   void* block;
 };
 
@@ -75,8 +69,6 @@ static int init_kernel_attrs() {
                               (int)kConv1FwdSmem));
   DQZ_HIP(hipFuncSetAttribute((const void*)fwd_conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kConv1FwdSmem));
-  DQZ_HIP(hipFuncSetAttribute((const void*)bwd_d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kBwdDSmem));
   g_attr_done = 1;
   return DQZ_OK;
 }
@@ -104,16 +96,6 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   L->Z = cfg->algo == DQZ_ALGO_DQN ? 2 : 3;
   L->shared_bias = cfg->algo == DQZ_ALGO_DQN ? 0 : 1;
   param_layout(cfg->num_actions, L->shared_bias, L->off, L->sz, &L->total);
-  {
-    const char* e = getenv("DQZ_FUSED_BWD");
-    L->fused_bwd = !(e && e[0] == '0');
-    e = getenv("DQZ_DW_LATE");
-    L->dw_late = e && e[0] == '1';
-    e = getenv("DQZ_FUSED_HEAD");
-    L->fused_head = e && e[0] == '1';
-    e = getenv("DQZ_FUSED_FWD");
-    L->fused_fwd = e && e[0] == '1';
-  }
   const int B = cfg->batch, Z = L->Z, A = cfg->num_actions;
   L->S_fc1 = FC1_S;
   L->S2 = B;  // per-sample conv2 dW partials (conv2_bwd_kernel)
@@ -306,9 +288,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     Conv1Src fsrc = src;
     fsrc.fused = 1;
     fsrc.draw = *draw;
-    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, L->fused_fwd)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, false)) return rc;
   } else {
-    if (int rc = forward_impl(L, nz, Z, B, src, st, pe, L->fused_fwd)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, src, st, pe, false)) return rc;
   }
 
   Rms rms;
@@ -337,8 +319,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.ga = L->ga;
   h.dz1 = L->dz1;
 
-  // Backward: fc1 dX (in the head's launch), then the merged launch that pairs
-  // the dX chain with the independent dW job sets (bwd.hpp).
+  // Backward: fc1 dX, then the merged launch that pairs the dX chain with the
+  // independent dW job sets (bwd.hpp).
   Fc1BwdArgs fb;
   fb.dz1 = L->dz1;
   fb.y3 = L->y3;
@@ -353,17 +335,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w2 = P->online + L->off[2];
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
-  if (L->fused_head) {
-    // dz1 hand-off words: err at 16B, batch counter at 16B + 1, ack at 16B + 2 (x kStride)
-    int* const hw = L->sync + 16 * B * Handoff::kStride;
-    const Handoff hand{hw + Handoff::kStride, hw + 2 * Handoff::kStride, hw, B, HDX_BLOCKS};
-    DQZ_PHASE(4, DQZ_HIP(launch_head_dx(h, fb, hand, st)));
-    if (pe.on()) pe.ms[5] = 0.f;
-  } else {
-    DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
-    DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
-              DQZ_HIP(hipGetLastError()));
-  }
+  DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
+  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+            DQZ_HIP(hipGetLastError()));
 
   Conv3BwdArgs c3b;
   c3b.dy3 = L->dy3;
@@ -376,8 +350,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  const bool all_dw = L->fused_bwd && !L->dw_late;  // conv1 / conv2 dW inside bwd_bc_kernel
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, all_dw ? 16 : 8};
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16};
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -397,25 +370,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
-  if (L->fused_bwd) {
-    Conv1DwArgs c1k = c1dw;
-    if (!all_dw) c1k.B = 0;  // bwd_bc_kernel stops after the conv3 dW range
-    const int grid = 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + (all_dw ? 16 * B8 : 0);
-    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1k);
-              DQZ_HIP(hipGetLastError()));
-    if (pe.on()) pe.ms[7] = 0.f;
-  } else {
-    DQZ_PHASE(6, hipLaunchKernelGGL(bwd_b_kernel, dim3(8 * B8 + 4 * (FLAT / 16)), dim3(256), 0, st, c3b, fb);
-              DQZ_HIP(hipGetLastError()));
-    DQZ_PHASE(7, hipLaunchKernelGGL(bwd_c_kernel, dim3(8 * B8 + 4 * B8), dim3(256), 0, st, c2b, c3b);
-              DQZ_HIP(hipGetLastError()));
-  }
-  if (all_dw) {
-    if (pe.on()) pe.ms[8] = 0.f;
-  } else {
-    DQZ_PHASE(8, hipLaunchKernelGGL(bwd_d_kernel, dim3(4 * B8 + 4 * B8), dim3(256), kBwdDSmem, st, c1dw, c2b);
-              DQZ_HIP(hipGetLastError()));
-  }
+  const int grid = 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 16 * B8;
+  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw);
+            DQZ_HIP(hipGetLastError()));
+  if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
   UpdArgs u;
   u.th = P->online;

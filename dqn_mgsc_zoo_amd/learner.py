@@ -152,12 +152,6 @@ class Learner:
         _native.stream_handle(stream)))
     ms = [float(x) for x in out]
     names = list(_native.PHASE_NAMES)
-    if ms[5] == 0.0:  # head and fc1 dX as one launch
-      names[4] = _native.PHASE4_FUSED
-    if ms[7] > 0.0:  # split-backward layout: phase 6 is conv3 dX + fc1 dW only
-      names[6] = _native.PHASE6_SPLIT
-    elif ms[8] > 0.0:  # late-dW layout: conv2 / conv1 dW in a launch of their own
-      names[6] = _native.PHASE6_LATE_DW
     # phases merged into another launch report 0 and are left out
     return {n: t for n, t in zip(names, ms) if t > 0.0}
 

@@ -68,22 +68,20 @@ def test_error_paths_without_a_gpu(libdqz):
 
 
 def test_bench_prices_every_reportable_phase():
-  """Every phase name dqz_learner_profile can report, in every launch layout
-  (default, DQZ_FUSED_BWD=0, DQZ_DW_LATE=1, DQZ_FUSED_HEAD=1), has the
-  algorithmic FLOPs, bytes and kernel symbol bench.py's roofline needs."""
+  """Every phase name dqz_learner_profile can report has the algorithmic
+  FLOPs, bytes and kernel symbol bench.py's roofline needs."""
   import sys  # pylint: disable=g-import-not-at-top
   sys.path.insert(0, ROOT)
   import bench  # pylint: disable=g-import-not-at-top
   from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
-  names = set(_native.PHASE_NAMES) | {
-      _native.PHASE6_SPLIT, _native.PHASE6_LATE_DW, _native.PHASE4_FUSED}
+  names = set(_native.PHASE_NAMES) - {'unused7', 'unused8'}
   for algo in ('dqn', 'double'):
     flops, nbytes = bench.phase_flops(algo, 32), bench.phase_bytes(algo, 32)
     for n in names:
       assert n in flops and n in nbytes and n in bench.PHASE_KERNEL, n
       assert nbytes[n] > 0, n
-  # the merged launches count each phase's algorithmic work once
+  # the launches together count each FLOP of the step once
   f = bench.phase_flops('dqn', 32)
-  assert f['head+fc1_dx'] == f['head'] + f['fc1_dx']
-  assert f[bench.ALL_BWD] == (f['conv3_dx+fc1_dw'] + f['conv2_dx+conv3_dw'] +
-                              f['conv1_dw+conv2_dw'])
+  assert sum(f.values()) == bench.STEP_FLOP['dqn']
+  f = bench.phase_flops('double', 32)
+  assert sum(f.values()) == bench.STEP_FLOP['double']

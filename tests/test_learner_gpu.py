@@ -223,23 +223,16 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
   np.testing.assert_allclose(q_t.cpu().numpy(), q_ref, atol=Q_ATOL)
 
 
-@pytest.mark.parametrize('algo,batch,dw_late', [('dqn', 32, False), ('per', 20, False),
-                                                ('double', 64, False), ('dqn', 32, True)])
-def test_fused_handoff_kernels_bit_exact(device, algo, batch, dw_late, monkeypatch):
-  """fwd_conv_kernel (conv1 -> conv2 -> conv3 hand-offs), head_dx_kernel
-  (head -> fc1 dX hand-off of dz1) and bwd_bc_kernel
-  (conv3 dX -> conv2 dX / conv2 dW, conv2 dX -> conv1 dW hand-offs; or with
-  the dW jobs in bwd_d_kernel) give the same bits as the separate launches,
-  over many steps, under hipGraph replay and after profile-mode repeated
-  launches."""
-  monkeypatch.setenv('DQZ_FUSED_BWD', '0')
-  monkeypatch.setenv('DQZ_FUSED_FWD', '0')
-  monkeypatch.setenv('DQZ_FUSED_HEAD', '0')
-  _, ref, st, _, _, _, _, _ = _setup(algo, batch, seed=21)
-  monkeypatch.setenv('DQZ_FUSED_BWD', '1')
-  monkeypatch.setenv('DQZ_FUSED_FWD', '1')
-  monkeypatch.setenv('DQZ_FUSED_HEAD', '1')
-  monkeypatch.setenv('DQZ_DW_LATE', '1' if dw_late else '0')
+@pytest.mark.parametrize('algo,batch', [('dqn', 32), ('per', 20), ('double', 64),
+                                        ('dqn', 33)])
+def test_handoff_kernels_bit_reproducible(device, algo, batch):
+  """The in-launch hand-offs (bwd_bc_kernel: conv3 dX -> conv2 dX / conv2 dW,
+  conv2 dX -> conv1 dW) and the last-arriver head of fc1_head_kernel sum in
+  fixed orders, whichever workgroup arrives last: two learners fed the same
+  steps agree bit for bit, eagerly, under hipGraph replay and after
+  profile-mode back-to-back launches; the hand-off words reset themselves
+  (sync_status 0); and the result stays at the oracle."""
+  _, ref, st, host, online, target, mu, nu = _setup(algo, batch, seed=21)
   _, lrn, _, _, _, _, _, _ = _setup(algo, batch, seed=21)
   rng = np.random.default_rng(22)
   w = torch.rand((batch,), device=device) + 0.5 if algo == 'per' else None
@@ -248,7 +241,6 @@ def test_fused_handoff_kernels_bit_exact(device, algo, batch, dw_late, monkeypat
         rng.integers(0, st.capacity, size=batch).astype(np.int32)).to(device)
     ref.step(st, slots, w)
     lrn.step(st, slots, w)
-  # graph replay of the fused path
   slots = torch.from_numpy(
       rng.integers(0, st.capacity, size=batch).astype(np.int32)).to(device)
   side = torch.cuda.Stream(device)
@@ -266,17 +258,27 @@ def test_fused_handoff_kernels_bit_exact(device, algo, batch, dw_late, monkeypat
   for _ in range(12):
     ref.step(st, slots, w)
   torch.cuda.synchronize()
-  assert lrn.sync_status() == 0
+  assert lrn.sync_status() == 0 and ref.sync_status() == 0
   for which in ('online', 'mu', 'nu'):
     assert torch.equal(getattr(lrn, which), getattr(ref, which)), which
   q1, td1, _ = lrn.fetch_outputs()
   q2, td2, _ = ref.fetch_outputs()
   assert torch.equal(q1, q2) and torch.equal(td1, td2)
-  # profile mode repeats every launch back to back; the hand-off words must
-  # reset themselves between launches.
+  # profile mode repeats every launch back to back; the hand-off words and
+  # the last-arriver counters must reset themselves between launches.
   lrn.profile(st, slots, weights=w, iters=5)
   torch.cuda.synchronize()
   assert lrn.sync_status() == 0
+  # one more step from the same state on both: still identical, still sane
+  slots = torch.from_numpy(
+      rng.integers(0, st.capacity, size=batch).astype(np.int32)).to(device)
+  lrn.set_params(ref.params_tree('online'), ref.params_tree('target'))
+  lrn.set_opt_state(ref.params_tree('mu'), ref.params_tree('nu'))
+  ref.step(st, slots, w)
+  lrn.step(st, slots, w)
+  torch.cuda.synchronize()
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(lrn, which), getattr(ref, which)), which
 
 
 def test_per_write_back_device(device):
