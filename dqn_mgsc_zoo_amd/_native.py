@@ -163,7 +163,11 @@ SIGNATURES = {
     'dqz_per_sample': (
         _int,
         [_vp, _i64, _i64, _i64, _i64, _int, ctypes.c_double, ctypes.c_double,
-         _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
+         _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'dqz_per_add': (
+        _int,
+        [_vp, _i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, _vp,
+         ctypes.c_double, _vp, ctypes.c_int32, _vp]),
     'dqz_meta_create': (
         _int, [ctypes.POINTER(DqzMetaConfig), ctypes.POINTER(_vp)]),
     'dqz_meta_destroy': (_int, [_vp]),

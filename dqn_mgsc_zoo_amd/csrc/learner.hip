@@ -735,17 +735,55 @@ int dqz_sumtree_query(const double* tree, int64_t cap, const double* targets, in
 }
 
 int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t size, int64_t capacity, int n,
-                   double usp, double beta, int normalize, uint64_t seed, uint64_t* counter_dev, int32_t* out_slots,
-                   float* out_weights, double* out_probs, void* stream) {
-  if (!tree || !counter_dev || !out_slots || !out_weights) return fail(DQZ_ERR_INVALID, "null argument");
+                   double usp, double beta, int normalize, uint64_t seed, uint64_t* counter_dev,
+                   const int32_t* injected_uniform, const double* injected_u, const int32_t* index_to_slot,
+                   int32_t* out_indices, int32_t* out_slots, float* out_weights, double* out_probs, void* stream) {
+  if (!tree || !out_slots || !out_weights) return fail(DQZ_ERR_INVALID, "null argument");
+  if (!injected_u && !counter_dev) return fail(DQZ_ERR_INVALID, "Philox draws need counter_dev");
+  if ((injected_u == nullptr) != (injected_uniform == nullptr))
+    return fail(DQZ_ERR_INVALID, "injected_uniform and injected_u go together");
   if (cap < capacity || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two >= capacity");
   if (size < 1) return fail(DQZ_ERR_INVALID, "No IDs to sample.");
   if (n < 1 || n > 1024) return fail(DQZ_ERR_INVALID, "n must be in [1, 1024]");
   if (!(beta >= 0.0 && beta <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= exponent <= 1.");
   if (!(usp >= 0.0 && usp <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= uniform_sample_probability <= 1.");
-  hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, tree, cap, tree_levels(cap),
-                     live_base, size,
-                     capacity, n, usp, beta, normalize, seed, counter_dev, out_slots, out_weights, out_probs);
+  PerSampleArgs a;
+  a.tree = tree;
+  a.cap = cap;
+  a.levels = tree_levels(cap);
+  a.live_base = live_base;
+  a.size = size;
+  a.capacity = capacity;
+  a.n = n;
+  a.usp = usp;
+  a.beta = beta;
+  a.normalize = normalize;
+  a.seed = seed;
+  a.counter = counter_dev;
+  a.inj_uniform = injected_uniform;
+  a.inj_u = injected_u;
+  a.index_to_slot = index_to_slot;
+  a.out_indices = out_indices;
+  a.out_slots = out_slots;
+  a.out_weights = out_weights;
+  a.out_probs = out_probs;
+  hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_per_add(double* tree, int64_t cap, int32_t remove_index, int32_t add_index, double priority,
+                const double* max_seen_dev, double alpha, int32_t* index_to_slot, int32_t slot, void* stream) {
+  if (!tree) return fail(DQZ_ERR_INVALID, "null tree");
+  if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
+  const int levels = tree_levels(cap);
+  if (levels > 32) return fail(DQZ_ERR_INVALID, "cap must be <= 2^32");
+  if (add_index < 0 || add_index >= cap || remove_index >= cap) return fail(DQZ_ERR_INVALID, "index out of range");
+  if (priority < 0.0 && !max_seen_dev) return fail(DQZ_ERR_INVALID, "priority < 0 needs max_seen_dev");
+  if (priority >= 0.0 && !std::isfinite(priority)) return fail(DQZ_ERR_INVALID, "value must be finite and positive.");
+  if (alpha < 0.0) return fail(DQZ_ERR_INVALID, "Require priority_exponent >= 0.");
+  hipLaunchKernelGGL(per_add_kernel, dim3(1), dim3(ST_FAST), 0, (hipStream_t)stream, tree, cap, levels, remove_index,
+                     add_index, priority, max_seen_dev, alpha, index_to_slot, slot);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }

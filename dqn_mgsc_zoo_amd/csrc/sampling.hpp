@@ -445,55 +445,106 @@ __global__ __launch_bounds__(256) void sumtree_query_kernel(const double* __rest
   if (l == 0) out[i] = d.slot;
 }
 
-// PrioritizedDistribution.sample + importance_sampling_weights with device
-// Philox streams (replay.py:680-716, 344-376).  Tree index == replay slot.
-// One block of 32 half-waves; half-wave h handles draws h, h + 32, ...;
-// n <= 1024.
-__global__ __launch_bounds__(1024) void per_sample_kernel(const double* __restrict__ tree, int64_t cap, int levels,
-                                                          int64_t live_base, int64_t size, int64_t capacity, int n,
-                                                          double usp, double beta, int normalize, uint64_t seed,
-                                                          uint64_t* counter, int32_t* out_slots,
-                                                          float* out_weights, double* out_probs) {
+// PrioritizedDistribution.sample + importance_sampling_weights
+// (replay.py:680-716, 344-376).  Draws either from device Philox streams or,
+// when `inj_u` is set, injected from the caller's RandomState in the
+// reference's order: inj_uniform[i] = active_indices[randint] (a tree index),
+// inj_u[i] = the target uniform, inj_u[n + i] = the usp-mix uniform; the
+// counter is then neither read nor advanced.  Philox mode: tree index ==
+// replay slot, uniform picks over the live window (live_base + j) % capacity.
+// Tree index -> replay slot through `index_to_slot` when set.  One block of
+// 32 half-waves; half-wave h handles draws h, h + 32, ...; n <= 1024.
+// Probabilities are formed without contraction, as numpy evaluates them:
+// (1 - usp) * (leaf / root) + usp * (1 / size).
+struct PerSampleArgs {
+  const double* tree;
+  int64_t cap;
+  int levels;
+  int64_t live_base, size, capacity;
+  int n;
+  double usp, beta;
+  int normalize;
+  uint64_t seed;
+  uint64_t* counter;
+  const int32_t* inj_uniform;
+  const double* inj_u;
+  const int32_t* index_to_slot;
+  int32_t* out_indices;
+  int32_t* out_slots;
+  float* out_weights;
+  double* out_probs;
+};
+
+__global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
   __shared__ double s_w[1024];
-  const uint64_t ctr = *counter;
+  const bool inj = a.inj_u != nullptr;
+  const uint64_t ctr = inj ? 0 : *a.counter;
   const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
-  for (int i = h; i < n; i += 32) {
-    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
-                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-    const double u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
-    const double u_mix = (double)(r.z >> 8) * 0x1.0p-24;
-    const int64_t uni = (live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)size)) % capacity;
-    const bool use_uniform = u_mix < usp;
+  for (int i = h; i < a.n; i += 32) {
+    double u_target, u_mix;
+    int64_t uni;
+    if (inj) {
+      u_target = a.inj_u[i];
+      u_mix = a.inj_u[a.n + i];
+      uni = a.inj_uniform[i];
+    } else {
+      const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
+                                 make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32)));
+      u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+      u_mix = (double)(r.z >> 8) * 0x1.0p-24;
+      uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
+    }
+    const bool use_uniform = u_mix < a.usp;
     // t = u_target * root inside the descent (the root arrives with the first round)
-    Descent d = halfwave_descend(tree, cap, levels, 0.0, use_uniform ? 0.0 : u_target, l);
+    Descent d = halfwave_descend(a.tree, a.cap, a.levels, 0.0, use_uniform ? 0.0 : u_target, l);
     const double root = d.root;
-    int64_t slot = uni;
+    int64_t idx = uni;
     double leaf;
     if (root > 0.0 && !use_uniform) {
-      slot = d.slot;
+      idx = d.slot;
       leaf = d.leaf;
     } else {
-      leaf = tree[cap + slot];
+      leaf = a.tree[a.cap + idx];
     }
-    const double up = 1.0 / (double)size;
+    const double up = 1.0 / (double)a.size;
     const double pp = root > 0.0 ? leaf / root : up;
-    const double prob = (1.0 - usp) * pp + usp * up;
-    const double w = pow(up / prob, beta);
+    const double prob = __dadd_rn(__dmul_rn(1.0 - a.usp, pp), __dmul_rn(a.usp, up));
+    const double w = pow(up / prob, a.beta);
     if (l == 0) {
-      out_slots[i] = (int32_t)slot;
-      if (out_probs) out_probs[i] = prob;
+      if (a.out_indices) a.out_indices[i] = (int32_t)idx;
+      a.out_slots[i] = a.index_to_slot ? a.index_to_slot[idx] : (int32_t)idx;
+      if (a.out_probs) a.out_probs[i] = prob;
       s_w[i] = w;
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    double m = 0.0;
-    if (normalize)
-      for (int j = 0; j < n; ++j) m = fmax(m, s_w[j]);
-    out_weights[i] = (float)(normalize ? s_w[i] / m : s_w[i]);
-  }
+  double m = 0.0;
+  if (a.normalize)
+    for (int j = 0; j < a.n; ++j) m = fmax(m, s_w[j]);
+  for (int i = threadIdx.x; i < a.n; i += blockDim.x) a.out_weights[i] = (float)(a.normalize ? s_w[i] / m : s_w[i]);
   __syncthreads();
-  if (threadIdx.x == 0) *counter = ctr + 1;
+  if (threadIdx.x == 0 && !inj) *a.counter = ctr + 1;
+}
+
+// PrioritizedTransitionReplay.add on device (replay.py:1068-1096 with
+// PrioritizedDistribution.remove_priorities / add_priorities): the evicted
+// tree index (or -1) gets 0, the new one (priority >= 0 ? priority :
+// *max_seen) ** alpha (0 -> 0, _power), ancestors rebuilt, and
+// index_to_slot[add] = slot.  One launch of ST_FAST threads, two live.
+__global__ __launch_bounds__(ST_FAST) void per_add_kernel(double* tree, int64_t cap, int levels, int32_t remove_idx,
+                                                          int32_t add_idx, double priority, const double* max_seen,
+                                                          double alpha, int32_t* index_to_slot, int32_t slot) {
+  const int i = threadIdx.x;
+  int64_t leaf = -1;
+  double v = 0.0;
+  if (i == 0 && remove_idx >= 0 && remove_idx != add_idx) leaf = cap + remove_idx;
+  if (i == 1) {
+    const double p = priority >= 0.0 ? priority : *max_seen;
+    v = p == 0.0 ? 0.0 : pow(p, alpha);
+    leaf = cap + add_idx;
+  }
+  sumtree_set_small_body(tree, levels, 2, leaf, v);
+  if (i == 0 && index_to_slot) index_to_slot[add_idx] = slot;
 }
 
 }  // namespace dqz

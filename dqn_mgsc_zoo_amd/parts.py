@@ -1,23 +1,21 @@
 """Agent protocol and run loop of `dqn_zoo/parts.py`, unchanged in behaviour.
 
 Kept so the device agents are drop-ins for the reference's runners:
-`Agent` ABC (parts.py:43-68), `run_loop` (:71-123), `generate_statistics`
-and trackers (:126-340), `EpsilonGreedyActor` (:343-412), `LinearSchedule`
-(:415-431), `NullWriter`/`CsvWriter` (:434-494), `NullCheckpoint` /
-`Checkpoint` (:497-561).  dm_env is not installed here, so a minimal
+`Agent` ABC (parts.py:43-68), `run_loop` (:71-123), `EpsilonGreedyActor`
+(:343-412), `LinearSchedule` (:415-431) and a `Checkpoint` with the role of
+:497-561.  The statistics trackers and CSV writers (:126-340, :434-494) are
+outside the learner hot path and are not provided.  dm_env is not installed here, so a minimal
 `StepType` / `TimeStep` with the same fields and methods is provided; any
 dm_env.TimeStep works as well.
 """
 
 import abc
-import collections
-import csv
 import enum
 import os
 import pickle
-import timeit
+import types
 import typing
-from typing import Any, Iterable, Mapping, Optional, Sequence, Tuple
+from typing import Any, Iterable, Mapping, Optional, Tuple
 
 import numpy as np
 
@@ -107,130 +105,6 @@ def run_loop(agent: Agent, environment, max_steps_per_episode: int = 0,
         break
 
 
-def generate_statistics(trackers: Sequence[Any], timestep_action_sequence) -> Mapping[str, Any]:
-  for tracker in trackers:
-    tracker.reset()
-  for environment, timestep_t, agent, a_t in timestep_action_sequence:
-    for tracker in trackers:
-      tracker.step(environment, timestep_t, agent, a_t)
-  return dict(collections.ChainMap(*(t.get() for t in trackers)))
-
-
-class EpisodeTracker:
-  """Episode returns; the reward of a FIRST timestep is ignored."""
-
-  def __init__(self):
-    self._num_steps_since_reset = None
-    self._num_steps_over_episodes = None
-    self._episode_returns = None
-    self._current_episode_rewards = None
-    self._current_episode_step = None
-
-  def step(self, environment, timestep_t, agent, a_t) -> None:
-    del environment, agent, a_t
-    if self._episode_returns is None:
-      raise RuntimeError('reset() must be called before first call to step().')
-    if timestep_t.first():
-      if self._current_episode_rewards:
-        raise ValueError('Current episode reward list should be empty.')
-      if self._current_episode_step != 0:
-        raise ValueError('Current episode step should be zero.')
-    else:
-      self._current_episode_rewards.append(timestep_t.reward)
-    self._num_steps_since_reset += 1
-    self._current_episode_step += 1
-    if timestep_t.last():
-      self._episode_returns.append(sum(self._current_episode_rewards))
-      self._current_episode_rewards = []
-      self._num_steps_over_episodes += self._current_episode_step
-      self._current_episode_step = 0
-
-  def reset(self) -> None:
-    self._num_steps_since_reset = 0
-    self._num_steps_over_episodes = 0
-    self._episode_returns = []
-    self._current_episode_step = 0
-    self._current_episode_rewards = []
-
-  def get(self) -> Mapping[str, Any]:
-    if self._episode_returns is None:
-      raise RuntimeError('reset() must be called before first call to get().')
-    if self._episode_returns:
-      mean_return = np.array(self._episode_returns).mean()
-      current = sum(self._current_episode_rewards)
-      episode_return = mean_return
-    else:
-      mean_return = np.nan
-      current = (sum(self._current_episode_rewards)
-                 if self._num_steps_since_reset > 0 else np.nan)
-      episode_return = current
-    return {'mean_episode_return': mean_return,
-            'current_episode_return': current,
-            'episode_return': episode_return,
-            'num_episodes': len(self._episode_returns),
-            'num_steps_over_episodes': self._num_steps_over_episodes,
-            'current_episode_step': self._current_episode_step,
-            'num_steps_since_reset': self._num_steps_since_reset}
-
-
-class StepRateTracker:
-  """Steps per second since reset."""
-
-  def __init__(self):
-    self._num_steps_since_reset = None
-    self._start = None
-
-  def step(self, environment, timestep_t, agent, a_t) -> None:
-    del environment, timestep_t, agent, a_t
-    self._num_steps_since_reset += 1
-
-  def reset(self) -> None:
-    self._num_steps_since_reset = 0
-    self._start = timeit.default_timer()
-
-  def get(self) -> Mapping[str, float]:
-    if self._start is None:
-      raise RuntimeError('reset() must be called before first call to get().')
-    duration = timeit.default_timer() - self._start
-    rate = (self._num_steps_since_reset / duration
-            if self._num_steps_since_reset > 0 else np.nan)
-    return {'step_rate': rate, 'num_steps': self._num_steps_since_reset,
-            'duration': duration}
-
-
-class UnbiasedExponentialWeightedAverageAgentTracker:
-  """Sutton & Barto's unbiased constant-step-size trick over agent stats."""
-
-  def __init__(self, step_size: float, initial_agent: Agent):
-    self._initial_statistics = dict(initial_agent.statistics)
-    self._step_size = step_size
-    self.trace = 0.0
-    self._statistics = dict(self._initial_statistics)
-
-  def step(self, environment, timestep_t, agent, a_t) -> None:
-    del environment, timestep_t, a_t
-    self.trace = (1 - self._step_size) * self.trace + self._step_size
-    final = self._step_size / self.trace
-    assert 0 <= final <= 1
-    if final == 1:
-      self._statistics = dict(agent.statistics)
-    else:
-      self._statistics = {k: (1 - final) * self._statistics[k] + final * v
-                          for k, v in agent.statistics.items()}
-
-  def reset(self) -> None:
-    self.trace = 0.0
-    self._statistics = dict(self._initial_statistics)
-
-  def get(self) -> Mapping[str, float]:
-    return self._statistics
-
-
-def make_default_trackers(initial_agent: Agent):
-  return [EpisodeTracker(), StepRateTracker(),
-          UnbiasedExponentialWeightedAverageAgentTracker(1e-3, initial_agent)]
-
-
 def epsilon_greedy_probs(q, epsilon):
   """distrax.EpsilonGreedy: (1-eps) spread over argmax ties + eps/A."""
   q = np.asarray(q, np.float64)
@@ -315,63 +189,70 @@ class LinearSchedule:
     return (1 - frac) * self._begin_value + frac * self._end_value
 
 
-class NullWriter:
+class Checkpoint:
+  """Resume point of a training run (the role of parts.py:517-561).
 
-  def write(self, *args, **kwargs) -> None:
-    pass
+  `state` is a namespace the runner fills (`iteration`, `train_agent`,
+  `eval_agent`, `random_state`, optionally `writer`).  `save()` writes one
+  pickle of the agents' `get_state()` dictionaries (device tensors come back
+  as host numpy arrays) next to `path`; the file is written under a
+  temporary name and renamed, so an interrupted save never leaves a
+  truncated checkpoint behind.  `restore()` loads it and pushes every piece
+  back through `set_state()`.  Only files this class wrote are read.
+  """
 
-  def close(self) -> None:
-    pass
+  def __init__(self, path: Optional[str] = None):
+    self.state = types.SimpleNamespace()
+    self._path = path
+
+  @property
+  def filepath(self) -> str:
+    if self._path is not None:
+      return self._path
+    writer = getattr(self.state, 'writer', None)
+    fname = getattr(writer, 'fname', None) or getattr(writer, '_fname', None)
+    if fname is None:
+      raise ValueError('Checkpoint needs a path or a state.writer with a file name')
+    return os.path.splitext(fname)[0] + '.chkpt'
+
+  def _payload(self) -> Mapping[str, Any]:
+    out = {}
+    for key in ('iteration', 'random_state'):
+      if hasattr(self.state, key):
+        out[key] = getattr(self.state, key)
+    for key in ('train_agent', 'eval_agent', 'writer'):
+      obj = getattr(self.state, key, None)
+      if obj is not None and hasattr(obj, 'get_state'):
+        out[key] = obj.get_state()
+    return out
+
+  def save(self) -> None:
+    path = self.filepath
+    folder = os.path.dirname(path)
+    if folder:
+      os.makedirs(folder, exist_ok=True)
+    tmp = path + '.tmp'
+    with open(tmp, 'wb') as f:
+      pickle.dump(self._payload(), f, protocol=pickle.HIGHEST_PROTOCOL)
+    os.replace(tmp, path)
+
+  def can_be_restored(self) -> bool:
+    return os.path.isfile(self.filepath)
+
+  def restore(self) -> None:
+    with open(self.filepath, 'rb') as f:  # written by save() above
+      payload = pickle.load(f)
+    for key in ('iteration', 'random_state'):
+      if key in payload:
+        setattr(self.state, key, payload[key])
+    for key in ('train_agent', 'eval_agent', 'writer'):
+      obj = getattr(self.state, key, None)
+      if key in payload and obj is not None and hasattr(obj, 'set_state'):
+        obj.set_state(payload[key])
 
 
-class CsvWriter:
-  """Appends OrderedDict rows to a CSV file with a fixed header."""
-
-  def __init__(self, fname: str):
-    dirname = os.path.dirname(fname)
-    if dirname and not os.path.exists(dirname):
-      os.makedirs(dirname)
-    self._fname = fname
-    self._header_written = False
-    self._fieldnames = None
-
-  def write(self, values) -> None:
-    if self._fieldnames is None:
-      self._fieldnames = list(values.keys())
-    with open(self._fname, 'a') as f:
-      writer = csv.DictWriter(f, fieldnames=self._fieldnames)
-      if not self._header_written:
-        writer.writeheader()
-        self._header_written = True
-      writer.writerow(values)
-
-  def close(self) -> None:
-    pass
-
-  def get_state(self) -> Mapping[str, Any]:
-    return {'header_written': self._header_written, 'fieldnames': self._fieldnames}
-
-  def set_state(self, state: Mapping[str, Any]) -> None:
-    self._header_written = state['header_written']
-    self._fieldnames = state['fieldnames']
-
-
-class AttributeDict(dict):
-
-  def __getattr__(self, key):
-    return self[key]
-
-  def __setattr__(self, key, value):
-    self[key] = value
-
-  def __delattr__(self, key):
-    del self[key]
-
-
-class NullCheckpoint:
-
-  def __init__(self):
-    self.state = AttributeDict()
+class NullCheckpoint(Checkpoint):
+  """Checkpointing disabled: nothing is written or restored."""
 
   def save(self) -> None:
     pass
@@ -381,43 +262,3 @@ class NullCheckpoint:
 
   def restore(self) -> None:
     pass
-
-
-class Checkpoint:
-  """Pickles {iteration, agents' get_state(), random_state, writer} next to
-  the results CSV (parts.py:517-561).  Device tensors in agent states are
-  converted to numpy by the agents' get_state()."""
-
-  def __init__(self):
-    self.state = AttributeDict()
-
-  @property
-  def filepath(self) -> str:
-    return os.path.splitext(self.state.writer._fname)[0] + '.chkpt'  # pylint: disable=protected-access
-
-  def save(self) -> None:
-    payload = {'iteration': self.state.iteration,
-               'train_agent': self.state.train_agent.get_state(),
-               'eval_agent': self.state.eval_agent.get_state(),
-               'random_state': self.state.random_state,
-               'writer': self.state.writer.get_state()}
-    try:
-      with open(self.filepath, 'wb') as f:
-        pickle.dump(payload, f)
-    except Exception:
-      if os.path.exists(self.filepath):
-        os.remove(self.filepath)
-      raise
-
-  def can_be_restored(self) -> bool:
-    return os.path.isfile(self.filepath)
-
-  def restore(self) -> None:
-    with open(self.filepath, 'rb') as f:  # our own file format
-      payload = pickle.load(f)
-    self.state.iteration = payload['iteration']
-    self.state.train_agent.set_state(payload['train_agent'])
-    self.state.eval_agent.set_state(payload['eval_agent'])
-    self.state.random_state = payload['random_state']
-    self.state.writer.set_state(payload['writer'])
-    self.state.writer._header_written = True  # pylint: disable=protected-access

@@ -270,6 +270,13 @@ class _StorageMixin:
       self._backend = self._make_backend(backend_state.get('kind') == 'device')
     self._backend.set_state(backend_state)
 
+  def stores_on_device(self, item) -> bool:
+    """Whether `item` is (or, on the first add, will be) stored in HBM."""
+    if self._backend is not None:
+      return self._backend.device
+    device = self._backend_args[3]
+    return bool(device) if device is not None else is_frame_transition(item)
+
   @property
   def on_device(self) -> bool:
     return self._backend is not None and self._backend.device
@@ -367,6 +374,10 @@ class TransitionReplay(_StorageMixin):
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
     self._restore_backend(state.get('backend'))
+    if self._distribution.on_device:
+      self._sync_index_map()
+    elif self.on_device:
+      self._device_tree()
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._order):
@@ -615,6 +626,115 @@ class SumTree:
     return node - self._first_leaf
 
 
+class _DeviceSumTree:
+  """The SumTree's fp64 storage in HBM (same implicit layout: root at 1,
+  leaves from `capacity`), for replays whose transitions live on device.
+
+  Writes go through libdqz (`dqz_sumtree_set`, `dqz_per_add`,
+  `dqz_per_write_back`: ancestors rebuilt as left + right, bit-identical to
+  SumTree.set).  Host reads (`get`, `root`, `storage`, state) copy back and
+  synchronise; the learner path never makes them.  Also owns the device map
+  tree index -> replay slot the sampler uses.
+  """
+
+  def __init__(self, host_tree: SumTree, device):
+    import torch  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+    self._torch, self._native = torch, _native
+    self._size = host_tree.size
+    cap = max(host_tree.capacity, 1)
+    self._first_leaf = cap
+    st = np.zeros((2 * cap,), np.float64)
+    st[:len(host_tree.storage)] = host_tree.storage
+    self.tree = torch.from_numpy(st).to(device)
+    self.index_to_slot = torch.zeros((cap,), dtype=torch.int32, device=device)
+
+  def _check(self, rc):
+    return self._native.check(rc)
+
+  def resize(self, size: int) -> None:
+    if size > self._first_leaf:
+      raise ValueError('the device sum tree has a fixed capacity of %d leaves'
+                       % self._first_leaf)
+    if size < self._size:
+      self.tree[self._first_leaf + size:] = 0.0
+      self._rebuild()
+    self._size = size
+
+  def _rebuild(self):
+    st = self.tree.cpu().numpy()
+    fl = self._first_leaf
+    for i in range(fl - 1, 0, -1):
+      st[i] = st[2 * i] + st[2 * i + 1]
+    self.tree.copy_(self._torch.from_numpy(st))
+
+  def get(self, indices: Sequence[int]) -> np.ndarray:
+    indices = np.asarray(indices)
+    if not ((0 <= indices) & (indices < self.size)).all():
+      raise IndexError('index out of range, expect 0 <= index < %s' % self.size)
+    return self.values[indices]
+
+  def set(self, indices: Sequence[int], values: Sequence[float]) -> None:
+    values = np.asarray(values, np.float64)
+    if not np.isfinite(values).all() or (values < 0.0).any():
+      raise ValueError('value must be finite and positive.')
+    indices = np.asarray(indices, np.int64).reshape(-1)
+    if indices.size == 0:
+      return
+    last = {}
+    for i, v in zip(indices.tolist(), np.broadcast_to(values, indices.shape).tolist()):
+      last[i] = v  # numpy fancy assignment: the last write of an index wins
+    t = self._torch
+    idx = t.tensor(list(last.keys()), dtype=t.int64).to(self.tree.device, non_blocking=True)
+    val = t.tensor(list(last.values()), dtype=t.float64).to(self.tree.device, non_blocking=True)
+    n = self._native
+    self._check(n.lib().dqz_sumtree_set(n.ptr(self.tree), self._first_leaf, n.ptr(idx),
+                                        n.ptr(val), len(last), n.stream_handle()))
+
+  def per_add(self, remove_index, add_index, priority, max_seen_dev, alpha, slot):
+    n = self._native
+    self._check(n.lib().dqz_per_add(
+        n.ptr(self.tree), self._first_leaf, int(remove_index), int(add_index),
+        float(priority), n.ptr(max_seen_dev), float(alpha),
+        n.ptr(self.index_to_slot), int(slot), n.stream_handle()))
+
+  def root(self) -> float:
+    return float(self.tree[1].item()) if self.size > 0 else np.nan
+
+  @property
+  def values(self) -> np.ndarray:
+    fl = self._first_leaf
+    return self.tree[fl:fl + self.size].cpu().numpy()
+
+  @property
+  def size(self) -> int:
+    return self._size
+
+  @property
+  def capacity(self) -> int:
+    return self._first_leaf
+
+  @property
+  def storage(self) -> np.ndarray:
+    return self.tree.cpu().numpy()
+
+  def get_state(self) -> Mapping[str, Any]:
+    return {'size': self._size, 'storage': self.storage,
+            'first_leaf': self._first_leaf}
+
+  def set_state(self, state: Mapping[str, Any]) -> None:
+    if state['first_leaf'] != self._first_leaf:
+      raise ValueError('sum tree capacity mismatch: %d vs %d' %
+                       (state['first_leaf'], self._first_leaf))
+    self._size = state['size']
+    self.tree.copy_(self._torch.from_numpy(np.asarray(state['storage'], np.float64)))
+
+  def check_valid(self) -> Tuple[bool, str]:
+    host = SumTree()
+    host.set_state(self.get_state())
+    return host.check_valid()
+
+
 class PrioritizedDistribution:
   """Proportional prioritized sampling of integer IDs (replay.py:562-784)."""
 
@@ -645,6 +765,39 @@ class PrioritizedDistribution:
   def sum_tree(self) -> SumTree:
     return self._sum_tree
 
+  @property
+  def priority_exponent(self) -> float:
+    return self._priority_exponent
+
+  @property
+  def uniform_sample_probability(self) -> float:
+    return self._uniform_sample_probability
+
+  @property
+  def on_device(self) -> bool:
+    return isinstance(self._sum_tree, _DeviceSumTree)
+
+  def to_device(self, device) -> None:
+    """Moves the tree into HBM (fixed capacity from here on)."""
+    if not self.on_device:
+      self._sum_tree = _DeviceSumTree(self._sum_tree, device)
+
+  def draw(self, size: int):
+    """The three random streams of sample(), in the reference's order
+    (replay.py:684-697): tree indices of the uniform picks, target
+    fractions, usp-mix uniforms.  The target fractions are drawn whatever
+    the root (the reference skips them only while every priority is 0)."""
+    if self.size == 0:
+      raise RuntimeError('No IDs to sample.')
+    rs = self._random_state
+    uniform_idx = np.array([self._active_indices[j]
+                            for j in rs.randint(self.size, size=size)], np.int32)
+    u = np.concatenate([rs.uniform(size=size), rs.uniform(size=size)])
+    return uniform_idx, u
+
+  def index_to_id(self, indices) -> np.ndarray:
+    return np.array([self._index_to_id[int(i)] for i in indices], dtype=np.int64)
+
   def ensure_capacity(self, capacity: int) -> None:
     if self._max_capacity is not None and capacity > self._max_capacity:
       raise ValueError('capacity %d cannot exceed max_capacity %d' %
@@ -654,7 +807,8 @@ class PrioritizedDistribution:
     self._inactive_indices.extend(range(self._sum_tree.size, capacity))
     self._sum_tree.resize(capacity)
 
-  def add_priorities(self, ids: Sequence[int], priorities: Sequence[float]) -> None:
+  def _assign_indices(self, ids: Sequence[int]):
+    """add_priorities' bookkeeping: checks, growth, tree indices for ids."""
     for i in ids:
       if i in self._id_to_index:
         raise IndexError('ID %d already exists.' % i)
@@ -674,10 +828,10 @@ class PrioritizedDistribution:
       self._id_to_index[i] = idx
       self._index_to_id[idx] = i
       indices.append(idx)
-    self._sum_tree.set(indices, _power(priorities, self._priority_exponent))
     return indices
 
-  def remove_priorities(self, ids: Sequence[int]) -> None:
+  def _release_indices(self, ids: Sequence[int]):
+    """remove_priorities' bookkeeping (swap-remove); the freed indices."""
     indices = [self._id_to_index[i] for i in ids]  # KeyError if absent
     for i, idx in zip(ids, indices):
       del self._id_to_index[i]
@@ -689,6 +843,15 @@ class PrioritizedDistribution:
       self._active_indices.pop()
       del self._active_indices_location[idx]
     self._inactive_indices.extend(indices)
+    return indices
+
+  def add_priorities(self, ids: Sequence[int], priorities: Sequence[float]) -> None:
+    indices = self._assign_indices(ids)
+    self._sum_tree.set(indices, _power(priorities, self._priority_exponent))
+    return indices
+
+  def remove_priorities(self, ids: Sequence[int]) -> None:
+    indices = self._release_indices(ids)
     self._sum_tree.set(indices, np.zeros((len(indices),), dtype=np.float64))
     return indices
 
@@ -808,8 +971,15 @@ class PrioritizedTransitionReplay(_StorageMixin):
   def _slot(self, item_id):
     return item_id % self._capacity
 
-  def add(self, item, priority: float) -> None:
+  def add(self, item, priority) -> None:
+    """`priority` is a float, or — for a device replay — a device f64 [1]
+    tensor (the agent's running max_seen_priority, read on device)."""
     backend = self._storage_for(item)
+    if backend.device:
+      self._add_device(backend, item, priority)
+      return
+    if not isinstance(priority, (int, float, np.floating, np.integer)):
+      priority = float(priority.item())
     if self.size == self._capacity:
       oldest_id, _ = self._order.popitem(last=False)
       self._distribution.remove_priorities([oldest_id])
@@ -822,14 +992,104 @@ class PrioritizedTransitionReplay(_StorageMixin):
     self._order[item_id] = None
     self._t += 1
 
+  def _device_tree(self):
+    dist = self._distribution
+    if not dist.on_device:
+      dist.to_device(self._backend.store.device)
+      self._sync_index_map()
+    return dist.sum_tree
+
+  def _sync_index_map(self):
+    """index_to_slot of every live ID (after a restore)."""
+    import torch  # pylint: disable=g-import-not-at-top
+    dist = self._distribution
+    ids = list(self._order)
+    if not ids:
+      return
+    idx = torch.as_tensor(dist.index_of(ids), dtype=torch.int64)
+    slots = torch.as_tensor(np.asarray(ids, np.int64) % self._capacity,
+                            dtype=torch.int32)
+    m = dist.sum_tree.index_to_slot
+    m[idx.to(m.device)] = slots.to(m.device)
+
+  def _add_device(self, backend, item, priority) -> None:
+    """One dqz_per_add launch: evicted leaf -> 0, new leaf -> p ** alpha,
+    tree index -> slot; ID bookkeeping stays on the host."""
+    tree = self._device_tree()
+    dist = self._distribution
+    remove = -1
+    if self.size == self._capacity:
+      oldest_id, _ = self._order.popitem(last=False)
+      remove = dist._release_indices([oldest_id])[0]  # pylint: disable=protected-access
+      backend.drop(self._slot(oldest_id))
+    item_id = self._t
+    add = dist._assign_indices([item_id])[0]  # pylint: disable=protected-access
+    if isinstance(priority, (int, float, np.floating, np.integer)):
+      p, max_seen = float(priority), None
+      if not (np.isfinite(p) and p >= 0.0):
+        raise ValueError('value must be finite and positive.')
+    else:
+      p, max_seen = -1.0, priority
+    tree.per_add(remove, add, p, max_seen, dist.priority_exponent,
+                 self._slot(item_id))
+    oldest = next(iter(self._order)) if self._order else None
+    backend.put(self._slot(item_id), item,
+                None if oldest is None else self._slot(oldest))
+    self._order[item_id] = None
+    self._t += 1
+
   def get(self, ids: Sequence[int]) -> Iterable[Any]:
     for i in ids:
       if i not in self._order:
         raise KeyError(i)
       yield self._backend.get(self._slot(i))
 
+  def sample_device(self, size: int, out=None):
+    """Device sample for the learner: (tree indices, slots, weights), device
+    int32 / int32 / f32 [size], drawn with the caller's RandomState in the
+    reference's order and resolved on device (dqz_per_sample) — no host
+    synchronisation.  `out` may pass preallocated tensors."""
+    import torch  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+    tree = self._device_tree()
+    dist = self._distribution
+    dev = tree.tree.device
+    uniform_idx, u = dist.draw(size)
+    inj_i = torch.from_numpy(uniform_idx).pin_memory().to(dev, non_blocking=True)
+    inj_u = torch.from_numpy(u).pin_memory().to(dev, non_blocking=True)
+    if out is None:
+      out = (torch.empty((size,), dtype=torch.int32, device=dev),
+             torch.empty((size,), dtype=torch.int32, device=dev),
+             torch.empty((size,), dtype=torch.float32, device=dev))
+    indices, slots, weights = out
+    beta = self.importance_sampling_exponent
+    if not 0.0 <= beta <= 1.0:
+      raise ValueError('Require 0 <= exponent <= 1.')
+    _native.check(_native.lib().dqz_per_sample(
+        _native.ptr(tree.tree), tree.capacity, 0, self.size, self._capacity,
+        int(size), float(dist.uniform_sample_probability), float(beta),
+        int(bool(self._normalize_weights)), 0, None, _native.ptr(inj_i),
+        _native.ptr(inj_u), _native.ptr(tree.index_to_slot),
+        _native.ptr(indices), _native.ptr(slots), _native.ptr(weights), None,
+        _native.stream_handle()))
+    return indices, slots, weights
+
+  def write_back(self, learner, indices, max_seen_dev) -> None:
+    """|td| of the learner's last step -> max_seen_priority -> priorities of
+    the sampled tree indices (prioritized/agent.py:201-206), one launch."""
+    from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+    tree = self._device_tree()
+    _native.check(_native.lib().dqz_per_write_back(
+        learner._h, _native.ptr(tree.tree), tree.capacity, _native.ptr(indices),  # pylint: disable=protected-access
+        float(self._distribution.priority_exponent), _native.ptr(max_seen_dev),
+        _native.stream_handle()))
+
   def sample_ids(self, size: int):
     """(ids, normalised importance weights) as the reference computes them."""
+    if self._distribution.on_device:
+      indices, _, weights = self.sample_device(size)
+      ids = self._distribution.index_to_id(indices.cpu().numpy())
+      return ids, weights.cpu().numpy().astype(np.float64)
     ids, probabilities = self._distribution.sample(size)
     weights = importance_sampling_weights(
         probabilities, uniform_probability=1.0 / self.size,
@@ -875,6 +1135,10 @@ class PrioritizedTransitionReplay(_StorageMixin):
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
     self._restore_backend(state.get('backend'))
+    if self._distribution.on_device:
+      self._sync_index_map()
+    elif self.on_device:
+      self._device_tree()
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._order):

@@ -258,7 +258,8 @@ int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out,
 /* Priority write-back of the learner's last step (prioritized/agent.py:201-206,
  * replay.py:620-630): p = |td| (fp64 of the f32 TD errors), *max_seen_dev =
  * max(*max_seen_dev, max p), leaf[slots[i]] = p^alpha (0 -> 0) with the sum
- * tree's ancestors rebuilt (a slot drawn twice keeps its last draw).  All
+ * tree's ancestors rebuilt (a tree index drawn twice keeps its last draw;
+ * `slots` holds tree indices, dqz_per_sample's out_indices).  All
  * device pointers; one launch, no host synchronisation.  Batch <= 256. */
 int dqz_per_write_back(dqz_learner* learner, double* tree, int64_t cap, const int32_t* slots, double alpha,
                        double* max_seen_dev, void* stream);
@@ -275,13 +276,30 @@ int dqz_sumtree_query(const double* tree, int64_t cap, const double* targets, in
                       void* stream);
 
 /* PrioritizedDistribution.sample + importance_sampling_weights on device
- * (replay.py:680-716, 344-376) with Philox draws; tree leaf index = replay
- * slot; live slots are (live_base + j) mod capacity, j < size.  n <= 1024.
- * out_probs (device f64 [n]) may be NULL. */
+ * (replay.py:680-716, 344-376).  Draws: injected_u == NULL -> device Philox
+ * (seed, *counter_dev; the counter is advanced), tree leaf index = replay
+ * slot, uniform picks over the live window (live_base + j) mod capacity.
+ * injected_u != NULL -> the caller's RandomState draws in the reference's
+ * order: injected_uniform[i] = active_indices[randint(size)[i]] (a tree
+ * index), injected_u[i] = uniform target fraction, injected_u[n + i] = the
+ * usp-mix uniform; counter_dev is ignored.  index_to_slot (device int32
+ * [cap], or NULL for identity) maps tree indices to replay slots.
+ * out_indices (tree indices) and out_probs (f64) may be NULL.  n <= 1024. */
 int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t size, int64_t capacity,
                    int n, double uniform_sample_probability, double importance_exponent,
-                   int normalize_weights, uint64_t seed, uint64_t* counter_dev, int32_t* out_slots,
-                   float* out_weights, double* out_probs, void* stream);
+                   int normalize_weights, uint64_t seed, uint64_t* counter_dev,
+                   const int32_t* injected_uniform, const double* injected_u, const int32_t* index_to_slot,
+                   int32_t* out_indices, int32_t* out_slots, float* out_weights, double* out_probs,
+                   void* stream);
+
+/* PrioritizedTransitionReplay.add on device (replay.py:1068-1096 ->
+ * PrioritizedDistribution.remove_priorities / add_priorities, :642-678): the
+ * evicted tree index remove_index (-1: none) is set to 0, add_index to
+ * _power(priority, alpha) -- priority < 0 reads the agent's running
+ * max_seen_priority from max_seen_dev (prioritized/agent.py:155) -- and
+ * index_to_slot[add_index] = slot.  One launch, no host synchronisation. */
+int dqz_per_add(double* tree, int64_t cap, int32_t remove_index, int32_t add_index, double priority,
+                const double* max_seen_dev, double alpha, int32_t* index_to_slot, int32_t slot, void* stream);
 
 /* Target sync: target <- online (dqn/agent.py:155-156; hard copy, not Polyak). */
 int dqz_target_copy(float* target, const float* online, int64_t total, void* stream);

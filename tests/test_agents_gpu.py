@@ -146,32 +146,37 @@ def test_agent_learner_step_matches_oracle(device, kind):
 
 
 def test_per_priorities_after_learning(device):
+  """The device PER learn: sampled tree leaves become |td| ** alpha and
+  max_seen_priority the running max (prioritized/agent.py:201-206)."""
   from dqn_mgsc_zoo_amd import replay as replay_lib
   agent, replay = _make('per', seed=3)
   _run(agent, 100)
+  assert replay.on_device and replay.distribution.on_device
   captured = {}
-  orig = replay.update_priorities
+  orig = replay.sample_device
 
-  def spy(ids, priorities):
-    captured['ids'] = np.array(ids)
-    captured['p'] = np.array(priorities, np.float64)
-    return orig(ids, priorities)
+  def spy(size, out=None):
+    res = orig(size, out=out)
+    captured['idx'] = res[0].clone()
+    return res
 
-  replay.update_priorities = spy
+  replay.sample_device = spy
+  before = agent.max_seen_priority
   agent._learn()  # pylint: disable=protected-access
   _, td, _ = agent.learner.fetch_outputs()
-  np.testing.assert_array_equal(captured['p'],
-                                np.abs(td.cpu().numpy().astype(np.float64)))
-  dist = replay._distribution  # pylint: disable=protected-access
-  # last write wins for duplicated ids
-  last = {}
-  for i, p in zip(captured['ids'], captured['p']):
-    last[int(i)] = p
-  idx = [dist._id_to_index[i] for i in last]  # pylint: disable=protected-access
+  p = np.abs(td.cpu().numpy().astype(np.float64))
+  assert agent.max_seen_priority == max(before, p.max())
+  last = {}  # last write wins for duplicated draws
+  for i, v in zip(captured['idx'].cpu().numpy().tolist(), p.tolist()):
+    last[i] = v
+  tree = replay.distribution.sum_tree
+  leaves = tree.storage[tree.capacity:]
   np.testing.assert_allclose(
-      dist.sum_tree.get(idx),
+      leaves[list(last)],
       replay_lib._power(np.array(list(last.values())), 0.6),  # pylint: disable=protected-access
-      rtol=1e-12)
+      rtol=1e-15)
+  ok, msg = replay.check_valid()
+  assert ok, msg
 
 
 @pytest.mark.parametrize('kind', ['dqn', 'per'])

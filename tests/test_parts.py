@@ -96,17 +96,6 @@ def test_linear_schedule():
     parts.LinearSchedule(1.0, 0.0, 0)
 
 
-def test_episode_tracker_and_statistics():
-  tape = []
-  seq = parts.run_loop(TapeAgent(tape), TapeEnv(tape, 3))
-  import itertools
-  stats = parts.generate_statistics(
-      [parts.EpisodeTracker(), parts.StepRateTracker()],
-      itertools.islice(seq, 9))
-  assert stats['num_episodes'] == 2
-  assert stats['episode_return'] == 6.0  # 3 rewards of 2.0, FIRST ignored
-
-
 def test_epsilon_greedy_probs_ties():
   p = parts.epsilon_greedy_probs([1.0, 3.0, 3.0, 0.0], 0.2)
   np.testing.assert_allclose(p, [0.05, 0.45, 0.45, 0.05])

@@ -6,7 +6,11 @@
 * fp64 sum tree: device storage bit-identical to the host SumTree after the
   same set() calls; device queries identical to host queries.
 * device PER sampler: frequencies vs (1-usp) p^a/sum + usp/N (rtol as the
-  reference's statistical test), weights = (1/N / prob)^beta / max.
+  reference's statistical test), weights = (1/N / prob)^beta / max; with the
+  reference RandomState's draws injected, ids and probabilities equal the
+  reference's golden vectors index for index (distribution level) and the
+  device-resident prioritized replay reproduces the golden replay log (ids,
+  stored items, importance weights) through add / sample / update.
 """
 
 import ctypes
@@ -178,7 +182,7 @@ def test_per_device_sampler_distribution(device):
   for _ in range(60):
     _native.check(lib.dqz_per_sample(
         _native.ptr(dev), cap, 0, cap, cap, n, usp, beta, 1, 77,
-        _native.ptr(counter), _native.ptr(slots), _native.ptr(w),
+        _native.ptr(counter), None, None, None, None, _native.ptr(slots), _native.ptr(w),
         _native.ptr(probs), _native.stream_handle()))
     s = slots.cpu().numpy()
     counts += np.bincount(s, minlength=cap)
@@ -224,3 +228,145 @@ def test_sumtree_query_large_tree_boundaries(device):
                                       _native.ptr(dt), targets.size,
                                       _native.ptr(out), _native.stream_handle()))
   assert out.cpu().numpy().tolist() == list(host.query(targets))
+
+
+def test_per_device_sampler_injected_matches_golden_distribution(device):
+  """PrioritizedDistribution.sample (replay.py:680-716) on device, fed the
+  reference RandomState(3)'s own draws: ids and probabilities bit-equal to
+  the goldens recorded from the reference."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  g = GOLDEN['prioritized']['distribution']
+  rs = np.random.RandomState(g['seed'])
+  d = replay_lib.PrioritizedDistribution(g['exponent'], g['usp'], rs, 0, None)
+  for op, ids, prios in [o + [None] * (3 - len(o)) for o in g['ops']]:
+    if op == 'add':
+      d.add_priorities(ids, prios)
+    elif op == 'update':
+      d.update_priorities(ids, prios)
+    else:
+      d.remove_priorities(ids)
+  n = len(g['ids'])
+  host_tree = d.sum_tree
+  d.to_device(device)
+  tree = d.sum_tree
+  assert np.array_equal(tree.storage[1:2 * host_tree.capacity],
+                        host_tree.storage[1:])
+  uniform_idx, u = d.draw(n)
+  inj_i = torch.from_numpy(uniform_idx).to(device)
+  inj_u = torch.from_numpy(u).to(device)
+  idx = torch.empty(n, dtype=torch.int32, device=device)
+  slots = torch.empty(n, dtype=torch.int32, device=device)
+  w = torch.empty(n, dtype=torch.float32, device=device)
+  probs = torch.empty(n, dtype=torch.float64, device=device)
+  lib = _native.lib()
+  _native.check(lib.dqz_per_sample(
+      _native.ptr(tree.tree), tree.capacity, 0, d.size, tree.capacity, n,
+      g['usp'], 0.5, 1, 0, None, _native.ptr(inj_i), _native.ptr(inj_u), None,
+      _native.ptr(idx), _native.ptr(slots), _native.ptr(w), _native.ptr(probs),
+      _native.stream_handle()))
+  got_idx = idx.cpu().numpy()
+  assert d.index_to_id(got_idx).tolist() == g['ids']
+  assert slots.cpu().numpy().tolist() == got_idx.tolist()  # identity map
+  assert probs.cpu().numpy().tolist() == g['probs']  # bit-exact fp64
+  want_w = replay_lib.importance_sampling_weights(np.array(g['probs']),
+                                                  1.0 / d.size, 0.5, True)
+  np.testing.assert_allclose(w.cpu().numpy(), want_w.astype(np.float32),
+                             rtol=2e-7)
+
+
+def _frame(v):
+  return np.full((84, 84, 4), v, dtype=np.uint8)
+
+
+@pytest.mark.parametrize('case', [0, 1])
+def test_device_prioritized_replay_reproduces_golden_log(device, case):
+  """PrioritizedTransitionReplay (replay.py:1046-1160) with its sum tree in
+  HBM: frame transitions, RandomState(seed) as in the golden run; every
+  sample's ids, items and importance weights equal the reference's, and
+  the device tree equals the host mirror's after the same operations."""
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  g = GOLDEN['prioritized']['replay'][case]
+  structure = replay_lib.Transition(None, None, None, None, None)
+
+  def make():
+    return replay_lib.PrioritizedTransitionReplay(
+        capacity=8, structure=structure, priority_exponent=0.6,
+        importance_sampling_exponent=lambda t: 0.4,
+        uniform_sample_probability=0.1, normalize_weights=True,
+        random_state=np.random.RandomState(g['seed']))
+
+  r = make()
+  host = make()
+  log = iter(g['log'])
+  for i, p in enumerate(g['priorities']):
+    tr = replay_lib.Transition(_frame(i), 0, 0.0, 1.0, _frame(i))
+    r.add(tr, priority=p)
+    host.add(replay_lib.Transition(i, 0, 0.0, 1.0, i), priority=p)
+    assert r.on_device and r.distribution.on_device
+    if i < 3:
+      continue
+    want = next(log)
+    indices, slots, weights = r.sample_device(5)
+    ids = r.distribution.index_to_id(indices.cpu().numpy())
+    assert ids.tolist() == want['ids']
+    assert (slots.cpu().numpy() == ids % 8).all()
+    items = r.frame_store.gather_stacks(slots, 0).cpu().numpy()[:, 0, 0, 0]
+    assert items.tolist() == want['items']
+    np.testing.assert_allclose(weights.cpu().numpy(),
+                               np.float32(want['weights']), rtol=2e-7)
+    _, host_ids, _ = host.sample(5)
+    assert host_ids.tolist() == want['ids']
+    uids, uprios = want['update']
+    r.update_priorities(uids, uprios)
+    host.update_priorities(uids, uprios)
+    np.testing.assert_array_equal(r.distribution.sum_tree.storage[1:],
+                                  host.distribution.sum_tree.storage[1:])
+  ok, msg = r.check_valid()
+  assert ok, msg
+
+
+def test_device_per_add_and_write_back(device):
+  """dqz_per_add (evict -> 0, new leaf -> max_seen ** alpha, tree index ->
+  slot) and dqz_per_write_back (|td| -> max_seen -> leaves) against the host
+  SumTree arithmetic."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  from dqn_mgsc_zoo_amd import store as store_lib
+  alpha = 0.6
+  r = replay_lib.PrioritizedTransitionReplay(
+      capacity=16, structure=replay_lib.Transition(None, None, None, None, None),
+      priority_exponent=alpha, importance_sampling_exponent=lambda t: 0.4,
+      uniform_sample_probability=1e-3, normalize_weights=True,
+      random_state=np.random.RandomState(5))
+  max_seen = torch.full((1,), 2.5, dtype=torch.float64, device=device)
+  for i in range(40):  # wraps the FIFO twice: every add also evicts
+    r.add(replay_lib.Transition(_frame(i), i % 6, 0.0, 0.99, _frame(i + 1)),
+          priority=max_seen if i % 3 else 0.75)
+  d = r.distribution
+  live = list(r._order)  # pylint: disable=protected-access
+  vals = d.get_exponentiated_priorities(live)
+  want = [np.float64(0.75)**alpha if i % 3 == 0 else np.float64(2.5)**alpha for i in live]
+  np.testing.assert_allclose(vals, want, rtol=1e-15)
+  host = replay_lib.SumTree()
+  host.resize(16)
+  host.set(d.index_of(live), vals)
+  np.testing.assert_array_equal(d.sum_tree.storage[1:], host.storage[1:])
+  m = d.sum_tree.index_to_slot.cpu().numpy()
+  assert [int(m[d.index_of([i])[0]]) for i in live] == [i % 16 for i in live]
+  # write-back of a learner step's |td|
+  net = networks.double_dqn_atari_network(6)
+  lrn = learner_lib.Learner(net, 32, algo='per')
+  lrn.set_params(net.init(3))
+  indices, slots, w = r.sample_device(32)
+  lrn.step(r.frame_store, slots, w)
+  r.write_back(lrn, indices, max_seen)
+  _, td, _ = lrn.fetch_outputs()
+  p = np.abs(td.cpu().numpy().astype(np.float64))
+  assert max_seen.item() == max(2.5, p.max())
+  last = {}
+  for k, v in zip(indices.cpu().numpy().tolist(), p.tolist()):
+    last[k] = v
+  host.set(list(last), replay_lib._power(np.array(list(last.values())), alpha))  # pylint: disable=protected-access
+  np.testing.assert_allclose(d.sum_tree.storage[1:], host.storage[1:], rtol=1e-15)

@@ -105,7 +105,8 @@ def main():
   def per_step():
     _native.check(lib.dqz_per_sample(
         _native.ptr(tree), tcap, 0, cap, cap, B, ctypes.c_double(1e-3), ctypes.c_double(0.4), 1, 11,
-        _native.ptr(p_ctr), _native.ptr(p_slots), _native.ptr(p_w), None, _native.stream_handle()))
+        _native.ptr(p_ctr), None, None, None, None, _native.ptr(p_slots), _native.ptr(p_w), None,
+        _native.stream_handle()))
     lrn_p.step(store, p_slots, p_w)
     _native.check(lib.dqz_per_write_back(lrn_p._h, _native.ptr(tree), tcap, _native.ptr(p_slots),  # pylint: disable=protected-access
                                          ctypes.c_double(0.6), _native.ptr(max_seen), _native.stream_handle()))
