@@ -540,7 +540,7 @@ __global__ __launch_bounds__(ST_FAST) void per_add_kernel(double* tree, int64_t 
   if (i == 0 && remove_idx >= 0 && remove_idx != add_idx) leaf = cap + remove_idx;
   if (i == 1) {
     const double p = priority >= 0.0 ? priority : *max_seen;
-    v = p == 0.0 ? 0.0 : pow(p, alpha);
+    v = p == 0.0 ? 0.0 : (alpha == 1.0 ? p : pow(p, alpha));  // alpha 1: host-exponentiated
     leaf = cap + add_idx;
   }
   sumtree_set_small_body(tree, levels, 2, leaf, v);

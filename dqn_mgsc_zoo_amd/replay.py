@@ -374,10 +374,6 @@ class TransitionReplay(_StorageMixin):
     self._t = state['t']
     self._distribution.set_state(state['distribution'])
     self._restore_backend(state.get('backend'))
-    if self._distribution.on_device:
-      self._sync_index_map()
-    elif self.on_device:
-      self._device_tree()
 
   def check_valid(self) -> Tuple[bool, str]:
     if self._t < len(self._order):
@@ -1025,13 +1021,15 @@ class PrioritizedTransitionReplay(_StorageMixin):
     item_id = self._t
     add = dist._assign_indices([item_id])[0]  # pylint: disable=protected-access
     if isinstance(priority, (int, float, np.floating, np.integer)):
-      p, max_seen = float(priority), None
+      # host priority: exponentiated here with numpy, like the reference
+      # (SumTree leaves bit-equal to the host path); the kernel's ** 1 is exact
+      p = float(_power(float(priority), dist.priority_exponent))
       if not (np.isfinite(p) and p >= 0.0):
         raise ValueError('value must be finite and positive.')
+      tree.per_add(remove, add, p, None, 1.0, self._slot(item_id))
     else:
-      p, max_seen = -1.0, priority
-    tree.per_add(remove, add, p, max_seen, dist.priority_exponent,
-                 self._slot(item_id))
+      tree.per_add(remove, add, -1.0, priority, dist.priority_exponent,
+                   self._slot(item_id))
     oldest = next(iter(self._order)) if self._order else None
     backend.put(self._slot(item_id), item,
                 None if oldest is None else self._slot(oldest))
