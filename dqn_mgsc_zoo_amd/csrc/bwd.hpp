@@ -355,19 +355,23 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
   f32x4 acc[9];
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp) acc[tp] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A = dy3 (rows: co), B = the y2 patch (columns: ci): a lane's four
+  // accumulators are four consecutive co of one (tap, ci) row, stored as one
+  // float4 (the products and their k order are those of the transposed form,
+  // so the values are the same bits)
 #pragma unroll
   for (int kk = 0; kk < 13; ++kk)
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const int off = (tp / 3) * C3W_RS + (tp % 3) * C3W_S;
-      acc[tp] = mfma4(s_win[pb[kk] + off], dr[kk], acc[tp]);
+      acc[tp] = mfma4(dr[kk], s_win[pb[kk] + off], acc[tp]);
     }
-  // C layout: row = 4 kq + r -> ci = 16 w + 4 kq + r of tap tp; col = co = n
-  float* part = a.part + (int64_t)b * (C3KK + 1) * C3CO + 16 * nq + n;
+  // C layout: row = 4 kq + r -> co = 16 nq + 4 kq + r; col = n -> ci = 16 w + n of tap tp
+  float* slab = a.part + (int64_t)b * (C3KK + 1) * C3CO;
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) part[(tp * C3CI + 16 * w + 4 * kq + rr) * C3CO] = acc[tp][rr];
+    *reinterpret_cast<f32x4*>(slab + (tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) = acc[tp];
+  float* part = slab + 16 * nq + n;
   if (w == 0) {  // bias row: sum over positions, lanes kq = 0..3 hold p = 4 kk + kq
     float sb = 0.f;
 #pragma unroll
@@ -556,22 +560,25 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A = dy2 (rows: co), B = y1 (columns: ci): a lane's accumulators are four
+  // consecutive co, stored as one float4 (same bits as the transposed form)
 #pragma unroll
   for (int kk = 0; kk < 21; ++kk)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const float av = s_win[pb[kk] + 16 * mt];
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = mfma4(av, dr[kk][ct], acc[mt][ct]);
+      for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = mfma4(dr[kk][ct], av, acc[mt][ct]);
     }
-  float* part = a.part + (int64_t)b * (C2KK + 1) * C2CO + 32 * ch + n;
+  // C: row 4 kq + r -> co = 32 ch + 16 ct + 4 kq + r; col n -> ci = 16 mt + n
+  float* slab = a.part + (int64_t)b * (C2KK + 1) * C2CO;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        part[((kh * C2K + w) * C2CI + 16 * mt + 4 * kq + rr) * C2CO + 16 * ct] = acc[mt][ct][rr];
+      *reinterpret_cast<f32x4*>(slab + ((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq) =
+          acc[mt][ct];
+  float* part = slab + 32 * ch + n;
   if (kh == 0 && w == 0) {  // bias row (per lane over kk, then over kq)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {

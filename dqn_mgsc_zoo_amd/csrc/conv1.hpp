@@ -250,14 +250,18 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
     const int p0 = 2 * jj;  // positions p0 + h share an output row
     const float av = pa[(C1S * (p0 / C1O)) * FW + C1S * (p0 % C1O)];
     const float bv = pb[64 * jj];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    // A = dy1 (rows: co), B = the frame patch (columns: dW row m): four
+    // consecutive co per accumulator group, same bits as the transposed form
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv, av, acc, 0, 0, 0);
   }
-  // C row m = (r & 3) + 8 (r >> 2) + 4 h -> kh = 2 wave + (m >> 4), kw = (m >> 1) & 7, ci = 2 ch + (m & 1)
+  // C col = lane & 31 = m -> kh = 2 wave + (m >> 4), kw = (m >> 1) & 7, ci = 2 ch + (m & 1);
+  // rows co = (r & 3) + 8 (r >> 2) + 4 h: one float4 store per r >> 2
+  {
+    const int row = (2 * wave + (i >> 4)) * 32 + ((i >> 1) & 7) * 4 + 2 * ch + (i & 1);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int row = (2 * wave + (m >> 4)) * 32 + ((m >> 1) & 7) * 4 + 2 * ch + (m & 1);
-    part[row * C1CO + i] = acc[r];
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<f32x4*>(part + row * C1CO + 8 * q + 4 * h) =
+          f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
   }
   DQZ_STAMP(8, 3);
 }
