@@ -608,9 +608,10 @@ int dqz_gather_stacks(const dqz_store* S, const int32_t* slots, int n, int which
 struct dqz_logit_buffer {
   int64_t capacity;
   int nblocks, max_queries;
-  void* block;  // MaxSum[nblocks] | double bsum[nblocks] | float lse
+  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | int minlsb[nblocks] | float lse
   MaxSum* part;
   double* bsum;
+  int* minlsb;
   float* lse;
 };
 
@@ -620,7 +621,7 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->capacity = capacity;
   b->max_queries = max_queries;
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
-  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double)) + 64;
+  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int)) + 64;
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
@@ -628,7 +629,8 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   char* p = (char*)b->block;
   b->bsum = (double*)p;
   b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
-  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
+  b->minlsb = (int*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
+  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum) + sizeof(int)));
   *out = b;
   return DQZ_OK;
 }
@@ -673,11 +675,23 @@ int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* un
   hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
                      b->capacity, b->part, (int64_t)-1);
   hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
-                     b->nblocks, b->lse, b->bsum);
+                     b->nblocks, b->lse, b->bsum, b->minlsb, (float*)nullptr);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(softmax_choice_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse, b->bsum,
-                     b->nblocks, uniforms, out_idx);
+                     b->minlsb, b->nblocks, uniforms, out_idx);
   DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, float* lse_out, void* stream) {
+  if (!b || !logits || !p_out) return fail(DQZ_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
+                     b->capacity, b->part, (int64_t)-1);
+  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
+                     b->nblocks, b->lse, b->bsum, b->minlsb, p_out);
+  DQZ_HIP(hipGetLastError());
+  if (lse_out) DQZ_HIP(hipMemcpyAsync(lse_out, b->lse, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }
 

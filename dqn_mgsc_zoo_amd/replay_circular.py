@@ -93,6 +93,16 @@ class _DeviceLogits:
                                 device=self.device)
     return self.logits[pos].cpu().numpy()
 
+  def probs(self):
+    """(p, lse) as dqz_logits_sample forms them (diagnostic; device tensors)."""
+    p = self._torch.empty_like(self.logits)
+    lse = self._torch.empty((1,), dtype=self._torch.float32, device=self.device)
+    nat = self._native
+    nat.check(nat.lib().dqz_logits_probs(self._h, nat.ptr(self.logits),
+                                         nat.ptr(p), nat.ptr(lse),
+                                         nat.stream_handle()))
+    return p, lse
+
   def sample_abs(self, uniforms):
     """Absolute slots for host uniforms (device int64 tensor)."""
     n = len(uniforms)

@@ -252,6 +252,14 @@ int dqz_logits_add(dqz_logit_buffer* buf, float* logits, int64_t clear_pos, int6
 int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
                       int64_t* out_idx, void* stream);
 
+/* Diagnostic: the f32 p = exp(x - lse) of every slot exactly as
+ * dqz_logits_sample forms it (p_out: device f32 [capacity]) and lse
+ * (device f32, may be NULL) — probabilities_from_logits,
+ * replay_circular.py:69-76.  Lets a checker separate the index search (which
+ * is bit-exact against numpy given the same p) from the last-ulp differences
+ * of f32 exp / log between numpy and the device. */
+int dqz_logits_probs(dqz_logit_buffer* buf, const float* logits, float* p_out, float* lse_out, void* stream);
+
 /* n uniform doubles in [0,1) from Philox4x32-10 (counter advanced on device). */
 int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream);
 
