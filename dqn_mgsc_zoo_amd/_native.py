@@ -158,6 +158,9 @@ SIGNATURES = {
     'dqz_logits_add': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     'dqz_logits_sample': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
     'dqz_logits_probs': (_int, [_vp, _vp, _vp, _vp, _vp]),
+    'dqz_logits_write': (_int, [_vp, _vp, _vp, _vp, _int, _vp]),
+    'dqz_logits_put': (_int, [_vp, _vp, _i64, ctypes.c_float, _vp]),
+    'dqz_logits_invalidate': (_int, [_vp]),
     'dqz_uniform_philox': (_int, [ctypes.c_uint64, _vp, _int, _vp, _vp]),
     'dqz_sumtree_set': (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
     'dqz_sumtree_query': (_int, [_vp, _i64, _vp, _int, _vp, _vp]),

@@ -608,12 +608,19 @@ int dqz_gather_stacks(const dqz_store* S, const int32_t* slots, int n, int which
 struct dqz_logit_buffer {
   int64_t capacity;
   int nblocks, max_queries;
-  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | int minlsb[nblocks] | float lse
+  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | int minlsb[nblocks] | float lse | LogitRun
   MaxSum* part;
   double* bsum;
   int* minlsb;
   float* lse;
+  LogitRun* run;   // running log-sum-exp (sampling.hpp)
+  bool run_known;  // host side: every write since the last scan went through the library
+  int run_adds;    // running adds since the last scan
 };
+
+// Running adds between full re-scans of a logit buffer (bounds the running
+// sum's drift; each scan reads the whole buffer once).
+constexpr int kLogitReseed = 4096;
 
 int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out) {
   if (!out || capacity < 1 || max_queries < 1) return fail(DQZ_ERR_INVALID, "bad logit buffer arguments");
@@ -621,7 +628,7 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->capacity = capacity;
   b->max_queries = max_queries;
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
-  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int)) + 64;
+  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int)) + 64 + sizeof(LogitRun);
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
@@ -631,6 +638,9 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
   b->minlsb = (int*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
   b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum) + sizeof(int)));
+  b->run = (LogitRun*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum) + sizeof(int)) + 64);
+  b->run_known = false;
+  b->run_adds = 0;
   *out = b;
   return DQZ_OK;
 }
@@ -642,14 +652,17 @@ int dqz_logit_buffer_destroy(dqz_logit_buffer* b) {
   return DQZ_OK;
 }
 
+// Full two-pass log-sum-exp over the buffer (re-seeds the running state).
 static int logits_lse(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
                       float* lse_out, hipStream_t st) {
   hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
                      clear_pos);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part, b->nblocks, lse_out ? lse_out : b->lse,
-                     logits, write_pos, size);
+                     logits, write_pos, size, b->run);
   DQZ_HIP(hipGetLastError());
+  b->run_known = true;
+  b->run_adds = 0;
   return DQZ_OK;
 }
 
@@ -660,9 +673,41 @@ int dqz_logits_add(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_
     return fail(DQZ_ERR_INVALID, "position out of range");
   if (size < 0) return fail(DQZ_ERR_INVALID, "size must be >= 0");
   hipStream_t st = (hipStream_t)stream;
-  // the reservoir `replace` clear (logits[clear_pos] = -inf) happens inside pass 1
-  if (int rc = logits_lse(b, logits, clear_pos, write_pos, size, lse_out, st)) return rc;
+  if (!b->run_known || b->run_adds >= kLogitReseed) {
+    // the reservoir `replace` clear (logits[clear_pos] = -inf) happens inside pass 1
+    if (int rc = logits_lse(b, logits, clear_pos, write_pos, size, lse_out, st)) return rc;
+  } else {
+    hipLaunchKernelGGL(logits_add_running_kernel, dim3(1), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
+                       clear_pos, write_pos, size, lse_out ? lse_out : b->lse);
+    DQZ_HIP(hipGetLastError());
+    ++b->run_adds;
+  }
   if (lse_out) DQZ_HIP(hipMemcpyAsync(b->lse, lse_out, sizeof(float), hipMemcpyDeviceToDevice, st));
+  return DQZ_OK;
+}
+
+int dqz_logits_write(dqz_logit_buffer* b, float* logits, const int64_t* positions, const float* values, int n,
+                     void* stream) {
+  if (!b || !logits || (n > 0 && (!positions || !values))) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 0) return fail(DQZ_ERR_INVALID, "n must be >= 0");
+  if (n == 0) return DQZ_OK;
+  hipLaunchKernelGGL(logits_write_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, logits, b->run, positions, values,
+                     n);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_logits_put(dqz_logit_buffer* b, float* logits, int64_t position, float value, void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
+  if (position < 0 || position >= b->capacity) return fail(DQZ_ERR_INVALID, "position out of range");
+  hipLaunchKernelGGL(logits_put1_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, logits, b->run, position, value);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_logits_invalidate(dqz_logit_buffer* b) {
+  if (!b) return fail(DQZ_ERR_INVALID, "null argument");
+  b->run_known = false;
   return DQZ_OK;
 }
 

@@ -111,18 +111,140 @@ __device__ __forceinline__ MaxSum combine_parts(const MaxSum* __restrict__ part,
   return block_reduce_ms(acc, sbuf);
 }
 
+// Running log-sum-exp of a logit buffer: S = sum_i exp(x_i - c) in float64
+// about a fixed shift c, kept up to date by every write that goes through
+// the library (the add / reservoir replace / popleft / explicit writes of
+// replay_circular.py:166-190, 209-215, 526-545), so an add costs O(1)
+// instead of a scan of the whole buffer.  A full scan re-seeds it (c = max,
+// S from the scan) whenever the host-side owner cannot vouch for it (logits
+// handed out for writing, e.g. to the meta-update; set_state), every
+// kLogitReseed running adds (bounds the drift), and on the device when a
+// removal would cancel most of S or an item lands far above c (valid = 0:
+// the next add rescans inside its own block).
+struct LogitRun {
+  double S;
+  float c;
+  int valid;
+};
+
+// The reference's default logit (replay_circular.py:171-176): the float32
+// logsumexp minus np.log(size) in float64, stored back as float32.
+__device__ __forceinline__ float logmeanexp_item(float lse, int64_t size) {
+  return size == 0 ? 0.f : (float)((double)lse - log((double)size));
+}
+
+__device__ __forceinline__ double run_term(float x, float c) { return x == -INFINITY ? 0.0 : exp((double)x - (double)c); }
+
 // Pass 2 (one block): lse = m + log(s); optional logit write of a new item:
-// logits[write_pos] = size == 0 ? 0 : lse - log(size)   (log-mean-exp).
+// logits[write_pos] = size == 0 ? 0 : lse - log(size) (log-mean-exp); seeds
+// the running state `run` (may be null) from the scan.
 __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __restrict__ part, int nparts,
                                                                float* lse_out, float* logits, int64_t write_pos,
-                                                               int64_t size) {
+                                                               int64_t size, LogitRun* run) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
   const MaxSum acc = combine_parts(part, nparts, sbuf);
   if (threadIdx.x == 0) {
     const float lse = acc.m == -INFINITY ? -INFINITY : acc.m + logf(acc.s);
     if (lse_out) *lse_out = lse;
-    if (logits && write_pos >= 0) logits[write_pos] = size == 0 ? 0.f : lse - logf((float)size);
+    float item = -INFINITY;
+    if (logits && write_pos >= 0) {
+      item = logmeanexp_item(lse, size);
+      logits[write_pos] = item;
+    }
+    if (run) {
+      LogitRun r{acc.m == -INFINITY ? 0.0 : (double)acc.s, acc.m == -INFINITY ? 0.f : acc.m, 1};
+      r.S += run_term(item, r.c);  // the slot was -inf during the scan
+      *run = r;
+    }
   }
+}
+
+// Guard of a running update: S must stay well conditioned (no removal that
+// cancels most of it) and terms within exp's range about c.
+__device__ __forceinline__ bool run_ok(double s_before, double s_after, float x, float c) {
+  return s_after >= 1e-6 * s_before && s_after > 0.0 && (x == -INFINITY || (double)x - (double)c < 80.0);
+}
+
+// add / reservoir replace with the running state (one block).  If `run` is
+// not valid (a guard tripped), the block rescans the buffer itself first.
+__global__ __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* __restrict__ x, int64_t n,
+                                                                        LogitRun* run, int64_t clear_pos,
+                                                                        int64_t write_pos, int64_t size,
+                                                                        float* lse_out) {
+  __shared__ int s_valid;
+  __shared__ double dbuf[SM_THREADS / 64];
+  __shared__ float fbuf[SM_THREADS / 64];
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    if (r.valid && clear_pos >= 0) {
+      const double before = r.S;
+      r.S -= run_term(x[clear_pos], r.c);
+      if (!run_ok(before, r.S, -INFINITY, r.c) && r.S != 0.0) r.valid = 0;
+    }
+    if (clear_pos >= 0) x[clear_pos] = -INFINITY;
+    s_valid = r.valid;
+    *run = r;
+  }
+  __syncthreads();
+  if (!s_valid) {  // rescan: c = max, S = sum exp(x - c) in float64
+    float m = -INFINITY;
+    for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, x[j]);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
+    const float c = m == -INFINITY ? 0.f : m;
+    double sum = 0.0;
+    for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(x[j], c);
+    sum = block_sum_f64(sum, dbuf);
+    if (threadIdx.x == 0) *run = LogitRun{sum, c, 1};
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    const float lse = r.S > 0.0 ? (float)((double)r.c + log(r.S)) : -INFINITY;
+    if (lse_out) *lse_out = lse;
+    if (write_pos >= 0) {
+      const float item = logmeanexp_item(lse, size);
+      const double before = r.S;
+      r.S += run_term(item, r.c) - run_term(x[write_pos], r.c);
+      x[write_pos] = item;
+      if (!run_ok(before, r.S, item, r.c)) r.valid = 0;
+    }
+    *run = r;
+  }
+}
+
+// One write x[pos] = v passed by value (popleft's -inf), keeping the running state.
+__global__ void logits_put1_kernel(float* __restrict__ x, LogitRun* run, int64_t pos, float v) {
+  if (threadIdx.x != 0) return;
+  LogitRun r = *run;
+  if (r.valid) {
+    const double before = r.S;
+    r.S += run_term(v, r.c) - run_term(x[pos], r.c);
+    if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
+  }
+  x[pos] = v;
+  *run = r;
+}
+
+// Explicit writes x[pos[i]] = val[i] in order (a repeated slot keeps its last
+// value, as numpy fancy assignment does), keeping the running state.
+__global__ void logits_write_kernel(float* __restrict__ x, LogitRun* run, const int64_t* __restrict__ pos,
+                                    const float* __restrict__ val, int n) {
+  if (threadIdx.x != 0) return;
+  LogitRun r = *run;
+  for (int i = 0; i < n; ++i) {
+    const int64_t j = pos[i];
+    const float v = val[i];
+    if (r.valid) {
+      const double before = r.S;
+      r.S += run_term(v, r.c) - run_term(x[j], r.c);
+      if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
+    }
+    x[j] = v;
+  }
+  *run = r;
 }
 
 // Uniform doubles in [0, 1) from Philox (53-bit mantissa), counter advanced on device.

@@ -82,11 +82,34 @@ class _DeviceLogits:
                                    n.stream_handle()))
 
   def set(self, positions, values):
+    """logits[positions] = values in order, keeping the running log-sum-exp."""
     pos = self._torch.as_tensor(np.asarray(positions, np.int64),
                                 device=self.device)
     val = self._torch.as_tensor(np.asarray(values, np.float32),
                                 device=self.device)
-    self.logits[pos] = val
+    n = self._native
+    n.check(n.lib().dqz_logits_write(self._h, n.ptr(self.logits), n.ptr(pos),
+                                     n.ptr(val), int(pos.numel()),
+                                     n.stream_handle()))
+
+  def put(self, position, value):
+    """logits[position] = value (one write, no host->device copy)."""
+    n = self._native
+    n.check(n.lib().dqz_logits_put(self._h, n.ptr(self.logits), int(position),
+                                   float(value), n.stream_handle()))
+
+  def invalidate(self):
+    """The logits tensor was (or may be) written outside the library."""
+    self._native.check(self._native.lib().dqz_logits_invalidate(self._h))
+
+  def writable(self):
+    """The logits tensor for an outside writer (the meta-update)."""
+    self.invalidate()
+    return self.logits
+
+  def load(self, logits):
+    self.logits.copy_(self._torch.from_numpy(np.asarray(logits, np.float32)))
+    self.invalidate()
 
   def get(self, positions):
     pos = self._torch.as_tensor(np.asarray(positions, np.int64),
@@ -138,8 +161,9 @@ class CircularLogitBuffer:
 
   @property
   def logits(self):
-    """Device f32 logits [capacity] (absolute slot order)."""
-    return self._dev.logits
+    """Device f32 logits [capacity] (absolute slot order).  Handed out for
+    writing (the meta-update's Adam step), so the next add re-scans."""
+    return self._dev.writable()
 
   def is_full(self) -> bool:
     return self._size == self._capacity
@@ -150,7 +174,7 @@ class CircularLogitBuffer:
     if item is None:
       self._dev.add_default(self._right_head, self._size)
     else:
-      self._dev.set([self._right_head], [item])
+      self._dev.put(self._right_head, item)
     self._right_head = (self._right_head + 1) % self._capacity
     self._size += 1
 
@@ -158,7 +182,7 @@ class CircularLogitBuffer:
     if self._size == 0:
       raise BufferError('Buffer is empty and cannot be popped from. Add an item first.')
     item = self._dev.get([self._left_head])[0] if return_value else None
-    self._dev.set([self._left_head], [-np.inf])
+    self._dev.put(self._left_head, -np.inf)
     self._left_head = (self._left_head + 1) % self._capacity
     self._size -= 1
     return item
@@ -205,6 +229,9 @@ class CircularLogitBuffer:
     return self._rng_state.choice(self._size, size=size, replace=replace)
 
   def get_state(self) -> Mapping[str, Any]:
+    # the saver re-scans at its next add, as a restored copy will: both
+    # continue from the same bits
+    self._dev.invalidate()
     return {'capacity': self._capacity,
             'logits': self._dev.logits.cpu().numpy(), 'size': self._size,
             'left_head': self._left_head, 'right_head': self._right_head,
@@ -212,8 +239,7 @@ class CircularLogitBuffer:
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._capacity = state['capacity']
-    self._dev.logits.copy_(self._dev._torch.from_numpy(  # pylint: disable=protected-access
-        np.asarray(state['logits'], np.float32)))
+    self._dev.load(state['logits'])
     self._size = state['size']
     self._left_head = state['left_head']
     self._right_head = state['right_head']
@@ -439,7 +465,8 @@ class MGSCReservoirDistribution:
 
   @property
   def logits(self):
-    return self._dev.logits
+    """Device f32 logits [capacity]; handed out for writing (next add re-scans)."""
+    return self._dev.writable()
 
   def is_full(self) -> bool:
     return self._size == self._capacity
@@ -450,7 +477,7 @@ class MGSCReservoirDistribution:
     if priority is None:
       self._dev.add_default(self._size, self._size)
     else:
-      self._dev.set([self._size], [priority])
+      self._dev.put(self._size, priority)
     self._size += 1
 
   def replace(self, idx: int, priority: Optional[float] = None) -> None:
@@ -461,7 +488,7 @@ class MGSCReservoirDistribution:
     if priority is None:
       self._dev.add_default(idx, self._size, clear_pos=idx)
     else:
-      self._dev.set([idx], [priority])
+      self._dev.put(idx, priority)
 
   def __getitem__(self, key):
     key = np.asarray(key)
@@ -490,13 +517,13 @@ class MGSCReservoirDistribution:
     return self._rng_state.choice(self._size, size=size, replace=replace)
 
   def get_state(self) -> Mapping[str, Any]:
+    self._dev.invalidate()  # saver and restored copy both re-scan at their next add
     return {'capacity': self._capacity, 'logits': self._dev.logits.cpu().numpy(),
             'size': self._size, 'rng_state': self._rng_state}
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._capacity = state['capacity']
-    self._dev.logits.copy_(self._dev._torch.from_numpy(  # pylint: disable=protected-access
-        np.asarray(state['logits'], np.float32)))
+    self._dev.load(state['logits'])
     self._size = state['size']
     self._rng_state = state['rng_state']
 

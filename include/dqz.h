@@ -240,9 +240,28 @@ int dqz_logit_buffer_destroy(dqz_logit_buffer* buf);
 /* Default logit of an added item (replay_circular.py:166-179, :518-533):
  * if clear_pos >= 0, logits[clear_pos] = -inf first (the reservoir
  * `replace`); then logits[write_pos] = size == 0 ? 0
- *   : logsumexp(logits[0:capacity]) - log(size).  lse_out (device f32) may be NULL. */
+ *   : logsumexp(logits[0:capacity]) - log(size).  lse_out (device f32) may be NULL.
+ * The buffer keeps a running float64 sum of exp(x - c), so an add is O(1);
+ * it is re-seeded by a full scan after dqz_logits_invalidate, every 4096
+ * running adds, or when a removal would cancel most of it.  Every write to
+ * `logits` must go through dqz_logits_add / dqz_logits_write, or be followed
+ * by dqz_logits_invalidate. */
 int dqz_logits_add(dqz_logit_buffer* buf, float* logits, int64_t clear_pos, int64_t write_pos,
                    int64_t size, float* lse_out, void* stream);
+
+/* logits[positions[i]] = values[i] for i in order (a repeated position keeps
+ * its last value), keeping the running sum (popleft's -inf, __setitem__,
+ * update_priorities: replay_circular.py:180-215).  positions: device int64
+ * [n], values: device f32 [n]. */
+int dqz_logits_write(dqz_logit_buffer* buf, float* logits, const int64_t* positions, const float* values, int n,
+                     void* stream);
+
+/* One write logits[position] = value (by value: popleft's -inf), keeping the running sum. */
+int dqz_logits_put(dqz_logit_buffer* buf, float* logits, int64_t position, float value, void* stream);
+
+/* The logits were written outside the library (e.g. the meta-update's Adam
+ * step, a state restore): the next dqz_logits_add re-scans the buffer. */
+int dqz_logits_invalidate(dqz_logit_buffer* buf);
 
 /* Softmax sampling with replacement (CircularLogitBuffer.sample,
  * replay_circular.py:205-217 = Generator.choice(capacity, n, p=softmax)):

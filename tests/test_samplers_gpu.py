@@ -420,3 +420,72 @@ def test_device_per_add_and_write_back(device):
     last[k] = v
   host.set(list(last), replay_lib._power(np.array(list(last.values())), alpha))  # pylint: disable=protected-access
   np.testing.assert_allclose(d.sum_tree.storage[1:], host.storage[1:], rtol=1e-15)
+
+
+def _ref_lse(x):
+  return replay_ref.logsumexp_f32(x)
+
+
+@pytest.mark.parametrize('reservoir', [False, True])
+def test_running_logsumexp_matches_full_recompute(device, reservoir):
+  """12k random add / popleft (replace) / set / hand-out operations on a
+  3000-slot buffer: the running log-sum-exp adds (replay_circular.py:166-190,
+  526-533) stay within 1e-5 of the reference's full float32 recompute, across
+  the 4096-add re-seed, guard re-scans and invalidations."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap = 3000
+  rng = np.random.default_rng(11)
+  ref = np.full(cap, -np.inf, np.float32)
+  if reservoir:
+    buf = rc.MGSCReservoirDistribution(np.random.default_rng(0), cap)
+  else:
+    buf = rc.CircularLogitBuffer(cap, np.random.default_rng(0))
+  size = left = right = 0
+  worst = 0.0
+  for step in range(12000):
+    op = rng.random()
+    if reservoir:
+      if size < cap:
+        item = np.float32(0.0) if size == 0 else np.float32(_ref_lse(ref) - np.log(size))
+        ref[size] = item
+        buf.add()
+        size += 1
+      elif op < 0.8:
+        idx = int(rng.integers(0, cap))
+        ref[idx] = -np.inf
+        ref[idx] = np.float32(_ref_lse(ref) - np.log(size))
+        buf.replace(idx)
+      else:
+        keys = rng.integers(0, cap, 5)
+        vals = rng.normal(0, 2, 5).astype(np.float32)
+        for k, v in zip(keys, vals):
+          ref[k] = v
+        buf[keys] = vals
+    else:
+      if size == cap or (size > 0 and op < 0.3):
+        ref[left] = -np.inf
+        buf.popleft(return_value=False)
+        left = (left + 1) % cap
+        size -= 1
+      elif size > 0 and op < 0.38:
+        keys = rng.integers(0, size, 5)
+        vals = rng.normal(0, 2, 5).astype(np.float32)
+        for k, v in zip(keys, vals):
+          ref[(left + k) % cap] = v
+        buf[keys] = vals
+      else:
+        item = np.float32(0.0) if size == 0 else np.float32(_ref_lse(ref) - np.log(size))
+        ref[right] = item
+        buf.add()
+        right = (right + 1) % cap
+        size += 1
+    if step % 2500 == 1249:  # hand the tensor out (as to the meta-update): next add re-scans
+      _ = buf.logits
+    if step % 1000 == 999:
+      got = buf._dev.logits.cpu().numpy()  # pylint: disable=protected-access
+      live = np.isfinite(ref)
+      assert (np.isfinite(got) == live).all()
+      worst = max(worst, float(np.abs(got[live] - ref[live]).max()))
+      np.testing.assert_allclose(got[live], ref[live], rtol=0, atol=1e-5)
+      ref[live] = got[live]  # re-anchor so errors do not compound across checks
+  assert worst < 1e-5
