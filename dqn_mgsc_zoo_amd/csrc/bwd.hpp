@@ -246,13 +246,10 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
       wr[4 * tp + 3] = v.w;
     }
   }
-  float ym[3];  // relu'(y2) operands of the epilogue, loaded early
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int i = t + 256 * k;
-    const int p = min(48 * mh + (i >> 4), C2M - 1);
-    ym[k] = a.y2[((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15)];
-  }
+  // relu'(y2) operands of the epilogue, loaded early: thread t < 192 owns
+  // position 48 mh + t / 4, channels 16 nq + 4 (t & 3) .. +3
+  const int ep = min(48 * mh + (t >> 2), C2M - 1);
+  const float4 ym4 = *reinterpret_cast<const float4*>(a.y2 + ((int64_t)b * C2M + ep) * C2CO + 16 * nq + 4 * (t & 3));
   // padded dy3 window: (ph, pw) in 11 x 11, interior [2, 9)
   const float4* src = reinterpret_cast<const float4*>(a.dy3 + (int64_t)b * FLAT);
   constexpr int NW4 = 121 * 16;  // 1936
@@ -303,18 +300,23 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 768 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
+  // 4 channels per lane: one 16-byte (write-through when PUB) store each
+  if (t < 192 && 48 * mh + (t >> 2) < C2M) {
+    const int i = 4 * t;  // s_red index of (position t / 4, channel 4 (t & 3))
+    f32x4 v;  // (a 4-byte write-through store costs ~6x the 16-byte one per byte)
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int i = t + 256 * k;
-    const int p = 48 * mh + (i >> 4);
-    if (p < C2M) {
-      const float v = (s_red[i] + s_red[768 + i]) + (s_red[1536 + i] + s_red[2304 + i]);
-      float* dst = a.dy2 + ((int64_t)b * C2M + p) * C2CO + 16 * nq + (i & 15);
-      if constexpr (PUB)
-        __hip_atomic_store(dst, ym[k] > 0.f ? v : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *dst = ym[k] > 0.f ? v : 0.f;
-    }
+    for (int e = 0; e < 4; ++e)
+      v[e] = (s_red[i + e] + s_red[768 + i + e]) + (s_red[1536 + i + e] + s_red[2304 + i + e]);
+    v[0] = ym4.x > 0.f ? v[0] : 0.f;
+    v[1] = ym4.y > 0.f ? v[1] : 0.f;
+    v[2] = ym4.z > 0.f ? v[2] : 0.f;
+    v[3] = ym4.w > 0.f ? v[3] : 0.f;
+    float* slab = a.dy2 + (int64_t)b * C2M * C2CO;
+    const int off = ((48 * mh + (t >> 2)) * C2CO + 16 * nq + 4 * (t & 3)) * 4;
+    if constexpr (PUB)
+      store_sc1_f4(slab, C2M * C2CO * 4, off, v);
+    else
+      *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(slab) + off) = v;
   }
   if constexpr (PUB) a.sync.arrive(b);
 }
@@ -427,11 +429,14 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
       wr[4 * tp + 3] = v.w;
     }
   }
-  float ym[7];  // relu'(y1) operands of the epilogue, loaded early
+  // relu'(y1) operands of the epilogue, loaded early: thread t owns output
+  // positions q = t / 4 and q + 64 (< 100), channels 16 hh + 4 (t & 3) .. +3
+  float4 ym4[2];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int p = min((t + 256 * k) >> 4, 99), ah = p / 10, cw = p % 10;
-    ym[k] = a.y1[((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (t & 15)];
+  for (int k = 0; k < 2; ++k) {
+    const int q = min((t >> 2) + 64 * k, 99), ah = q / 10, cw = q % 10;
+    ym4[k] = *reinterpret_cast<const float4*>(a.y1 + ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO +
+                                              16 * hh + 4 * (t & 3));
   }
   const float4* src = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * (C2M * C2CO));
   constexpr int NW4 = 121 * 16;  // 1936
@@ -464,41 +469,70 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   __syncthreads();
   DQZ_STAMP(7, 1);
-  int base[7];
+  // 100 pixels = 6 MFMA row tiles + pixels 96..99 on the VALU (fwd.hpp DQZ_TRIM)
+  constexpr int MT = DQZ_TRIM ? 6 : 7;
+  int base[MT];
 #pragma unroll
-  for (int m = 0; m < 7; ++m) {
+  for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, 99);  // p = 10 a + c
     base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + 16 * w + kq;
   }
-  f32x4 acc[7];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int m = 0; m < 7; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float last[4] = {0.f, 0.f, 0.f, 0.f};  // pixels 96..99 (a = 9, c = 6..9), this lane's k rows
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     const int tp = kk >> 2;  // (u', v') = (tp >> 1, tp & 1)
     const int off = (tp >> 1) * C2X_RS + (tp & 1) * C2X_S + 4 * (kk & 3);
 #pragma unroll
-    for (int m = 0; m < 7; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
+    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
+    if constexpr (DQZ_TRIM) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + 16 * w + kq + off], wr[kk], last[e]);
+    }
+  }
+  if constexpr (DQZ_TRIM) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      last[e] += __shfl_xor(last[e], 16, 64);
+      last[e] += __shfl_xor(last[e], 32, 64);
+    }
   }
   __syncthreads();
   DQZ_STAMP(7, 2);
   float* s_red = s_win;  // [4][112][16]
 #pragma unroll
-  for (int m = 0; m < 7; ++m)
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
-  __syncthreads();
+  if (DQZ_TRIM && kq == 0) {
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int i = t + 256 * k;
-    if (i < 1600) {
-      const int p = i >> 4, ah = p / 10, cw = p % 10;
-      const float v = (s_red[i] + s_red[1792 + i]) + (s_red[3584 + i] + s_red[5376 + i]);
-      float* dst = a.dy1 + ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + (i & 15);
+    for (int e = 0; e < 4; ++e) s_red[w * 1792 + (96 + e) * 16 + n] = last[e];
+  }
+  __syncthreads();
+  // 4 channels per lane: one 16-byte (write-through when PUB) store each
+  // (a 4-byte write-through store costs ~6x the 16-byte one per byte)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = (t >> 2) + 64 * k;
+    if (q < 100) {
+      const int i = 16 * q + 4 * (t & 3), ah = q / 10, cw = q % 10;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = (s_red[i + e] + s_red[1792 + i + e]) + (s_red[3584 + i + e] + s_red[5376 + i + e]);
+      v[0] = ym4[k].x > 0.f ? v[0] : 0.f;
+      v[1] = ym4[k].y > 0.f ? v[1] : 0.f;
+      v[2] = ym4[k].z > 0.f ? v[2] : 0.f;
+      v[3] = ym4[k].w > 0.f ? v[3] : 0.f;
+      float* slab = a.dy1 + (int64_t)b * C1M * C1CO;
+      const int off = (((2 * ah + ph) * C1O + 2 * cw + pw) * C1CO + 16 * hh + 4 * (t & 3)) * 4;
       if constexpr (PUB)
-        __hip_atomic_store(dst, ym[k] > 0.f ? v : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        store_sc1_f4(slab, C1M * C1CO * 4, off, v);
       else
-        *dst = ym[k] > 0.f ? v : 0.f;
+        *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(slab) + off) = v;
     }
   }
   if constexpr (PUB) a.sync1.arrive(b);

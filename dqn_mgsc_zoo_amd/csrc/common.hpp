@@ -238,6 +238,14 @@ __device__ __forceinline__ float4 load_sc1_f4(const float4* base, int bytes, int
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 16));
 }
 
+// 16-byte write-through (sc1) store of v at byte offset `off` of a buffer of
+// `bytes` bytes whose base is wave-uniform (buffer_store_dwordx4 ... sc1).
+__device__ __forceinline__ void store_sc1_f4(float* base, int bytes, int off, f32x4 v) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+
 // Uniform replay draw of the device sampler (replay.py:119-125 distribution):
 // draw i of step `ctr` -> live slot (base + floor(u * size)) mod capacity,
 // u from Philox(counter = (ctr, i), key = seed).

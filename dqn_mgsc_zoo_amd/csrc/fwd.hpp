@@ -22,6 +22,12 @@
 
 namespace dqz {
 
+// 1: the mostly-empty last MFMA row tile of conv2 / conv3 forward and conv2
+// dX is replaced by VALU dot products of its few live positions
+#ifndef DQZ_TRIM
+#define DQZ_TRIM 1
+#endif
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -79,28 +85,39 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   }
   DQZ_STAMP(1, 1);
   __syncthreads();
-  int base[6];
+  // 81 positions = 5 MFMA row tiles + position 80, which every lane folds
+  // from its own weight registers on the VALU (a 6th tile would be 1/16 live)
+  constexpr int MT = DQZ_TRIM ? 5 : 6;
+  int base[MT];
 #pragma unroll
-  for (int m = 0; m < 6; ++m) {
+  for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, C2M - 1);
     base[m] = (2 * (p / C2O) + w) * C2L_RS + 2 * (p % C2O) * C2L_S + kq;
   }
-  f32x4 acc[6];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int m = 0; m < 6; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float last = 0.f;  // position 80 (oh = ow = 8), this lane's k rows
+  const int blast = (2 * (C2O - 1) + w) * C2L_RS + 2 * (C2O - 1) * C2L_S + kq;
 #pragma unroll
   for (int kk = 0; kk < 32; ++kk) {
     const int off = (kk >> 3) * C2L_S + 4 * (kk & 7);  // kw, ci block
 #pragma unroll
-    for (int m = 0; m < 6; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+    if constexpr (DQZ_TRIM) last = __fmaf_rn(s_in[blast + off], wr[kk], last);
   }
   DQZ_STAMP(1, 2);
+  if constexpr (DQZ_TRIM) {
+    last += __shfl_xor(last, 16, 64);
+    last += __shfl_xor(last, 32, 64);
+  }
   __syncthreads();
   float* s_red = s_in;  // [4][96][16]
 #pragma unroll
-  for (int m = 0; m < 6; ++m)
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1536 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  if (DQZ_TRIM && kq == 0) s_red[w * 1536 + (C2M - 1) * 16 + n] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
@@ -165,29 +182,39 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   }
   DQZ_STAMP(2, 1);
   __syncthreads();
-  int base[4];
+  // 49 positions = 3 MFMA row tiles + position 48 on the VALU (see conv2)
+  constexpr int MT = DQZ_TRIM ? 3 : 4;
+  int base[MT];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
+  for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, C3M - 1);
     base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + 16 * w + kq;
   }
-  f32x4 acc[4];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float last = 0.f;  // position 48 (oh = ow = 6), this lane's k rows
+  const int blast = (C3O - 1) * C3L_RS + (C3O - 1) * C3L_S + 16 * w + kq;
 #pragma unroll
   for (int kk = 0; kk < 36; ++kk) {
     const int tap = kk >> 2;
     const int off = (tap / 3) * C3L_RS + (tap % 3) * C3L_S + 4 * (kk & 3);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+    if constexpr (DQZ_TRIM) last = __fmaf_rn(s_in[blast + off], wr[kk], last);
   }
   DQZ_STAMP(2, 2);
+  if constexpr (DQZ_TRIM) {
+    last += __shfl_xor(last, 16, 64);
+    last += __shfl_xor(last, 32, 64);
+  }
   __syncthreads();
   float* s_red = s_in;  // [4][64][16]
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1024 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  if (DQZ_TRIM && kq == 0) s_red[w * 1024 + (C3M - 1) * 16 + n] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
