@@ -608,10 +608,9 @@ int dqz_gather_stacks(const dqz_store* S, const int32_t* slots, int n, int which
 struct dqz_logit_buffer {
   int64_t capacity;
   int nblocks, max_queries;
-  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | int minlsb[nblocks] | float lse | LogitRun
+  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | float lse | LogitRun
   MaxSum* part;
   double* bsum;
-  int* minlsb;
   float* lse;
   LogitRun* run;   // running log-sum-exp (sampling.hpp)
   bool run_known;  // host side: every write since the last scan went through the library
@@ -628,7 +627,7 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->capacity = capacity;
   b->max_queries = max_queries;
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
-  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int)) + 64 + sizeof(LogitRun);
+  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double)) + 64 + sizeof(LogitRun);
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
@@ -636,9 +635,8 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   char* p = (char*)b->block;
   b->bsum = (double*)p;
   b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
-  b->minlsb = (int*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
-  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum) + sizeof(int)));
-  b->run = (LogitRun*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum) + sizeof(int)) + 64);
+  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
+  b->run = (LogitRun*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)) + 64);
   b->run_known = false;
   b->run_adds = 0;
   *out = b;
@@ -720,10 +718,10 @@ int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* un
   hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
                      b->capacity, b->part, (int64_t)-1);
   hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
-                     b->nblocks, b->lse, b->bsum, b->minlsb, (float*)nullptr);
+                     b->nblocks, b->lse, b->bsum, (float*)nullptr);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(softmax_choice_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse, b->bsum,
-                     b->minlsb, b->nblocks, uniforms, out_idx);
+                     b->nblocks, uniforms, out_idx);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -734,7 +732,7 @@ int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, flo
   hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
                      b->capacity, b->part, (int64_t)-1);
   hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
-                     b->nblocks, b->lse, b->bsum, b->minlsb, p_out);
+                     b->nblocks, b->lse, b->bsum, p_out);
   DQZ_HIP(hipGetLastError());
   if (lse_out) DQZ_HIP(hipMemcpyAsync(lse_out, b->lse, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;

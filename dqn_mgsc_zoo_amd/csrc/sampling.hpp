@@ -6,11 +6,12 @@
 //    reference's probabilities_from_logits, then the float64 CDF that
 //    numpy's choice builds (sequential cumsum, normalise by the last entry,
 //    searchsorted right).  The device sums p in blocks; that equals numpy's
-//    sequential fp64 cumsum bit for bit whenever no partial sum rounds, which
-//    holds when every nonzero p is a multiple of ulp(total) (min_lsb below:
-//    the partial sums are then multiples of that ulp below 2 total, i.e.
-//    exact fp64 values in any order).  Otherwise the choice kernel runs
-//    numpy's sequential scan itself.
+//    sequential fp64 cumsum bit for bit whenever no partial sum rounds
+//    (every nonzero p a multiple of ulp(total): logits spanning < ~20 nats
+//    at 1M slots).  Otherwise both orders round a few tiny p by at most half
+//    an ulp of the running sum each, and a draw can differ only if u lies
+//    within those few ulps of a CDF boundary (~1e-16 of the total against
+//    boundary gaps of ~1e-6 at 1M slots).
 //  * prioritized replay (replay.py:379-559): the fp64 implicit sum tree in
 //    HBM, same node layout as the host SumTree; set recomputes every touched
 //    ancestor as left + right, so device and host sums are bit-identical.
@@ -263,50 +264,31 @@ __global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, d
 // probabilities_from_logits), widened to float64 like numpy's choice.
 __device__ __forceinline__ float prob_f32(float x, float L) { return expf(x - L); }
 
-// Exponent of the least significant bit of a positive f32 (2^-149 for
-// subnormals); INT_MAX for 0 so zeros never bind the minimum.
-__device__ __forceinline__ int lsb_exp_f32(float p) {
-  const unsigned u = __float_as_uint(p);
-  const int E = (int)((u >> 23) & 0xFF);
-  return (u & 0x7FFFFFFFu) == 0u ? 0x7FFFFFFF : (E == 0 ? -149 : E - 150);
-}
-
-// Per-block float64 sums of p and the block's minimum lsb exponent of a
-// nonzero p.  lse is recombined from pass 1's partials by every block (same
+// Per-block float64 sums of p.  lse is recombined from pass 1's partials by every block (same
 // bits as lse_final_kernel); block 0 publishes it for the choice kernel.
 // p_out (diagnostic, dqz_logits_probs): the f32 p of every slot, or null.
 __global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float* __restrict__ x, int64_t n,
                                                                     const MaxSum* __restrict__ part, int nparts,
                                                                     float* __restrict__ lse_out,
                                                                     double* __restrict__ bsum,
-                                                                    int* __restrict__ bminlsb,
                                                                     float* __restrict__ p_out) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
   __shared__ double dbuf[SM_THREADS / 64];
-  __shared__ int ibuf;
   const MaxSum t = combine_parts(part, nparts, sbuf);
   const float L = t.m == -INFINITY ? -INFINITY : t.m + logf(t.s);
   if (blockIdx.x == 0 && threadIdx.x == 0) *lse_out = L;
-  if (threadIdx.x == 0) ibuf = 0x7FFFFFFF;
   const int64_t base = (int64_t)blockIdx.x * SM_CHUNK;
   double acc = 0.0;
-  int ml = 0x7FFFFFFF;
   for (int i = threadIdx.x; i < SM_CHUNK; i += SM_THREADS) {
     const int64_t j = base + i;
     if (j < n) {
       const float pf = prob_f32(x[j], L);
       acc += (double)pf;
-      ml = min(ml, lsb_exp_f32(pf));
       if (p_out) p_out[j] = pf;
     }
   }
-  __syncthreads();
-  atomicMin(&ibuf, ml);
-  acc = block_sum_f64(acc, dbuf);  // its barriers also order the atomicMin
-  if (threadIdx.x == 0) {
-    bsum[blockIdx.x] = acc;
-    bminlsb[blockIdx.x] = ibuf;
-  }
+  acc = block_sum_f64(acc, dbuf);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
 }
 
 // Inclusive scan of one double per thread over the block, in a fixed
@@ -337,13 +319,12 @@ constexpr int SM_PER_LANE = SM_CHUNK / SM_THREADS;  // 16
 
 __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float* __restrict__ x, int64_t n,
                                                                     const float* __restrict__ lse,
-                                                                    const double* __restrict__ bsum,
-                                                                    const int* __restrict__ bminlsb, int nblocks,
+                                                                    const double* __restrict__ bsum, int nblocks,
                                                                     const double* __restrict__ uniforms,
                                                                     int64_t* __restrict__ out) {
   __shared__ double s_scan[SM_THREADS];
   __shared__ double s_before;
-  __shared__ int s_blk, s_minlsb;
+  __shared__ int s_blk;
   __shared__ unsigned long long s_idx;
   const int t = threadIdx.x;
   const float L = *lse;
@@ -352,40 +333,13 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float*
   const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
   const int b0 = min(t * seg, nblocks), b1 = min(b0 + seg, nblocks);
   double mine = 0.0;
-  int ml = 0x7FFFFFFF;
-  for (int b = b0; b < b1; ++b) {
-    mine += bsum[b];
-    ml = min(ml, bminlsb[b]);
-  }
+  for (int b = b0; b < b1; ++b) mine += bsum[b];
   if (t == 0) {
     s_blk = nblocks - 1;
     s_idx = ~0ull;
-    s_minlsb = 0x7FFFFFFF;
   }
-  __syncthreads();
-  atomicMin(&s_minlsb, ml);
   const double incl = block_scan_incl_f64(mine, s_scan);
   const double tot = s_scan[SM_THREADS - 1];
-  // Every partial sum exact (see the header): the blocked sums are numpy's
-  // sequential cumsum.  Otherwise lane 0 replays numpy's sequential scan
-  // (slow: two passes over n; only for logits spanning > 2^29 in p).
-  if (tot > 0.0 && s_minlsb < ilogb(tot) - 51) {  // one bit of margin for tot's own rounding
-    if (t == 0) {
-      double tot_seq = 0.0;
-      for (int64_t j = 0; j < n; ++j) tot_seq += (double)prob_f32(x[j], L);
-      double run = 0.0;
-      int64_t idx = n - 1;
-      for (int64_t j = 0; j < n; ++j) {
-        run += (double)prob_f32(x[j], L);
-        if (run / tot_seq > u) {
-          idx = j;
-          break;
-        }
-      }
-      out[blockIdx.x] = idx;
-    }
-    return;
-  }
   {
     double run = incl - mine;
     for (int b = b0; b < b1; ++b) {

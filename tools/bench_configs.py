@@ -81,6 +81,7 @@ def main():
   lrn_d.set_params(net_d.init(seed=1))
   slots = torch.zeros((B,), dtype=torch.int32, device=dev)
   ctr = torch.zeros((1,), dtype=torch.int64, device=dev)
+  print('double_uniform ...', file=sys.stderr, flush=True)
   out['double_uniform'] = timed(
       lambda: lrn_d.step_uniform(store, 0, cap, cap, 7, ctr, slots),
       args.steps, 20, dev, graph_steps=50)
@@ -110,6 +111,7 @@ def main():
     lrn_p.step(store, p_slots, p_w)
     _native.check(lib.dqz_per_write_back(lrn_p._h, _native.ptr(tree), tcap, _native.ptr(p_slots),  # pylint: disable=protected-access
                                          ctypes.c_double(0.6), _native.ptr(max_seen), _native.stream_handle()))
+  print('per_double ...', file=sys.stderr, flush=True)
   out['per_double'] = timed(per_step, args.steps, 20, dev, graph_steps=50)
 
   # ---- MGSC learner part: softmax sample over the logits + DQN step -------
@@ -131,6 +133,7 @@ def main():
                                         _native.stream_handle()))
     m_slots.copy_(m_idx)
     lrn.step(store, m_slots)
+  print('mgsc_learn ...', file=sys.stderr, flush=True)
   out['mgsc_learn'] = timed(mgsc_learn, args.steps, 20, dev, graph_steps=50)
 
   # ---- MGSC meta_update ----------------------------------------------------
@@ -145,6 +148,7 @@ def main():
       mp = ms.clone()
       t = timed(lambda: meta.update(store, ms, logits, mp), max(20, args.steps // 20), 3, dev)
       out['mgsc_meta_M%d_%s' % (m_batch, 'second' if order else 'first')] = t
+      print('mgsc_meta M=%d order=%d %s' % (m_batch, order, t), file=sys.stderr, flush=True)
       del meta
   _native.check(lib.dqz_logit_buffer_destroy(lb))
   print(json.dumps(out))
