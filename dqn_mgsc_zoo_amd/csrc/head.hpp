@@ -66,11 +66,8 @@ __device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double e
 //   the cotangent at td is clip(w td / B, +-bound) because rlax.clip_gradient
 //   clips the incoming gradient; dq[b, a_b] = -that; dz1 = dq W2[:, a_b] relu'.
 // Cross-sample sums (fc2/fc1-bias grads, mean loss) happen in update_kernel.
-// PUB (head_dx_kernel): dz1 is handed to the fc1 dX blocks of the same launch
-// — its stores are write-through (agent-scope relaxed atomic stores) and the
-// block arrives on the batch counter `pub` (common.hpp Handoff, word 0).
-template <int AMAX, int SMAX, bool PUB>
-__device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handoff& pub) {
+template <int AMAX, int SMAX>
+__device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   DQZ_STAMP(4, 0);
   __shared__ float s_red[8][3 * AMAX];
   __shared__ float s_q[3][AMAX];
@@ -234,12 +231,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
     for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
     DQZ_STAMP(4, 2);
     const float dz = hz[0] > 0.f ? s_g * wv : 0.f;
-    if constexpr (PUB) {
-      __hip_atomic_store(h.dz1 + (int64_t)b * HID + n, dz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pub.arrive(0);
-    } else {
-      h.dz1[(int64_t)b * HID + n] = dz;
-    }
+    h.dz1[(int64_t)b * HID + n] = dz;
   } else if (h.act_out) {  // actor: eps-greedy draw b of call act_ctr
     __syncthreads();
     if (n == 0) {
@@ -262,7 +254,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b, const Handof
 
 template <int AMAX, int SMAX>
 __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
-  head_body<AMAX, SMAX, false>(h, blockIdx.x, Handoff{});
+  head_body<AMAX, SMAX>(h, blockIdx.x);
 }
 
 // Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.

@@ -177,7 +177,7 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
 
 // conv1..fc1 forward of Z network copies (phases 0-3).
 // fused_conv: conv1 -> conv2 -> conv3 as one hand-off launch (fwd_conv_kernel);
-// the learner step uses it only under DQZ_FUSED_FWD=1, the actor (n <= a few
+// the learner step keeps three launches (measured faster), the actor (n <= a few
 // samples, launch-latency bound) always.
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
                         PhaseEvents pe, bool fused_conv) {
