@@ -238,7 +238,14 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
   lg = replay.logits.cpu().numpy()
   assert np.isfinite(lg[lg != -np.inf]).all()
   assert not torch.equal(logits0, replay.logits)
-  # one more meta step through the agent path, checked against the oracle
+  _check_meta_step_against_oracle(agent, replay, stop_gradient=True)
+
+
+def _check_meta_step_against_oracle(agent, replay, stop_gradient):
+  """One more meta step through the agent path (_meta_prioritization_learn,
+  dqn_mgsc_batched/agent.py:302-334), its Adam-updated logits checked
+  against the fp64 oracle's meta_update on the same meta batch."""
+  meta = agent.meta_learner
   lrn = agent.learner
   trees = [_params_host(lrn.params_tree(w))
            for w in ('online', 'target', 'mu', 'nu')]
@@ -261,8 +268,9 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
   trans = replay_lib.Transition(ts0.observation, 2, ts1.reward, ts1.discount,
                                 ts1.observation)
   agent._meta_prioritization_learn(trans)  # pylint: disable=protected-access
-  indices, slots, positions = captured['out']
-  items = replay._items.stack(None, replay._slots(indices))  # pylint: disable=protected-access
+  replay.meta_batch_slots = orig
+  indices, _, positions = captured['out']
+  items = replay.stack_transitions(indices)
   mb = dict(s_tm1=items.s_tm1.cpu().numpy(), a_tm1=items.a_tm1.cpu().numpy(),
             r_t=items.r_t.cpu().numpy(), discount_t=items.discount_t.cpu().numpy(),
             s_t=items.s_t.cpu().numpy())
@@ -271,9 +279,13 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
       dict(s_tm1=trans.s_tm1, a_tm1=2, r_t=trans.r_t,
            discount_t=trans.discount_t, s_t=trans.s_t),
       st['mu'], st['nu'], st['count'], lr=LR, decay=DECAY, eps=EPS,
-      grad_error_bound=BOUND)
+      grad_error_bound=BOUND, stop_gradient=stop_gradient)
   after = replay.logits.cpu().numpy()
   np.testing.assert_allclose(after[positions], ref['new_logits'], atol=1e-6)
+  # untouched slots keep their logits
+  mask = np.ones(len(after), bool)
+  mask[np.asarray(positions)] = False
+  np.testing.assert_array_equal(after[mask], before[mask])
 
 
 def test_mgsc_reservoir_agent_run_loop(device):
@@ -305,3 +317,6 @@ def test_mgsc_reservoir_agent_run_loop(device):
   lg = replay.logits.cpu().numpy()
   assert np.isfinite(lg).all()
   assert torch.isfinite(agent.learner.online).all()
+  # the second-order meta step (no stop_gradient on theta'', reservoir
+  # agent.py:191) through the agent path, against the fp64 oracle
+  _check_meta_step_against_oracle(agent, replay, stop_gradient=False)
