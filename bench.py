@@ -543,7 +543,10 @@ def run_gpu(args, g, rem):
       'per_rank_steps_per_s': [round(float(x), 2) for x in per_rank[:, 0]],
       'per_gpu_min_steps_per_s': round(float(per_rank[:, 0].min()), 2),
       'stats_gathers': len(pending),
-      'handoff_status': int(max(status_max, status_after)),
+      # learner health word (dqz_learner_sync_status): bit 0 a hand-off wait
+      # gave up, bit 1 a step's mean loss was not finite
+      'handoff_status': int(max(status_max, status_after)) & 1,
+      'nonfinite_loss': bool(int(max(status_max, status_after)) & 2),
       'fill_s': round(t_fill, 2),
       'last_loss': float(loss.item()),
       'params_finite': finite,
@@ -554,9 +557,10 @@ def run_gpu(args, g, rem):
     out['cpu_baseline'] = None
   print(json.dumps(out), flush=True)
   reps.close()
-  if out['handoff_status'] != 0 or not finite:
-    print('bench.py: hand-off status %d, params finite %s: the timed steps are '
-          'invalid' % (out['handoff_status'], finite), file=sys.stderr)
+  if out['handoff_status'] != 0 or out['nonfinite_loss'] or not finite:
+    print('bench.py: hand-off status %d, non-finite loss %s, params finite %s: '
+          'the timed steps are invalid' % (out['handoff_status'], out['nonfinite_loss'],
+                                           finite), file=sys.stderr)
     return 3
   return 0
 

@@ -281,6 +281,7 @@ struct UpdArgs {
   const int32_t* ga; // [B]
   const float* loss_part;
   float* loss;
+  int* status;  // learner health word: bit 1 set when the batch loss is not finite
   int A, B, nb2;
   Rms rms;
 };
@@ -397,7 +398,11 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
   s_part[grp][pl] = g;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     loss = wave_sum(loss);
-    if (threadIdx.x == 0) u.loss[0] = loss / (float)u.B;
+    if (threadIdx.x == 0) {
+      u.loss[0] = loss / (float)u.B;
+      // NaN / inf guard: reported by dqz_learner_sync_status (bit 1)
+      if (u.status && !isfinite(loss)) __hip_atomic_fetch_or(u.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   if (grp == 0) {

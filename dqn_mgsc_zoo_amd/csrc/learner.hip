@@ -395,6 +395,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.ga = L->ga;
   u.loss_part = L->loss_part;
   u.loss = L->loss;
+  u.status = herr;
   u.A = A;
   u.B = B;
   u.nb2 = L->shared_bias ? 1 : A;

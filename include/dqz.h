@@ -163,11 +163,14 @@ int dqz_learner_profile(dqz_learner* learner, const dqz_params* params, const dq
  * q_tm1 [B][A] online Q(s_tm1), td [B] TD errors, loss [1] mean loss. */
 int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* loss, void* stream);
 
-/* Health of the in-launch hand-offs of the backward pass: *status = 0 when
- * every wait completed, 1 if a wait gave up (a bounded spin expired; the
- * step's results are then invalid).  Synchronises the device.  A non-zero
- * status also clears every hand-off word, so the next step starts clean;
- * callers treat the steps since their previous check as invalid. */
+/* Health word of the learner since the previous check: *status = 0 when
+ * every in-launch hand-off wait of the backward pass completed and every
+ * batch loss was finite; bit 0 (1): a wait gave up (a bounded spin expired;
+ * the step's results are then invalid); bit 1 (2): a step's mean loss was
+ * NaN or infinite (the update still ran, as the reference's jitted update
+ * would).  Synchronises the device.  A non-zero status also clears every
+ * hand-off word and the status, so the next step starts clean; callers treat
+ * the steps since their previous check as invalid. */
 int dqz_learner_sync_status(dqz_learner* learner, int* status);
 
 /* Q-values of the NatureQNetwork for uint8 HWC states [n][84][84][4]

@@ -227,8 +227,8 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
                                         ('dqn', 33)])
 def test_handoff_kernels_bit_reproducible(device, algo, batch):
   """The in-launch hand-offs (bwd_bc_kernel: conv3 dX -> conv2 dX / conv2 dW,
-  conv2 dX -> conv1 dW) and the last-arriver head of fc1_head_kernel sum in
-  fixed orders, whichever workgroup arrives last: two learners fed the same
+  conv2 dX -> conv1 dW) sum in fixed orders, whichever workgroup arrives
+  last: two learners fed the same
   steps agree bit for bit, eagerly, under hipGraph replay and after
   profile-mode back-to-back launches; the hand-off words reset themselves
   (sync_status 0); and the result stays at the oracle."""
@@ -264,8 +264,8 @@ def test_handoff_kernels_bit_reproducible(device, algo, batch):
   q1, td1, _ = lrn.fetch_outputs()
   q2, td2, _ = ref.fetch_outputs()
   assert torch.equal(q1, q2) and torch.equal(td1, td2)
-  # profile mode repeats every launch back to back; the hand-off words and
-  # the last-arriver counters must reset themselves between launches.
+  # profile mode repeats every launch back to back; the hand-off words must
+  # reset themselves between launches.
   lrn.profile(st, slots, weights=w, iters=5)
   torch.cuda.synchronize()
   assert lrn.sync_status() == 0
@@ -307,3 +307,17 @@ def test_per_write_back_device(device):
   host.set(slots_np, replay_lib._power(p, alpha))  # pylint: disable=protected-access
   np.testing.assert_allclose(tree.cpu().numpy()[1:], host.storage[1:], rtol=4e-16, atol=0)
   assert max_seen.item() == max(0.25, p.max())
+
+
+def test_nonfinite_loss_is_flagged(device):
+  """NaN guard: a step whose mean loss is not finite sets bit 1 of the
+  learner's health word (dqz_learner_sync_status); reading it clears it."""
+  _, lrn, st, _, _, _, _, _ = _setup('dqn', 32, seed=5)
+  rng = np.random.default_rng(6)
+  slots = torch.from_numpy(rng.integers(0, st.capacity, size=32).astype(np.int32)).to(device)
+  lrn.step(st, slots)
+  assert lrn.sync_status() == 0
+  st.reward[slots[0].long()] = float('nan')
+  lrn.step(st, slots)
+  assert lrn.sync_status() == 2
+  assert lrn.sync_status() == 0
