@@ -130,6 +130,7 @@ SIGNATURES = {
     ),
     'dqz_learner_outputs': (_int, [_vp, _vp, _vp, _vp, _vp]),
     'dqz_learner_sync_status': (_int, [_vp, _vp]),
+    'dqz_learner_debug_stall': (_int, [_vp, _int, ctypes.c_uint]),
     'dqz_per_write_back': (_int, [_vp, _vp, _i64, _vp, ctypes.c_double, _vp, _vp]),
     'dqz_learner_profile': (
         _int,

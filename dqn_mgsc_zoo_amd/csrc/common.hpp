@@ -206,6 +206,7 @@ struct Handoff {
   int* ack;  // [B * kStride] consumers past the wait
   int* err;  // timeout word (0 = ok)
   int need, consumers;
+  unsigned spin_max = 1u << 24;  // polls before a wait gives up (dqz_learner_debug_stall shortens it)
   __device__ __forceinline__ void arrive(int b) const {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -216,7 +217,7 @@ struct Handoff {
       unsigned spins = 0;
       while (__hip_atomic_load(cnt + b * kStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(4);
-        if (++spins > (1u << 24)) {
+        if (++spins > spin_max) {
           __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }

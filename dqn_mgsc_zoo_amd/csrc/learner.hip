@@ -58,6 +58,7 @@ struct dqz_learner {
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
+  unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
 
@@ -350,7 +351,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16};
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16, L->spin_max};
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -367,7 +368,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8};
+  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8,
+                       L->spin_max};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
   const int grid = 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 16 * B8;
@@ -455,6 +457,19 @@ int dqz_learner_sync_status(dqz_learner* L, int* status) {
     // the steps since the previous check as invalid.
     DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
     DQZ_HIP(hipDeviceSynchronize());
+  }
+  return DQZ_OK;
+}
+
+int dqz_learner_debug_stall(dqz_learner* L, int sample, unsigned spin_max) {
+  if (!L) return fail(DQZ_ERR_INVALID, "null learner");
+  if (sample >= L->cfg.batch) return fail(DQZ_ERR_INVALID, "sample out of range");
+  L->spin_max = spin_max ? spin_max : 1u << 24;
+  if (sample >= 0) {  // sample's dy2 arrival counter far below its 8 arrivals: its waits run out
+    const int32_t poison = -(1 << 30);
+    DQZ_HIP(hipDeviceSynchronize());
+    DQZ_HIP(hipMemcpy(L->sync + (int64_t)sample * Handoff::kStride, &poison, sizeof(poison),
+                      hipMemcpyHostToDevice));
   }
   return DQZ_OK;
 }

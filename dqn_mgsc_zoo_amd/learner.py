@@ -168,6 +168,11 @@ class Learner:
     _native.check(_native.lib().dqz_learner_sync_status(self._h, ctypes.byref(st)))
     return st.value
 
+  def debug_stall(self, sample, spin_max=0):
+    """Test hook (dqz_learner_debug_stall): poison `sample`'s dy2 hand-off
+    counter (sample >= 0) and cap the bounded spin at `spin_max` polls."""
+    _native.check(_native.lib().dqz_learner_debug_stall(self._h, int(sample), int(spin_max)))
+
   def q_values(self, states, params=None, stream=None):
     """network.apply(params, s).q_values for uint8 [n,84,84,4] device states."""
     params = self.online if params is None else params

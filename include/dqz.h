@@ -173,6 +173,13 @@ int dqz_learner_outputs(dqz_learner* learner, float* q_tm1, float* td, float* lo
  * the steps since their previous check as invalid. */
 int dqz_learner_sync_status(dqz_learner* learner, int* status);
 
+/* Diagnostic (tests): the bounded hand-off spin gives up after `spin_max`
+ * polls from the next step on (0 restores the default 2^24), and if sample
+ * >= 0 that sample's dy2 arrival counter is poisoned so the next step's
+ * waits on it run out — the timeout path of dqz_learner_sync_status,
+ * exercised.  Synchronises the device. */
+int dqz_learner_debug_stall(dqz_learner* learner, int sample, unsigned spin_max);
+
 /* Q-values of the NatureQNetwork for uint8 HWC states [n][84][84][4]
  * (network.apply(...).q_values, networks.py:352-363; used by select_action,
  * dqn/agent.py:121-131).  q_out: device f32 [n][A]. n <= learner batch. */

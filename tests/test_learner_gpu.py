@@ -321,3 +321,33 @@ def test_nonfinite_loss_is_flagged(device):
   lrn.step(st, slots)
   assert lrn.sync_status() == 2
   assert lrn.sync_status() == 0
+
+
+def test_handoff_timeout_is_reported_and_cleared(device):
+  """A hand-off wait that runs out (one sample's dy2 counter poisoned, the
+  bounded spin shortened) sets bit 0 of the health word; reading it clears
+  every hand-off word, and the next step from the same state equals a clean
+  learner's bit for bit."""
+  _, lrn, st, _, _, _, _, _ = _setup('dqn', 32, seed=8)
+  _, ref, _, _, _, _, _, _ = _setup('dqn', 32, seed=8)
+  rng = np.random.default_rng(9)
+
+  def slots():
+    return torch.from_numpy(rng.integers(0, st.capacity, size=32).astype(np.int32)).to(device)
+
+  s0 = slots()
+  lrn.step(st, s0)
+  ref.step(st, s0)
+  lrn.debug_stall(3, spin_max=4096)
+  lrn.step(st, slots())
+  assert lrn.sync_status() & 1
+  assert lrn.sync_status() == 0
+  lrn.debug_stall(-1)  # default spin limit again
+  for which in ('online', 'target', 'mu', 'nu'):
+    getattr(lrn, which).copy_(getattr(ref, which))
+  s1 = slots()
+  lrn.step(st, s1)
+  ref.step(st, s1)
+  assert lrn.sync_status() == 0 and ref.sync_status() == 0
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(lrn, which), getattr(ref, which)), which
