@@ -243,6 +243,8 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 // weight slices before they poll.  Dynamic LDS = conv1's 65 KB (2 blocks/CU:
 // conv1 and conv2 are co-resident from the start, conv3 blocks dispatch as
 // conv1 blocks retire).
+static_assert(C2L_WIN * sizeof(float) <= kConv1FwdSmem && C3L_WIN * sizeof(float) <= kConv1FwdSmem,
+              "fwd_conv_kernel's dynamic LDS holds every body's window");
 __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int zb = c1.Z * c1.B, n = 4 * ((zb + 7) / 8 * 8);
