@@ -94,6 +94,25 @@ def forward(params, s, shared_bias=False):
   return q, cache
 
 
+def relu_margin(params, s):
+  """Smallest |pre-activation| / largest |pre-activation| over the four ReLU
+  layers of the forward on uint8 states s.  The ReLU derivative jumps at 0,
+  so an f32 implementation can take the other side of the kink than fp64 for
+  a pre-activation within its rounding of 0 (~1e-7 of the layer's scale) and
+  move a whole unit's gradient contribution: gradient parity tests draw
+  inputs that keep this margin (tests/helpers.kink_free_slots)."""
+  x = np.asarray(s).astype(np.float64) / 255.0
+  margin = np.inf
+  for (k, st, _, co), name in zip(CONV_SPECS, CONV_NAMES):
+    z = _im2col(x, k, st) @ np.asarray(params[name]['w'], np.float64).reshape(-1, co) + \
+        np.asarray(params[name]['b'], np.float64)
+    margin = min(margin, np.abs(z).min() / np.abs(z).max())
+    x = np.maximum(z, 0.0)
+  z = x.reshape(x.shape[0], -1) @ np.asarray(params[_HEAD + '/linear']['w'], np.float64) + \
+      np.asarray(params[_HEAD + '/linear']['b'], np.float64)
+  return min(margin, np.abs(z).min() / np.abs(z).max())
+
+
 def backward(params, cache, dq, shared_bias=False):
   """Gradient tree of sum(dq * q) w.r.t. the online parameters."""
   grads = {}

@@ -48,3 +48,20 @@ def perturbed_tree(tree, seed, scale=0.02):
   rng = np.random.default_rng(seed)
   return {m: {n: (v + scale * rng.standard_normal(v.shape)).astype(np.float32)
               for n, v in d.items()} for m, d in tree.items()}
+
+
+def kink_free_slots(params, host, capacity, batch, rng, margin=1e-6, tries=64):
+  """Draws slots (rng.integers, as the tests did before) until the online
+  forward on their s_tm1 stacks keeps every ReLU pre-activation at least
+  `margin` x its layer's largest |value| away from 0 (oracle relu_margin):
+  elementwise gradient / optimizer-state comparisons against fp64 are only
+  meaningful away from the kink (seen: a conv2 pre-activation of 7.8e-8 at
+  scale 0.54 flipped with a change of f32 summation order and moved the
+  conv1 gradient by 2e-3 of its largest entry)."""
+  from oracle import learner_ref
+  for _ in range(tries):
+    slots = rng.integers(0, capacity, size=batch).astype(np.int32)
+    s = stacks_from(host['frames'], host['fidx'], slots, 0)
+    if learner_ref.relu_margin(params, s) >= margin:
+      return slots
+  raise AssertionError('no kink-free batch in %d draws' % tries)

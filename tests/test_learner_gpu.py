@@ -72,7 +72,7 @@ def test_learner_step_matches_oracle(device, algo, nonzero):
   net, lrn, st, host, online, target, mu, nu = _setup(
       algo, batch, seed=11 if nonzero else 3, nonzero_opt_state=nonzero)
   rng = np.random.default_rng(5)
-  slots = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+  slots = helpers.kink_free_slots(online, host, st.capacity, batch, rng)
   weights = None
   if algo == 'per':
     weights = rng.uniform(0.2, 1.0, size=batch).astype(np.float32)
@@ -130,7 +130,7 @@ def test_multi_step_with_target_sync(device):
   rng = np.random.default_rng(9)
   p, t = online, target
   for step in range(3):
-    slots = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+    slots = helpers.kink_free_slots(p, host, st.capacity, batch, rng)
     s_tm1 = helpers.stacks_from(host['frames'], host['fidx'], slots, 0)
     s_t = helpers.stacks_from(host['frames'], host['fidx'], slots, 1)
     ref = learner_ref.learner_step(
@@ -201,7 +201,7 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
       algo, batch, capacity=96, num_frames=260, num_actions=num_actions,
       seed=31 + batch)
   rng = np.random.default_rng(batch)
-  slots = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+  slots = helpers.kink_free_slots(online, host, st.capacity, batch, rng)
   weights = None
   if algo == 'per':
     weights = rng.uniform(0.2, 1.0, size=batch).astype(np.float32)

@@ -56,7 +56,7 @@ def test_learner_grad_matches_oracle(device, algo):
   lrn = learner_lib.Learner(net, 32, algo=algo)
   lrn.set_params(online, target)
   st, host = _store(128, 320, 6, 7, device)
-  slots = np.random.default_rng(8).integers(0, 128, 32).astype(np.int32)
+  slots = helpers.kink_free_slots(online, host, 128, 32, np.random.default_rng(8))
   s_tm1 = helpers.stacks_from(host['frames'], host['fidx'], slots, 0)
   s_t = helpers.stacks_from(host['frames'], host['fidx'], slots, 1)
   z = learner_ref.zeros_like_tree(online)

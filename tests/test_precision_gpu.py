@@ -37,7 +37,8 @@ def test_learner_error_vs_fp64(device, seed):
   for name, arr in (('frames', frames), ('fidx', fidx), ('action', action),
                     ('reward', reward), ('discount', discount)):
     getattr(st, name).copy_(torch.from_numpy(arr))
-  slots = np.random.default_rng(400 + seed).integers(0, 256, 32).astype(np.int32)
+  host = dict(frames=frames, fidx=fidx)
+  slots = helpers.kink_free_slots(online, host, 256, 32, np.random.default_rng(400 + seed))
   s_tm1 = helpers.stacks_from(frames, fidx, slots, 0)
   s_t = helpers.stacks_from(frames, fidx, slots, 1)
   z = learner_ref.zeros_like_tree(online)
