@@ -522,6 +522,9 @@ def run_gpu(args, g, rem):
       'scaling': 'weak',
       'vs_baseline': None,
       'dtype': 'f32',
+      'numerics': 'f32 everywhere; conv1 fwd / dW on bf16 MFMA with exact operands '
+                  '(integer pixels x three-piece exact bf16 splits of the f32 weights / dy1: '
+                  'every product exact, f32 accumulation)',
       'data': 'synthetic (uint8 U{0..255} frames, 1000-transition episodes, '
               'random-init NatureQNetwork)',
       'config': {'workload': 'BASELINE config 2: dqn agent learner-only loop, '
