@@ -80,8 +80,9 @@ def test_bench_prices_every_reportable_phase():
     for n in names:
       assert n in flops and n in nbytes and n in bench.PHASE_KERNEL, n
       assert nbytes[n] > 0, n
-  # the launches together count each FLOP of the step once
-  f = bench.phase_flops('dqn', 32)
-  assert sum(f.values()) == bench.STEP_FLOP['dqn']
-  f = bench.phase_flops('double', 32)
-  assert sum(f.values()) == bench.STEP_FLOP['double']
+  # the launches together count each FLOP of the step once (conv_fwd is the
+  # one launch of conv1..conv3, reported instead of their three phases)
+  for algo in ('dqn', 'double'):
+    f = bench.phase_flops(algo, 32)
+    assert f['conv_fwd'] == f['conv1_fwd'] + f['conv2_fwd'] + f['conv3_fwd']
+    assert sum(v for k, v in f.items() if k != 'conv_fwd') == bench.STEP_FLOP[algo]
