@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 // block indices (workgroups are dispatched in index order), so every wait
 // terminates; each range starts at a multiple of 8, so a sample's producer
 // and consumer blocks share an XCD (and its L2).  Consumers stage their
-// weight slices before they poll.  Dynamic LDS = conv1's 65 KB (2 blocks/CU:
+// weight slices before they poll.  Dynamic LDS = conv1's 57.6 KB (2 blocks/CU:
 // conv1 and conv2 are co-resident from the start, conv3 blocks dispatch as
 // conv1 blocks retire).
 static_assert(C2L_WIN * sizeof(float) <= kConv1FwdSmem && C3L_WIN * sizeof(float) <= kConv1FwdSmem,
