@@ -6,11 +6,14 @@ product entry point raises `NativeLibraryError`.
 """
 
 import ctypes
+import glob
+import hashlib
 import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DQZ_LIB') or os.path.join(_HERE, 'libdqz.so')
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), 'include', 'dqz.h')
 
 DQZ_OK = 0
 ALGO_DQN = 0
@@ -105,6 +108,7 @@ _i64 = ctypes.c_int64
 _int = ctypes.c_int
 SIGNATURES = {
     'dqz_last_error': (ctypes.c_char_p, []),
+    'dqz_build_id': (ctypes.c_char_p, []),
     'dqz_param_layout': (
         _int,
         [_int, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
@@ -187,6 +191,34 @@ _lib = None
 _lock = threading.Lock()
 
 
+def source_files():
+  """The files a libdqz.so is compiled from: csrc/*.hip, csrc/*.hpp, dqz.h."""
+  files = sorted(glob.glob(os.path.join(_HERE, 'csrc', '*.hip')) +
+                 glob.glob(os.path.join(_HERE, 'csrc', '*.hpp')))
+  return files + [HEADER_PATH]
+
+
+def source_build_id():
+  """First 16 hex digits of SHA-256 over the library's sources on disk.
+
+  __graft_entry__.build() bakes this into the library (dqz_build_id); lib()
+  refuses a library whose id differs, so a GPU run cannot silently test a
+  stale binary.
+  """
+  h = hashlib.sha256()
+  for f in source_files():
+    h.update(os.path.basename(f).encode() + b'\0')
+    with open(f, 'rb') as fh:
+      h.update(fh.read())
+    h.update(b'\0')
+  return h.hexdigest()[:16]
+
+
+def build_id():
+  """The id baked into the loaded library."""
+  return lib().dqz_build_id().decode()
+
+
 def lib():
   """Loads libdqz.so once; raises NativeLibraryError if it is unavailable."""
   global _lib
@@ -206,6 +238,13 @@ def lib():
         fn = getattr(handle, name)
         fn.restype = restype
         fn.argtypes = argtypes
+      got, want = handle.dqz_build_id().decode(), source_build_id()
+      # DQZ_ALLOW_STALE=1 is for tools/abv.sh A/Bs of prebuilt variants only.
+      if got != want and os.environ.get('DQZ_ALLOW_STALE') != '1':
+        raise NativeLibraryError(
+            '%s was built from other sources (build id %s, sources on disk %s):'
+            ' rebuild it with `python -c "import __graft_entry__ as g; '
+            'g.build()"`.' % (LIB_PATH, got, want))
       _lib = handle
   return _lib
 

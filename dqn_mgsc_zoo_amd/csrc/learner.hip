@@ -79,6 +79,11 @@ extern "C" {
 
 const char* dqz_last_error(void) { return err_buf().c_str(); }
 
+#ifndef DQZ_BUILD_ID
+#define DQZ_BUILD_ID "unset"
+#endif
+const char* dqz_build_id(void) { return DQZ_BUILD_ID; }
+
 int dqz_param_layout(int num_actions, int shared_bias, int64_t offsets[10], int64_t sizes[10], int64_t* total) {
   if (num_actions < 1 || num_actions > MAXA) return fail(DQZ_ERR_INVALID, "num_actions must be in [1, %d]", MAXA);
   if (!offsets || !sizes || !total) return fail(DQZ_ERR_INVALID, "null output pointer");

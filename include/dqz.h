@@ -50,6 +50,13 @@ extern "C" {
 /* Thread-local message for the last failing call on this thread. */
 const char* dqz_last_error(void);
 
+/* Source hash this library was compiled from: the first 16 hex digits of the
+ * SHA-256 over csrc/ (every .hip / .hpp) and include/dqz.h, baked in at build
+ * time (__graft_entry__.build()).  The Python loader refuses a library whose
+ * id differs from the sources beside it, so a GPU run proves which kernels it
+ * tested.  "unset" when built without the id. */
+const char* dqz_build_id(void);
+
 /* Flat parameter layout of the NatureQNetwork (networks.py:181-221,352-363):
  * leaves in Haiku order
  *   0 conv2_d/w [8,8,4,32]   1 conv2_d/b [32]

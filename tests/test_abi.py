@@ -86,3 +86,25 @@ def test_bench_prices_every_reportable_phase():
     f = bench.phase_flops(algo, 32)
     assert f['conv_fwd'] == f['conv1_fwd'] + f['conv2_fwd'] + f['conv3_fwd']
     assert sum(v for k, v in f.items() if k != 'conv_fwd') == bench.STEP_FLOP[algo]
+
+
+def test_library_build_id_matches_sources(libdqz):
+  """The loaded libdqz.so was compiled from the sources on disk."""
+  from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+  assert libdqz.dqz_build_id  # exported
+  assert _native.build_id() == _native.source_build_id()
+  assert len(_native.source_build_id()) == 16
+
+
+def test_stale_library_is_refused(monkeypatch):
+  """lib() raises when the library's id differs from the sources."""
+  from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+  saved = _native._lib  # pylint: disable=protected-access
+  try:
+    monkeypatch.setattr(_native, '_lib', None)
+    monkeypatch.setattr(_native, 'source_build_id', lambda: '0' * 16)
+    monkeypatch.delenv('DQZ_ALLOW_STALE', raising=False)
+    with pytest.raises(_native.NativeLibraryError, match='other sources'):
+      _native.lib()
+  finally:
+    _native._lib = saved  # pylint: disable=protected-access

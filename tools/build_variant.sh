@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a libdqz variant with extra -D flags: bash tools/build_variant.sh NAME [flags...]
+# (same sources and build id as libdqz.so; only the -D flags differ)
 set -e
 N=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -Iinclude \
-  -o dqn_mgsc_zoo_amd/libdqz_$N.so dqn_mgsc_zoo_amd/csrc/learner.hip
+python -c "import sys, __graft_entry__ as g; g._compile_lib('dqn_mgsc_zoo_amd/libdqz_$N.so', sys.argv[1:])" "$@"
