@@ -11,7 +11,14 @@ loss with clip_gradient -> backward -> centered RMSProp; the target copy
 runs every 2,500 steps (40,000 frames / learn_period 16) inside the timed
 loop.  Replicas are independent seeds (no gradient all-reduce); RCCL only
 all-gathers a per-rank statistics vector every 1,000 steps (SURVEY.md §8(d)
-config 4) and after the timed region.
+config 4) and after the timed region.  The process group exists at every
+world size, so the 1-GPU line goes through the same RCCL calls.
+
+`--algo` picks the BASELINE config the step follows: dqn (config 2, the
+default and the headline line), double (double-Q on the same uniform
+replay), per (config 4: device PER sample over a 2^20-leaf fp64 sum tree +
+double-Q step with IS weights + |td|^alpha write-back) or mgsc (config 3's
+learner part: softmax-CDF sample over 1M learned f32 logits + DQN step).
 
 Prints ONE JSON line on rank 0.
 """
@@ -37,8 +44,22 @@ BATCH = 32
 NUM_ACTIONS = 6  # Pong minimal action set (gym_atari.py:52-54)
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32 = f32 vector peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-STEP_FLOP = {'dqn': 2182873088, 'double': 2781020160}
-STEP_BYTES = {'dqn': 49048488, 'double': 49048488}
+STEP_FLOP = {'dqn': 2182873088, 'double': 2781020160,
+             'per': 2781020160, 'mgsc': 2182873088}
+# SURVEY.md §8(d); MGSC sampling adds one read of the 1M f32 logits
+STEP_BYTES = {'dqn': 49048488, 'double': 49048488, 'per': 49048488,
+              'mgsc': 53048488}
+LEARNER_ALGO = {'dqn': 'dqn', 'double': 'double', 'per': 'per', 'mgsc': 'dqn'}
+WORKLOAD = {
+    'dqn': 'BASELINE config 2: dqn agent learner-only loop',
+    'double': 'double_q learner-only loop (uniform replay, shared-bias head)',
+    'per': 'BASELINE config 4: prioritized (PER sum-tree sample + IS weights, '
+           'double-Q, |td|^alpha write-back) learner-only loop',
+    'mgsc': 'BASELINE config 3 learner part: dqn_mgsc_batched reservoir, '
+            'softmax sample over N(0,1) learned logits + DQN step',
+}
+PER_ALPHA, PER_BETA, PER_USP = 0.6, 0.4, 1e-3  # prioritized/run_atari.py:104-114
+STATS_LEN = 3  # the in-loop RCCL statistics vector: steps, loss, seconds
 
 ALL_BWD = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw'
 
@@ -49,6 +70,7 @@ MAC = dict(conv1=400 * 256 * 32, conv2=81 * 512 * 64, conv3=49 * 576 * 64,
 
 def phase_flops(algo, batch):
   """Algorithmic FLOPs of each libdqz phase (one launch each)."""
+  algo = LEARNER_ALGO.get(algo, algo)
   z = 2 if algo == 'dqn' else 3
   b = batch
   return {
@@ -82,6 +104,7 @@ def phase_bytes(algo, batch):
   writes theta, mu, nu (6 x 4 B per parameter); fc1's update runs inside the
   merged backward launch.
   """
+  algo = LEARNER_ALGO.get(algo, algo)
   z = 2 if algo == 'dqn' else 3
   b = batch
   rms = 6 * (sum(PARAM.values()) - PARAM['fc1'])
@@ -140,6 +163,7 @@ def cpu_baseline(seconds, algo):
   """
   from oracle import torch_cpu  # pylint: disable=g-import-not-at-top
   from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
+  algo = LEARNER_ALGO[algo]
   net = (networks.dqn_atari_network(NUM_ACTIONS) if algo == 'dqn' else
          networks.double_dqn_atari_network(NUM_ACTIONS))
   allotted = int(os.environ.get('OMP_NUM_THREADS', '0') or 0)
@@ -159,7 +183,8 @@ def cpu_baseline(seconds, algo):
       a = torch.randint(0, NUM_ACTIONS, (BATCH,), generator=gen)
       r = torch.zeros(BATCH)
       d = torch.full((BATCH,), 0.99)
-      lrn.step(s_tm1, a, r, d, s_t)
+      w = torch.rand((BATCH,), generator=gen) if algo == 'per' else None
+      lrn.step(s_tm1, a, r, d, s_t, weights=w)
       if t0 is None:  # the first step pays one-off allocation; not timed
         t0 = time.perf_counter()
         continue
@@ -293,7 +318,8 @@ def parse_args(argv=None):
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=5000)
   ap.add_argument('--warmup', type=int, default=200)
-  ap.add_argument('--algo', default='dqn', choices=['dqn', 'double'])
+  ap.add_argument('--algo', default='dqn',
+                  choices=['dqn', 'double', 'per', 'mgsc'])
   ap.add_argument('--capacity', type=int, default=1_000_000)
   ap.add_argument('--graph', type=int, default=1, help='hipGraph-replay steps')
   ap.add_argument('--graph-steps', type=int, default=50)
@@ -366,8 +392,10 @@ def selftest_cpu(args, g, rem):
   def sync_target():
     counters['syncs'] += 1
 
+  last = {}
+
   def on_stats(done):
-    reps.gather_stats([float(done), float(x[0, 0])])
+    last['stats'] = reps.gather_stats([float(done), float(x[0, 0])])
     counters['gathers'] += 1
 
   graphs = {k: _Graph(k) for k in (g, rem) if k > 1}
@@ -389,10 +417,119 @@ def selftest_cpu(args, g, rem):
         'chunks': [g, rem],
         'per_rank_steps': [int(v) for v in per_rank[:, 0]],
         'per_rank_target_syncs': [int(v) for v in per_rank[:, 2]],
-        'per_rank_stats_gathers': [int(v) for v in per_rank[:, 3]]}),
+        'per_rank_stats_gathers': [int(v) for v in per_rank[:, 3]],
+        'rccl': {'backend': reps.backend, 'world': reps.world,
+                 'last_in_loop_gather': {
+                     'steps_done': [int(v) for v in last['stats'][:, 0]],
+                     'value': [float(v) for v in last['stats'][:, 1]]}}}),
           flush=True)
   reps.close()
   return 0
+
+
+class Workload:
+  """One BASELINE config's step on device: the learner, the replay it reads,
+  `one_step()` (everything a step launches, capturable in a hipGraph) and
+  the sampler launches to time apart from the learner phases."""
+
+  def __init__(self, algo, capacity, rank, dev):
+    from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import synthetic  # pylint: disable=g-import-not-at-top
+    self.algo = algo
+    la = LEARNER_ALGO[algo]
+    net = (networks.dqn_atari_network(NUM_ACTIONS) if la == 'dqn' else
+           networks.double_dqn_atari_network(NUM_ACTIONS))
+    self.lrn = lrn = learner_lib.Learner(net, BATCH, algo=la, device=dev)
+    lrn.set_params(net.init(seed=rank))
+    t_fill = time.perf_counter()
+    self.store = store = synthetic.fill_episodic(capacity, NUM_ACTIONS,
+                                                 seed=rank, device=dev)
+    self.slots = slots = torch.zeros((BATCH,), dtype=torch.int32, device=dev)
+    self.weights = None
+    self.counter = counter = torch.zeros((1,), dtype=torch.int64, device=dev)
+    seed = 1 + rank
+    lib, ptr, stream = _native.lib(), _native.ptr, _native.stream_handle
+    self.samplers = {}  # name -> launch fn (timed apart, HIP events)
+    self.sampler_bytes = {}  # name -> algorithmic bytes per launch
+
+    if algo in ('dqn', 'double'):
+      def one_step():
+        # FIFO replay full: live ids [t - size, t) = slots [0, capacity).
+        # The uniform draw is fused into the step's conv1 kernel.
+        lrn.step_uniform(store, 0, capacity, capacity, seed, counter, slots)
+    elif algo == 'per':
+      # 2^20-leaf fp64 sum tree over alpha-exponentiated random priorities
+      tcap = 1 << max(1, (capacity - 1).bit_length())
+      gen = torch.Generator(device=dev)
+      gen.manual_seed(100 + rank)
+      self.tree = tree = torch.zeros((2 * tcap,), dtype=torch.float64, device=dev)
+      pri = torch.rand((capacity,), generator=gen, dtype=torch.float64,
+                       device=dev) * 1.99 + 0.01
+      idx_all = torch.arange(capacity, dtype=torch.int64, device=dev)
+      pri = pri ** PER_ALPHA
+      for s0 in range(0, capacity, 65536):  # <= 65536 leaves per call
+        n = min(65536, capacity - s0)
+        _native.check(lib.dqz_sumtree_set(
+            ptr(tree), tcap, ptr(idx_all[s0:s0 + n]), ptr(pri[s0:s0 + n]), n,
+            stream()))
+      self.weights = w = torch.zeros((BATCH,), dtype=torch.float32, device=dev)
+      self.max_seen = max_seen = torch.ones((1,), dtype=torch.float64, device=dev)
+
+      def per_sample():
+        _native.check(lib.dqz_per_sample(
+            ptr(tree), tcap, 0, capacity, capacity, BATCH, PER_USP, PER_BETA,
+            1, seed, ptr(counter), None, None, None, None, ptr(slots), ptr(w),
+            None, stream()))
+
+      def per_write_back():
+        _native.check(lib.dqz_per_write_back(
+            lrn._h, ptr(tree), tcap, ptr(slots), PER_ALPHA, ptr(max_seen),  # pylint: disable=protected-access
+            stream()))
+
+      def one_step():
+        per_sample()
+        lrn.step(store, slots, w)
+        per_write_back()
+      self.samplers = {'per_sample': per_sample, 'per_write_back': per_write_back}
+    elif algo == 'mgsc':
+      from dqn_mgsc_zoo_amd import replay_circular as rc  # pylint: disable=g-import-not-at-top
+      gen = torch.Generator(device=dev)
+      gen.manual_seed(200 + rank)
+      self.logit_buf = lb = rc._DeviceLogits(capacity, dev, max_queries=BATCH)  # pylint: disable=protected-access
+      lb.logits.copy_(torch.randn((capacity,), generator=gen, device=dev))
+      lb.invalidate()
+
+      def mgsc_sample():
+        lb.sample_slots_philox(seed, counter, slots)
+
+      def one_step():
+        mgsc_sample()
+        lrn.step(store, slots)
+      self.samplers = {'logits_sample': mgsc_sample}
+      self.sampler_bytes = {'logits_sample': 4 * capacity}
+    else:
+      raise ValueError(algo)
+    self.one_step = one_step
+    torch.cuda.synchronize(dev)
+    self.fill_s = time.perf_counter() - t_fill
+
+  def time_samplers(self, iters):
+    """Average ms per launch of each sampler call, back to back on the
+    launch stream (HIP events on that stream)."""
+    out = {}
+    for name, fn in self.samplers.items():
+      fn()
+      e0 = torch.cuda.Event(enable_timing=True)
+      e1 = torch.cuda.Event(enable_timing=True)
+      e0.record()
+      for _ in range(iters):
+        fn()
+      e1.record()
+      e1.synchronize()
+      out[name] = e0.elapsed_time(e1) / iters
+    return out
 
 
 def run_gpu(args, g, rem):
@@ -406,29 +543,9 @@ def run_gpu(args, g, rem):
     return 2
   dev = torch.device('cuda', local_rank)
 
-  from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
-  from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
-  from dqn_mgsc_zoo_amd import synthetic  # pylint: disable=g-import-not-at-top
-
   algo = args.algo
-  net = (networks.dqn_atari_network(NUM_ACTIONS) if algo == 'dqn' else
-         networks.double_dqn_atari_network(NUM_ACTIONS))
-  lrn = learner_lib.Learner(net, BATCH, algo=algo, device=dev)
-  lrn.set_params(net.init(seed=rank))
-  t_fill = time.perf_counter()
-  store = synthetic.fill_episodic(args.capacity, NUM_ACTIONS, seed=rank,
-                                  device=dev)
-  torch.cuda.synchronize(dev)
-  t_fill = time.perf_counter() - t_fill
-  slots = torch.zeros((BATCH,), dtype=torch.int32, device=dev)
-  counter = torch.zeros((1,), dtype=torch.int64, device=dev)
-  seed = 1 + rank
-
-  def one_step():
-    # FIFO replay full: live ids [t - size, t) = slots [0, capacity).  The
-    # uniform draw is fused into the step's conv1 kernel.
-    lrn.step_uniform(store, 0, args.capacity, args.capacity, seed, counter,
-                     slots)
+  wl = Workload(algo, args.capacity, rank, dev)
+  lrn, store, slots, one_step = wl.lrn, wl.store, wl.slots, wl.one_step
 
   graphs = {}
   if args.graph:
@@ -445,19 +562,21 @@ def run_gpu(args, g, rem):
           for _ in range(k):
             one_step()
 
-  # statistics vector [steps done, last loss], all-gathered over RCCL every
-  # stats_every steps (enqueued, never waited on inside the timed region)
-  stats_vec = torch.zeros((2,), dtype=torch.float64, device=dev)
-  gathered = torch.zeros((world, 2), dtype=torch.float64, device=dev)
+  # Statistics vector [steps done, last loss, seconds since the timed region
+  # began], all-gathered over RCCL every stats_every steps: enqueued on the
+  # stream, never waited for inside the timed region, read after it.
+  stats_vec = torch.zeros((STATS_LEN,), dtype=torch.float64, device=dev)
+  gathered = torch.zeros((world, STATS_LEN), dtype=torch.float64, device=dev)
   pending = []
+  clock = {'t0': time.perf_counter()}
 
   def on_stats(done):
     lrn.fetch_outputs()
     stats_vec[0].fill_(float(done))
     stats_vec[1].copy_(lrn.loss[0])
-    if reps.dist is not None:
-      pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
-                                                      async_op=True))
+    stats_vec[2].fill_(time.perf_counter() - clock['t0'])
+    pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
+                                                    async_op=True))
 
   runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
                       args.stats_every, on_stats)
@@ -465,20 +584,27 @@ def run_gpu(args, g, rem):
   for k in graphs:  # first replay of each graph uploads it: keep it untimed
     runner.run(k, k, 0)
   warm_steps = runner.done
+  pending.clear()  # warm-up gathers are not reported
+  torch.cuda.synchronize(dev)
+  clock['t0'] = time.perf_counter()
   elapsed = _timed(reps, runner, args.steps, g, rem,
                    lambda: torch.cuda.synchronize(dev))
   steps = args.steps
   for w in pending:
     w.wait()
+  in_loop = gathered.cpu().numpy() if pending else None
   status = lrn.sync_status()  # in-launch hand-off health over every step run
   elapsed_max = reps.max_over_ranks(elapsed, device=dev)
   status_max = reps.max_over_ranks(float(status), device=dev)
-  per_rank = reps.gather_stats([steps / elapsed, elapsed], device=dev)
+  lrn.fetch_outputs()
+  per_rank = reps.gather_stats([steps / elapsed, elapsed, float(steps),
+                                float(lrn.loss[0].item())], device=dev)
 
   # Per-phase device time (HIP events on the launch stream) for the roofline.
-  phases = lrn.profile(store, slots, iters=args.profile_iters)
+  phases = lrn.profile(store, slots, weights=wl.weights, iters=args.profile_iters)
   if 'conv1_fwd' in phases and 'conv2_fwd' not in phases:  # the one conv1..conv3 launch
     phases = {('conv_fwd' if k == 'conv1_fwd' else k): v for k, v in phases.items()}
+  sampler_ms = wl.time_samplers(args.profile_iters)
   q_tm1, td, loss = lrn.fetch_outputs()
   torch.cuda.synchronize(dev)
   finite = bool(torch.isfinite(lrn.online).all().item())
@@ -491,8 +617,14 @@ def run_gpu(args, g, rem):
   value = world * steps / elapsed_max
   flops = phase_flops(algo, BATCH)
   nbytes = phase_bytes(algo, BATCH)
-  dom = max(phases, key=phases.get)
-  dom_ms = phases[dom]
+  timed_phases = dict(phases)
+  for k, v in sampler_ms.items():
+    if k in wl.sampler_bytes:  # HBM-bound samplers compete for the roofline
+      timed_phases[k] = v
+      flops[k] = 0
+      nbytes[k] = wl.sampler_bytes[k]
+  dom = max(timed_phases, key=timed_phases.get)
+  dom_ms = timed_phases[dom]
   # The bound is whichever roof the kernel sits closer to.
   tflops = flops[dom] / (dom_ms * 1e-3) / 1e12
   gbs = nbytes[dom] / (dom_ms * 1e-3) / 1e9
@@ -507,14 +639,29 @@ def run_gpu(args, g, rem):
             'unit': 'GB/s', 'frac': round(hbm_frac, 4)}
   roof.update({
       'traffic': pmc_traffic(dom) if algo == 'dqn' else None,
-      'kernel': PHASE_KERNEL[dom] + ' (' + dom + ')',
+      'kernel': PHASE_KERNEL.get(dom, dom) + ' (' + dom + ')',
       'kernel_ms': round(dom_ms, 5),
       'algorithmic_flop_per_launch': flops[dom],
       'algorithmic_bytes_per_launch': nbytes[dom],
-      'mfma_frac': round(mfma_frac, 4), 'hbm_frac': round(hbm_frac, 4)})
+      'mfma_frac': round(mfma_frac, 4), 'hbm_frac': round(hbm_frac, 4),
+      'flop_basis': 'algorithmic f32-equivalent FLOP over the exact-f32 MFMA '
+                    'peak; conv1 fwd / dW issue three bf16 piece products per '
+                    'multiply on bf16 MFMA, counted once here'})
   per_gpu = steps / elapsed
   step_tflops = STEP_FLOP[algo] * per_gpu / 1e12
   step_gbs = STEP_BYTES[algo] * per_gpu / 1e9
+  rccl = {'backend': reps.backend, 'world': world,
+          'in_loop_gathers': len(pending), 'stats_every': args.stats_every,
+          'final_gather': {'steps_per_s': [round(float(x), 2) for x in per_rank[:, 0]],
+                           'steps': [int(x) for x in per_rank[:, 2]],
+                           'last_loss': [float(x) for x in per_rank[:, 3]],
+                           'loss_mean': float(per_rank[:, 3].mean())}}
+  if in_loop is not None:
+    rccl['last_in_loop_gather'] = {
+        'steps_done': [int(x) for x in in_loop[:, 0]],
+        'loss': [float(x) for x in in_loop[:, 1]],
+        'loss_mean': float(in_loop[:, 1].mean()),
+        'seconds': [round(float(x), 4) for x in in_loop[:, 2]]}
   out = {
       'metric': METRIC,
       'value': round(value, 2),
@@ -532,10 +679,9 @@ def run_gpu(args, g, rem):
                   'every product exact, f32 accumulation)',
       'data': 'synthetic (uint8 U{0..255} frames, 1000-transition episodes, '
               'random-init NatureQNetwork)',
-      'config': {'workload': 'BASELINE config 2: dqn agent learner-only loop, '
-                             'synthetic 84x84x4 uint8 replay pre-filled to %d, '
-                             'batch=32, A=%d, algo=%s' % (
-                                 args.capacity, NUM_ACTIONS, algo),
+      'config': {'workload': '%s, synthetic 84x84x4 uint8 replay pre-filled to '
+                             '%d, batch=32, A=%d, algo=%s' % (
+                                 WORKLOAD[algo], args.capacity, NUM_ACTIONS, algo),
                  'global_batch': BATCH * world, 'replay_capacity': args.capacity,
                  'parallelism': 'independent-seed replicas x%d' % world,
                  'hipgraph_chunks': [g, rem],
@@ -548,17 +694,22 @@ def run_gpu(args, g, rem):
           'frac_hbm': round(step_gbs / HBM_PEAK_GBS, 4),
           'flop_per_step': STEP_FLOP[algo], 'bytes_per_step': STEP_BYTES[algo]},
       'phase_ms': {k: round(v, 5) for k, v in phases.items()},
+      'sampler_us': {k: round(1e3 * v, 3) for k, v in sampler_ms.items()},
       'per_rank_steps_per_s': [round(float(x), 2) for x in per_rank[:, 0]],
       'per_gpu_min_steps_per_s': round(float(per_rank[:, 0].min()), 2),
-      'stats_gathers': len(pending),
+      'rccl': rccl,
       # learner health word (dqz_learner_sync_status): bit 0 a hand-off wait
       # gave up, bit 1 a step's mean loss was not finite
       'handoff_status': int(max(status_max, status_after)) & 1,
       'nonfinite_loss': bool(int(max(status_max, status_after)) & 2),
-      'fill_s': round(t_fill, 2),
+      'fill_s': round(wl.fill_s, 2),
       'last_loss': float(loss.item()),
       'params_finite': finite,
   }
+  if algo == 'mgsc':
+    # the reference's own per-call timings of this agent (V100 + JAX):
+    # dqn_mgsc_batched/run_atari.py:308-315
+    out['reference_per_call_ms'] = {'update': 12.24, 'replay_sample_batch': 57.1}
   if world == 1 and args.cpu_seconds > 0:
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
   else:

@@ -162,10 +162,17 @@ SIGNATURES = {
     'dqz_logit_buffer_destroy': (_int, [_vp]),
     'dqz_logits_add': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     'dqz_logits_sample': (_int, [_vp, _vp, _vp, _int, _vp, _vp]),
+    'dqz_logits_sample_slots': (
+        _int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _int, _vp, _vp, _vp]),
     'dqz_logits_probs': (_int, [_vp, _vp, _vp, _vp, _vp]),
     'dqz_logits_write': (_int, [_vp, _vp, _vp, _vp, _int, _vp]),
     'dqz_logits_put': (_int, [_vp, _vp, _i64, ctypes.c_float, _vp]),
     'dqz_logits_invalidate': (_int, [_vp]),
+    'dqz_logits_run_get': (
+        _int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float),
+               ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int), _vp]),
+    'dqz_logits_run_set': (
+        _int, [_vp, ctypes.c_double, ctypes.c_float, _int, _int, _int, _vp]),
     'dqz_uniform_philox': (_int, [ctypes.c_uint64, _vp, _int, _vp, _vp]),
     'dqz_sumtree_set': (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
     'dqz_sumtree_query': (_int, [_vp, _i64, _vp, _int, _vp, _vp]),
@@ -183,7 +190,7 @@ SIGNATURES = {
     'dqz_meta_update': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp,
-         ctypes.POINTER(DqzStore), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+         ctypes.POINTER(DqzStore), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'dqz_meta_outputs': (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
 }
 

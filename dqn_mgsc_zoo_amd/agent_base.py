@@ -12,6 +12,7 @@ replay hands it device slot indices, never stacked frames.
 """
 
 from typing import Any, Callable, Mapping
+import warnings
 
 import numpy as np
 import torch
@@ -65,6 +66,8 @@ class DeviceDqnAgent(parts.Agent):
     self._action = None
     self._frame_t = -1
     self._statistics = {'state_value': np.nan}
+    self._learn_steps = 0
+    self._nonfinite_loss_checks = 0
 
   # -- reference surface ----------------------------------------------------
 
@@ -83,9 +86,44 @@ class DeviceDqnAgent(parts.Agent):
       return action
     if self._frame_t % self._learn_period == 0:
       self._learn()
+      self._after_learn()
     if self._frame_t % self._target_network_update_period == 0:
       self._learner.sync_target()
+      self.check_learner_health()
     return action
+
+  # Learn steps between reads of the learner's health word (each read
+  # synchronises the device once; the acting path synchronises every frame
+  # anyway).
+  HEALTH_CHECK_PERIOD = 1000
+
+  def _after_learn(self) -> None:
+    self._learn_steps += 1
+    if self._learn_steps % self.HEALTH_CHECK_PERIOD == 0:
+      self.check_learner_health()
+
+  def check_learner_health(self) -> int:
+    """Reads the learner's health word (dqz_learner_sync_status).
+
+    A hand-off wait that gave up (bit 0) makes every step since the previous
+    check invalid: raises RuntimeError (reading the word has already reset
+    the hand-off words, so the learner itself can continue).  A non-finite
+    batch loss (bit 1) is counted and warned about; the update ran, as the
+    reference's jitted update would.  Called every HEALTH_CHECK_PERIOD learn
+    steps, at every target sync and from get_state.
+    """
+    status = self._learner.sync_status()
+    if status & 2:
+      self._nonfinite_loss_checks += 1
+      warnings.warn('learner: a batch loss since the last check was NaN or '
+                    'infinite (frame %d)' % self._frame_t, RuntimeWarning)
+    if status & 1:
+      raise RuntimeError(
+          'learner hand-off wait timed out between learn steps %d and %d '
+          '(frame %d): those updates are invalid' % (
+              max(0, self._learn_steps - self.HEALTH_CHECK_PERIOD),
+              self._learn_steps, self._frame_t))
+    return status
 
   def reset(self) -> None:
     self._transition_accumulator.reset()
@@ -128,6 +166,7 @@ class DeviceDqnAgent(parts.Agent):
 
   def get_state(self) -> Mapping[str, Any]:
     lrn = self._learner
+    self.check_learner_health()
     return {
         'rng_key': {'seed': self._act_seed, 'count': self._act_count},
         'frame_t': self._frame_t,

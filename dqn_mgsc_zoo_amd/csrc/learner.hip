@@ -214,12 +214,16 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c3.b_off = L->off[5];
   c3.out = L->y3;
   if (fused_conv) {
-    // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample (Z*B <= 3B samples)
-    int* hw = L->sync + 2 * B * Handoff::kStride;
-    int* err = L->sync + 16 * B * Handoff::kStride;
-    c1.pub = Handoff{hw, hw + 3 * B * Handoff::kStride, err, 4, 4};
+    // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample.  The
+    // word layout follows the learner's configured batch, not this call's n
+    // (the actor's forward has n = 1): Z * n <= 3 * cfg.batch samples, and
+    // every launch shares the one error word dqz_learner_sync_status reads.
+    const int Bc = L->cfg.batch;
+    int* hw = L->sync + 2 * Bc * Handoff::kStride;
+    int* err = L->sync + 16 * Bc * Handoff::kStride;
+    c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, 4};
     c2.wait = c1.pub;
-    c2.pub = Handoff{hw + 6 * B * Handoff::kStride, hw + 9 * B * Handoff::kStride, err, 4, 4};
+    c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, 4, 4};
     c3.wait = c2.pub;
     DQZ_PHASE(0, hipLaunchKernelGGL(fwd_conv_kernel, dim3(3 * xcd_grid(4, Z * B).x), dim3(256), kConv1FwdSmem, st, c1,
                                     c2, c3);
@@ -635,6 +639,7 @@ struct dqz_logit_buffer {
   double* bsum;
   float* lse;
   LogitRun* run;   // running log-sum-exp (sampling.hpp)
+  int* sync;       // softmax_sample_kernel's arrival / done / error words (SampleSync)
   bool run_known;  // host side: every write since the last scan went through the library
   int run_adds;    // running adds since the last scan
 };
@@ -649,16 +654,24 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->capacity = capacity;
   b->max_queries = max_queries;
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
-  const size_t bytes = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double)) + 64 + sizeof(LogitRun);
+  const size_t head = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double));
+  const size_t sync_off = (head + 64 + sizeof(LogitRun) + 255) / 256 * 256;
+  const size_t bytes = sync_off + 3 * SampleSync::kStride * sizeof(int);
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
   }
+  if (hipMemset(b->block, 0, bytes) != hipSuccess) {
+    (void)hipFree(b->block);
+    delete b;
+    return fail(DQZ_ERR_HIP, "hipMemset of logit scratch failed");
+  }
   char* p = (char*)b->block;
   b->bsum = (double*)p;
   b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
-  b->lse = (float*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
-  b->run = (LogitRun*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)) + 64);
+  b->lse = (float*)(p + head);
+  b->run = (LogitRun*)(p + head + 64);
+  b->sync = (int*)(p + sync_off);
   b->run_known = false;
   b->run_adds = 0;
   *out = b;
@@ -725,36 +738,79 @@ int dqz_logits_put(dqz_logit_buffer* b, float* logits, int64_t position, float v
   return DQZ_OK;
 }
 
+__global__ void logits_run_set_kernel(LogitRun* run, LogitRun v) {
+  if (threadIdx.x == 0) *run = v;
+}
+
+int dqz_logits_run_get(dqz_logit_buffer* b, double* S, float* c, int* valid, int* known, int* adds, void* stream) {
+  if (!b || !S || !c || !valid || !known || !adds) return fail(DQZ_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  LogitRun r{0.0, 0.f, 0};
+  DQZ_HIP(hipMemcpyAsync(&r, b->run, sizeof(LogitRun), hipMemcpyDeviceToHost, st));
+  DQZ_HIP(hipStreamSynchronize(st));
+  *S = r.S;
+  *c = r.c;
+  *valid = r.valid;
+  *known = b->run_known ? 1 : 0;
+  *adds = b->run_adds;
+  return DQZ_OK;
+}
+
+int dqz_logits_run_set(dqz_logit_buffer* b, double S, float c, int valid, int known, int adds, void* stream) {
+  if (!b) return fail(DQZ_ERR_INVALID, "null argument");
+  if (adds < 0) return fail(DQZ_ERR_INVALID, "adds must be >= 0");
+  hipLaunchKernelGGL(logits_run_set_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, b->run,
+                     LogitRun{S, c, valid ? 1 : 0});
+  DQZ_HIP(hipGetLastError());
+  b->run_known = known != 0;
+  b->run_adds = adds;
+  return DQZ_OK;
+}
+
 int dqz_logits_invalidate(dqz_logit_buffer* b) {
   if (!b) return fail(DQZ_ERR_INVALID, "null argument");
   b->run_known = false;
   return DQZ_OK;
 }
 
-int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
-                      void* stream) {
-  if (!b || !logits || !uniforms || !out_idx) return fail(DQZ_ERR_INVALID, "null argument");
-  if (n < 1 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
-  hipStream_t st = (hipStream_t)stream;
-  // pass 1 never writes when clear_pos < 0
-  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
-                     b->capacity, b->part, (int64_t)-1);
-  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
-                     b->nblocks, b->lse, b->bsum, (float*)nullptr);
-  DQZ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(softmax_choice_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->lse, b->bsum,
-                     b->nblocks, uniforms, out_idx);
+// The samplers use the running state's lse: seed it with a scan first when
+// the host cannot vouch for it.
+static int ensure_run(dqz_logit_buffer* b, const float* logits, hipStream_t st) {
+  if (b->run_known) return DQZ_OK;
+  return logits_lse(b, const_cast<float*>(logits), -1, -1, 0, nullptr, st);
+}
+
+static int logits_sample_impl(dqz_logit_buffer* b, const float* logits, uint64_t seed, uint64_t* counter_dev,
+                              const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, hipStream_t st) {
+  if (!b || !logits || (!uniforms && !counter_dev) || (!out_slots && !out_idx))
+    return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 1 || n > 65535 - b->nblocks) return fail(DQZ_ERR_INVALID, "n out of range");
+  if (out_slots && b->capacity > INT32_MAX) return fail(DQZ_ERR_INVALID, "int32 slots need capacity < 2^31");
+  if (int rc = ensure_run(b, logits, st)) return rc;
+  hipLaunchKernelGGL(softmax_sample_kernel, dim3(b->nblocks + n), dim3(SM_THREADS), 0, st, logits, b->capacity,
+                     b->run, b->bsum, b->nblocks, SampleSync{b->sync}, seed, counter_dev, uniforms, n, out_slots,
+                     out_idx);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
+}
+
+int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
+                      void* stream) {
+  if (!uniforms || !out_idx) return fail(DQZ_ERR_INVALID, "null argument");
+  return logits_sample_impl(b, logits, 0, nullptr, uniforms, n, nullptr, out_idx, (hipStream_t)stream);
+}
+
+int dqz_logits_sample_slots(dqz_logit_buffer* b, const float* logits, uint64_t seed, uint64_t* counter_dev,
+                            const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, void* stream) {
+  return logits_sample_impl(b, logits, seed, counter_dev, uniforms, n, out_slots, out_idx, (hipStream_t)stream);
 }
 
 int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, float* lse_out, void* stream) {
   if (!b || !logits || !p_out) return fail(DQZ_ERR_INVALID, "null argument");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, const_cast<float*>(logits),
-                     b->capacity, b->part, (int64_t)-1);
-  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
-                     b->nblocks, b->lse, b->bsum, p_out);
+  if (int rc = ensure_run(b, logits, st)) return rc;
+  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
+                     b->lse, b->bsum, p_out);
   DQZ_HIP(hipGetLastError());
   if (lse_out) DQZ_HIP(hipMemcpyAsync(lse_out, b->lse, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
@@ -978,7 +1034,8 @@ int dqz_meta_destroy(dqz_meta* H) {
 
 int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                     const dqz_store* S1, const int32_t* online_slot, float* logits, const int32_t* pos,
-                    float* adam_mu, float* adam_nu, int32_t* adam_count, void* stream) {
+                    float* adam_mu, float* adam_nu, int32_t* adam_count, dqz_logit_buffer* logit_buf,
+                    void* stream) {
   if (!H || !P || !P->online || !P->target || !P->mu || !P->nu || !slots || !online_slot || !logits || !pos ||
       !adam_mu || !adam_nu || !adam_count)
     return fail(DQZ_ERR_INVALID, "null argument");
@@ -1203,6 +1260,9 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.nparts = nloss;
   ad.loss = H->loss;
   ad.dlogits = H->dl;
+  // keep the buffer's running log-sum-exp current (the host keeps vouching
+  // for it: every write went through the library)
+  ad.run = logit_buf && logit_buf->run_known ? logit_buf->run : nullptr;
   hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;

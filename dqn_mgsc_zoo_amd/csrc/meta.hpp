@@ -15,6 +15,7 @@
 //        optax.adam on the logits (meta_adam_kernel).
 #pragma once
 #include "common.hpp"
+#include "sampling.hpp"
 
 namespace dqz {
 
@@ -217,6 +218,7 @@ struct MetaAdamArgs {
   int nparts;
   float* loss;
   float* dlogits;   // [M]
+  LogitRun* run;    // the logit buffer's running log-sum-exp, or null
 };
 
 // softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
@@ -231,7 +233,13 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
   lp = block_sum_f32(lp, sbuf);
   const int32_t cnt = *a.count + 1;
   const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
+  __shared__ double dbuf[META_THREADS / 64];
+  __shared__ int s_far;
+  if (threadIdx.x == 0) s_far = 0;
+  LogitRun r{0.0, 0.f, 0};
+  if (a.run) r = *a.run;
   __syncthreads();
+  double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
   for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
     const float g = a.s[i] - a.p[i] * tot;
     const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
@@ -241,7 +249,23 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
     a.m[i] = m;
     a.v[i] = v;
     a.dlogits[i] = g;
-    a.logits[a.pos[i]] = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+    const float nx = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+    a.logits[a.pos[i]] = nx;
+    if (r.valid) {
+      dS += run_term(nx, r.c) - run_term(a.x[i], r.c);
+      if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
+    }
+  }
+  // the buffer's running log-sum-exp follows the M writes (what
+  // dqz_logits_write does for them), so the next add / sample needs no scan
+  if (a.run && r.valid) {
+    dS = block_sum_f64(dS, dbuf);  // fixed order: deterministic
+    if (threadIdx.x == 0) {
+      const double before = r.S;
+      r.S += dS;
+      if (s_far || !run_ok(before, r.S, -INFINITY, r.c)) r.valid = 0;
+      *a.run = r;
+    }
   }
   if (threadIdx.x == 0) {
     *a.count = cnt;

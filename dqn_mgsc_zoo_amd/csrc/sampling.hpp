@@ -21,6 +21,10 @@
 namespace dqz {
 
 constexpr int SM_THREADS = 256;
+
+__device__ __forceinline__ double load_fresh(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int SM_CHUNK = 4096;  // logits per block in the reduction / CDF passes
 
 struct MaxSum {
@@ -145,7 +149,8 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
   __shared__ MaxSum sbuf[SM_THREADS / 64];
   const MaxSum acc = combine_parts(part, nparts, sbuf);
   if (threadIdx.x == 0) {
-    const float lse = acc.m == -INFINITY ? -INFINITY : acc.m + logf(acc.s);
+    // the f32 lse every sampler and add uses: c + log(S) of the running state
+    const float lse = acc.m == -INFINITY ? -INFINITY : (float)((double)acc.m + log((double)acc.s));
     if (lse_out) *lse_out = lse;
     float item = -INFINITY;
     if (logits && write_pos >= 0) {
@@ -264,30 +269,80 @@ __global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, d
 // probabilities_from_logits), widened to float64 like numpy's choice.
 __device__ __forceinline__ float prob_f32(float x, float L) { return expf(x - L); }
 
-// Per-block float64 sums of p.  lse is recombined from pass 1's partials by every block (same
-// bits as lse_final_kernel); block 0 publishes it for the choice kernel.
-// p_out (diagnostic, dqz_logits_probs): the f32 p of every slot, or null.
-__global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float* __restrict__ x, int64_t n,
-                                                                    const MaxSum* __restrict__ part, int nparts,
-                                                                    float* __restrict__ lse_out,
-                                                                    double* __restrict__ bsum,
-                                                                    float* __restrict__ p_out) {
-  __shared__ MaxSum sbuf[SM_THREADS / 64];
+// The f32 log-sum-exp of a running state: c + log(S) in float64, rounded once.
+__device__ __forceinline__ float run_lse(const LogitRun& r) {
+  return r.S > 0.0 ? (float)((double)r.c + log(r.S)) : -INFINITY;
+}
+
+// lse of the buffer as the samplers use it: the running state's when it is
+// valid (the host re-seeds it with a scan whenever it cannot vouch for it), or
+// — when a device-side guard invalidated it since (a removal that cancelled
+// most of S) — a full scan by this block: max, then float64 sum of exp(x - max)
+// in one fixed order, so every block of a launch gets the same bits.  Rare.
+__device__ __forceinline__ float sample_lse(const float* __restrict__ x, int64_t n, const LogitRun* run) {
+  __shared__ float s_L;
+  __shared__ float fbuf[SM_THREADS / 64];
   __shared__ double dbuf[SM_THREADS / 64];
-  const MaxSum t = combine_parts(part, nparts, sbuf);
-  const float L = t.m == -INFINITY ? -INFINITY : t.m + logf(t.s);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *lse_out = L;
-  const int64_t base = (int64_t)blockIdx.x * SM_CHUNK;
+  const LogitRun r = *run;
+  if (r.valid) return run_lse(r);
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, x[j]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
+  const float c = m == -INFINITY ? 0.f : m;
+  double sum = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(x[j], c);
+  sum = block_sum_f64(sum, dbuf);
+  if (threadIdx.x == 0) s_L = run_lse(LogitRun{sum, c, 1});
+  __syncthreads();
+  return s_L;
+}
+
+// float64 sum of the f32 p of chunk b (SM_CHUNK logits, lane t holding the
+// float4s t, t + 256, ...), in one fixed order; optionally stores every p.
+__device__ __forceinline__ double chunk_prob_sum(const float* __restrict__ x, int64_t n, int b, float L,
+                                                 float* __restrict__ p_out, double* dbuf) {
+  const int64_t base = (int64_t)b * SM_CHUNK;
   double acc = 0.0;
-  for (int i = threadIdx.x; i < SM_CHUNK; i += SM_THREADS) {
-    const int64_t j = base + i;
-    if (j < n) {
-      const float pf = prob_f32(x[j], L);
-      acc += (double)pf;
-      if (p_out) p_out[j] = pf;
+#pragma unroll
+  for (int q = 0; q < SM_CHUNK / SM_THREADS / 4; ++q) {
+    const int64_t j = base + 4 * (threadIdx.x + SM_THREADS * q);
+    float4 f = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    if (j + 3 < n && (reinterpret_cast<uintptr_t>(x + j) & 15) == 0) {
+      f = *reinterpret_cast<const float4*>(x + j);
+    } else {
+      if (j < n) f.x = x[j];
+      if (j + 1 < n) f.y = x[j + 1];
+      if (j + 2 < n) f.z = x[j + 2];
+      if (j + 3 < n) f.w = x[j + 3];
+    }
+    const float p0 = prob_f32(f.x, L), p1 = prob_f32(f.y, L), p2 = prob_f32(f.z, L), p3 = prob_f32(f.w, L);
+    acc += (double)p0;
+    acc += (double)p1;
+    acc += (double)p2;
+    acc += (double)p3;
+    if (p_out) {
+      if (j < n) p_out[j] = p0;
+      if (j + 1 < n) p_out[j + 1] = p1;
+      if (j + 2 < n) p_out[j + 2] = p2;
+      if (j + 3 < n) p_out[j + 3] = p3;
     }
   }
-  acc = block_sum_f64(acc, dbuf);
+  return block_sum_f64(acc, dbuf);
+}
+
+// Per-block float64 sums of p with the running lse (diagnostic
+// dqz_logits_probs: p_out gets the f32 p of every slot, block 0 the lse).
+__global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float* __restrict__ x, int64_t n,
+                                                                    const LogitRun* run, float* __restrict__ lse_out,
+                                                                    double* __restrict__ bsum,
+                                                                    float* __restrict__ p_out) {
+  __shared__ double dbuf[SM_THREADS / 64];
+  const float L = sample_lse(x, n, run);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *lse_out = L;
+  const double acc = chunk_prob_sum(x, n, blockIdx.x, L, p_out, dbuf);
   if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
 }
 
@@ -317,23 +372,25 @@ __device__ __forceinline__ double block_scan_incl_f64(double v, double* s) {
 // p) / total.
 constexpr int SM_PER_LANE = SM_CHUNK / SM_THREADS;  // 16
 
-__global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float* __restrict__ x, int64_t n,
-                                                                    const float* __restrict__ lse,
-                                                                    const double* __restrict__ bsum, int nblocks,
-                                                                    const double* __restrict__ uniforms,
-                                                                    int64_t* __restrict__ out) {
+// bsum is read with agent-scope (L2-bypassing) loads: in the fused sampler
+// its producers are other workgroups of the same launch.
+__device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, float L,
+                                                       const double* bsum, int nblocks, double u) {
   __shared__ double s_scan[SM_THREADS];
   __shared__ double s_before;
   __shared__ int s_blk;
   __shared__ unsigned long long s_idx;
   const int t = threadIdx.x;
-  const float L = *lse;
-  const double u = uniforms[blockIdx.x];
   // level 1: lane t owns block sums [t seg, (t + 1) seg)
   const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
   const int b0 = min(t * seg, nblocks), b1 = min(b0 + seg, nblocks);
   double mine = 0.0;
-  for (int b = b0; b < b1; ++b) mine += bsum[b];
+  double mb[8];  // this lane's block sums (seg <= 8 up to 8M logits), else re-read
+  for (int b = b0; b < b1; ++b) {
+    const double v = load_fresh(bsum + b);
+    if (b - b0 < 8) mb[b - b0] = v;
+    mine += v;
+  }
   if (t == 0) {
     s_blk = nblocks - 1;
     s_idx = ~0ull;
@@ -343,18 +400,19 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float*
   {
     double run = incl - mine;
     for (int b = b0; b < b1; ++b) {
-      if ((run + bsum[b]) / tot > u) {
+      const double v = b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
+      if ((run + v) / tot > u) {
         atomicMin(&s_blk, b);
         break;
       }
-      run += bsum[b];
+      run += v;
     }
   }
   __syncthreads();
   const int blk = s_blk;
   if (blk >= b0 && blk < b1) {  // the owner of the crossing block publishes the mass before it
     double run = incl - mine;
-    for (int b = b0; b < blk; ++b) run += bsum[b];
+    for (int b = b0; b < blk; ++b) run += b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
     s_before = run;
   }
   // level 2: the chunk's 256 lanes x 16 logits
@@ -379,6 +437,7 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float*
     }
   }
   __syncthreads();
+  __shared__ int64_t s_out;
   if (t == 0) {
     int64_t idx = s_idx == ~0ull ? -1 : (int64_t)s_idx;
     if (idx < 0) {  // rounding at the chunk edge: last live slot of the chunk
@@ -389,16 +448,83 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_choice_kernel(const float*
           break;
         }
     }
-    out[blockIdx.x] = idx;
+    s_out = idx;
+  }
+  __syncthreads();
+  return s_out;
+}
+
+// Learned-logit batch draw in one launch (replay_circular.py:205-217,
+// 540-545: Generator.choice(C, n, p=softmax(logits))).  Blocks [0, nb) are
+// producers: chunk b's float64 sum of p, stored agent-scope, then an arrival
+// on the launch's counter.  Blocks [nb, nb + n) are the n queries: draw q's
+// uniform (the caller's, or Philox (seed, *counter, q) — the stream
+// dqz_uniform_philox produces), wait for all nb arrivals, then the two-level
+// CDF search.  Workgroups are dispatched in index order and producers never
+// wait, so every wait ends; the spin is bounded anyway (the error word gets
+// 1).  The last query to finish resets the counters and advances *counter,
+// so graph replays start clean.
+struct SampleSync {
+  static constexpr int kStride = 64;  // cnt / done / err on their own 256-byte lines
+  int* words;
+};
+
+__global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
+    const float* __restrict__ x, int64_t n, const LogitRun* run, double* bsum, int nblocks, SampleSync sync,
+    uint64_t seed, uint64_t* counter, const double* __restrict__ uniforms, int nq, int32_t* __restrict__ out_slots,
+    int64_t* __restrict__ out_idx) {
+  __shared__ double dbuf[SM_THREADS / 64];
+  int* cnt = sync.words;
+  int* done = sync.words + SampleSync::kStride;
+  int* err = sync.words + 2 * SampleSync::kStride;
+  const float L = sample_lse(x, n, run);
+  const int b = blockIdx.x;
+  if (b < nblocks) {
+    const double acc = chunk_prob_sum(x, n, b, L, nullptr, dbuf);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(bsum + b, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const int q = b - nblocks;
+  double u;
+  uint64_t ctr = 0;
+  if (uniforms) {
+    u = uniforms[q];
+  } else {
+    ctr = *counter;
+    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)q, 0x50F7u),
+                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+    u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+  }
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nblocks) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t idx = softmax_choice_body(x, n, L, bsum, nblocks, u);
+  if (threadIdx.x == 0) {
+    if (out_slots) out_slots[q] = (int32_t)idx;
+    if (out_idx) out_idx[q] = idx;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nq - 1) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!uniforms) *counter = ctr + 1;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // fp64 sum tree (storage[1] = root; node i -> 2i, 2i+1; leaves from `cap`)
-
-__device__ __forceinline__ double load_fresh(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Single workgroup: write n leaves, then recompute their ancestors level by
 // level (duplicate parents write identical values).

@@ -70,8 +70,10 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
       return action
     if self._frame_t % self._learn_period == 0:
       self._learn()
+      self._after_learn()
     if self._frame_t % self._target_network_update_period == 0:
       self._learner.sync_target()
+      self.check_learner_health()
     return action
 
   def reset(self) -> None:
@@ -85,7 +87,8 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
     pos = torch.as_tensor(positions.astype('int32'),
                           device=self._learner.device)
     self._meta.set_online_transition(online_transition)
-    self._meta.update(self._store(), slots, self._replay.logits, pos)
+    dl = self._replay.device_logits  # running log-sum-exp kept current
+    self._meta.update(self._store(), slots, dl.logits, pos, logit_buffer=dl)
 
   def _learn(self) -> None:
     """agent.py:341-360: softmax(logits)-sampled batch, DQN update."""

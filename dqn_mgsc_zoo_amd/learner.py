@@ -334,9 +334,13 @@ class MetaLearner:
     st.reward.copy_(meta[:1])
     st.discount.copy_(meta[1:])
 
-  def update(self, store, slots, logits, positions, stream=None):
+  def update(self, store, slots, logits, positions, stream=None,
+             logit_buffer=None):
     """One meta_update on replay `slots` (device int32 [M]); logits updated
-    in place at `positions` (device int32 [M], distinct)."""
+    in place at `positions` (device int32 [M], distinct).  `logit_buffer`
+    (the replay's device logit buffer, replay_circular._DeviceLogits) keeps
+    its running log-sum-exp current through the write; without it the
+    caller must invalidate that state."""
     m = self.meta_batch_size
     if slots.dtype != torch.int32 or slots.numel() != m:
       raise ValueError('slots must be a device int32 tensor of meta batch size')
@@ -344,6 +348,8 @@ class MetaLearner:
       raise ValueError('positions must be a device int32 tensor [M]')
     if logits.dtype != torch.float32:
       raise ValueError('logits must be float32')
+    if logit_buffer is not None and logits.data_ptr() != logit_buffer.logits.data_ptr():
+      raise ValueError('logit_buffer does not own these logits')
     lrn = self.learner
     _native.check(_native.lib().dqz_meta_update(
         self._h, ctypes.byref(lrn._params_c), store.c_ref(),  # pylint: disable=protected-access
@@ -351,6 +357,7 @@ class MetaLearner:
         _native.ptr(self.online_slot), _native.ptr(logits),
         _native.ptr(positions), _native.ptr(self.adam_mu),
         _native.ptr(self.adam_nu), _native.ptr(self.adam_count),
+        None if logit_buffer is None else logit_buffer.handle,
         _native.stream_handle(stream)))
 
   def fetch_outputs(self, stream=None):

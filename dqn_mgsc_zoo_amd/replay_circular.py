@@ -98,6 +98,29 @@ class _DeviceLogits:
     n.check(n.lib().dqz_logits_put(self._h, n.ptr(self.logits), int(position),
                                    float(value), n.stream_handle()))
 
+  @property
+  def handle(self):
+    """The dqz_logit_buffer handle (for dqz_meta_update's logit_buf)."""
+    return self._h
+
+  def run_state(self):
+    """The running log-sum-exp state (dqz_logits_run_get; synchronises)."""
+    import ctypes  # pylint: disable=g-import-not-at-top
+    n = self._native
+    S, c = ctypes.c_double(), ctypes.c_float()
+    valid, known, adds = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    n.check(n.lib().dqz_logits_run_get(self._h, ctypes.byref(S), ctypes.byref(c),
+                                       ctypes.byref(valid), ctypes.byref(known),
+                                       ctypes.byref(adds), n.stream_handle()))
+    return {'S': S.value, 'c': c.value, 'valid': valid.value,
+            'known': known.value, 'adds': adds.value}
+
+  def set_run_state(self, st):
+    n = self._native
+    n.check(n.lib().dqz_logits_run_set(self._h, float(st['S']), float(st['c']),
+                                       int(st['valid']), int(st['known']),
+                                       int(st['adds']), n.stream_handle()))
+
   def invalidate(self):
     """The logits tensor was (or may be) written outside the library."""
     self._native.check(self._native.lib().dqz_logits_invalidate(self._h))
@@ -125,6 +148,18 @@ class _DeviceLogits:
                                          nat.ptr(p), nat.ptr(lse),
                                          nat.stream_handle()))
     return p, lse
+
+  def sample_slots_philox(self, seed, counter, out_slots, out_idx=None):
+    """Learner batch in one launch (dqz_logits_sample_slots): Philox
+    uniforms (seed, device int64 counter, advanced on device), softmax-CDF
+    choice, int32 absolute slots into `out_slots` (and int64 into `out_idx`
+    if given).  Draws what dqz_uniform_philox + sample_abs would."""
+    nat = self._native
+    nat.check(nat.lib().dqz_logits_sample_slots(
+        self._h, nat.ptr(self.logits), int(seed) & (2**64 - 1),
+        nat.ptr(counter), None, int(out_slots.numel()), nat.ptr(out_slots),
+        nat.ptr(out_idx), nat.stream_handle()))
+    return out_slots
 
   def sample_abs(self, uniforms):
     """Absolute slots for host uniforms (device int64 tensor)."""
@@ -228,18 +263,25 @@ class CircularLogitBuffer:
                         'requested sample size was %d.' % (self._size, size))
     return self._rng_state.choice(self._size, size=size, replace=replace)
 
+  @property
+  def device_logits(self):
+    """The device logit buffer (logits + running log-sum-exp), for writers
+    that keep the running state current (the meta-update)."""
+    return self._dev
+
   def get_state(self) -> Mapping[str, Any]:
-    # the saver re-scans at its next add, as a restored copy will: both
-    # continue from the same bits
-    self._dev.invalidate()
+    # The running log-sum-exp travels with the logits: saving does not
+    # disturb the saver, and a restored copy continues with the same bits.
     return {'capacity': self._capacity,
             'logits': self._dev.logits.cpu().numpy(), 'size': self._size,
             'left_head': self._left_head, 'right_head': self._right_head,
-            'rng_state': self._rng_state}
+            'rng_state': self._rng_state, 'logit_run': self._dev.run_state()}
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._capacity = state['capacity']
     self._dev.load(state['logits'])
+    if 'logit_run' in state:
+      self._dev.set_run_state(state['logit_run'])
     self._size = state['size']
     self._left_head = state['left_head']
     self._right_head = state['right_head']
@@ -421,6 +463,10 @@ class MGSCFiFoTransitionReplay:
     return self._distribution.logits
 
   @property
+  def device_logits(self):
+    return self._distribution.device_logits
+
+  @property
   def size(self) -> int:
     return self._ring.size
 
@@ -516,14 +562,20 @@ class MGSCReservoirDistribution:
                         'size %d.' % (size, self._size))
     return self._rng_state.choice(self._size, size=size, replace=replace)
 
+  @property
+  def device_logits(self):
+    return self._dev
+
   def get_state(self) -> Mapping[str, Any]:
-    self._dev.invalidate()  # saver and restored copy both re-scan at their next add
     return {'capacity': self._capacity, 'logits': self._dev.logits.cpu().numpy(),
-            'size': self._size, 'rng_state': self._rng_state}
+            'size': self._size, 'rng_state': self._rng_state,
+            'logit_run': self._dev.run_state()}
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._capacity = state['capacity']
     self._dev.load(state['logits'])
+    if 'logit_run' in state:
+      self._dev.set_run_state(state['logit_run'])
     self._size = state['size']
     self._rng_state = state['rng_state']
 
@@ -585,6 +637,10 @@ class MGSCReservoirTransitionReplay:
   @property
   def logits(self):
     return self._distribution.logits
+
+  @property
+  def device_logits(self):
+    return self._distribution.device_logits
 
   @property
   def size(self) -> int:

@@ -3,15 +3,26 @@
 The learner step is sequentially dependent and the reference never shares
 gradients (its SLURM arrays run one seed per job), so multi-GPU here is
 replicas only: each rank owns its own replay, learner and RNG streams.  The
-only collectives are a MAX of the timed-region wall clock and an all-gather
-of a small float64 statistics vector, both after the timed region — over
-RCCL ("nccl") on the GPU box, gloo in the CPU tests.
+collectives are a small float64 statistics all-gather every
+`--stats-every` steps inside bench.py's timed loop (enqueued, consumed after
+it), and a MAX of the timed-region wall clock plus a final statistics gather
+after it — over RCCL ("nccl") on the GPU box, gloo in the CPU tests.  The
+process group is initialised at every world size, 1 included, so a 1-GPU
+run goes through the same RCCL calls as an 8-GPU one (run_dqn_normal.sh:5,47
+runs one seed per job; here the seeds report through one group).
 """
 
 import os
+import socket
 
 import numpy as np
 import torch
+
+
+def _free_port():
+  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+    s.bind(('127.0.0.1', 0))
+    return s.getsockname()[1]
 
 
 class Replicas:
@@ -22,11 +33,16 @@ class Replicas:
     self.rank = int(os.environ.get('RANK', '0'))
     self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     self.dist = None
-    if self.world > 1:
-      import torch.distributed as dist  # pylint: disable=g-import-not-at-top
-      if not dist.is_initialized():
-        dist.init_process_group(backend or 'nccl')
-      self.dist = dist
+    import torch.distributed as dist  # pylint: disable=g-import-not-at-top
+    if not dist.is_initialized():
+      if self.world == 1 and 'MASTER_ADDR' not in os.environ:
+        # a lone rank still forms a group (loopback rendezvous)
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(_free_port())
+      dist.init_process_group(backend or 'nccl', rank=self.rank,
+                              world_size=self.world)
+    self.dist = dist
+    self.backend = dist.get_backend()
 
   def seed(self, base=0):
     """Per-rank seed: rank r runs seed base + r."""

@@ -276,6 +276,17 @@ int dqz_logits_write(dqz_logit_buffer* buf, float* logits, const int64_t* positi
 /* One write logits[position] = value (by value: popleft's -inf), keeping the running sum. */
 int dqz_logits_put(dqz_logit_buffer* buf, float* logits, int64_t position, float value, void* stream);
 
+/* Running log-sum-exp state of a logit buffer, for checkpoints
+ * (parts.py:517-561): S = float64 sum of exp(x - c) over the buffer, the
+ * shift c, the device-side valid flag, and the host bookkeeping (known: every
+ * write since the last scan went through the library; adds: running adds
+ * since that scan).  get synchronises `stream`; set restores all five, so a
+ * restored buffer continues with the saver's bits (no re-scan on either
+ * side). */
+int dqz_logits_run_get(dqz_logit_buffer* buf, double* S, float* c, int* valid, int* known, int* adds,
+                       void* stream);
+int dqz_logits_run_set(dqz_logit_buffer* buf, double S, float c, int valid, int known, int adds, void* stream);
+
 /* The logits were written outside the library (e.g. the meta-update's Adam
  * step, a state restore): the next dqz_logits_add re-scans the buffer. */
 int dqz_logits_invalidate(dqz_logit_buffer* buf);
@@ -287,6 +298,17 @@ int dqz_logits_invalidate(dqz_logit_buffer* buf);
  * in [0,1) (host Generator draws for parity, or dqz_uniform_philox). */
 int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
                       int64_t* out_idx, void* stream);
+
+/* Learner-batch draw in one launch: n uniforms — the caller's `uniforms`
+ * (device f64, NULL for Philox) or Philox4x32 (seed, *counter_dev, q), the
+ * stream dqz_uniform_philox produces, *counter_dev then advanced on device —
+ * and the softmax-CDF choice of dqz_logits_sample, written as int32 slots
+ * (out_slots, for dqz_learner_step) and/or int64 (out_idx); either may be
+ * NULL.  Replaces Generator.choice(C, n, p=softmax(logits)) +
+ * the batch's slot lookup (replay_circular.py:205-217, 540-545) without the
+ * uniform launch or an int64 -> int32 copy. */
+int dqz_logits_sample_slots(dqz_logit_buffer* buf, const float* logits, uint64_t seed, uint64_t* counter_dev,
+                            const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, void* stream);
 
 /* Diagnostic: the f32 p = exp(x - lse) of every slot exactly as
  * dqz_logits_sample forms it (p_out: device f32 [capacity]) and lse
@@ -383,11 +405,15 @@ int dqz_meta_destroy(dqz_meta* meta);
  * slots in `store`.  online_store/online_slot: the newest transition (device
  * int32 [1]).  logits: the replay's device logit buffer; pos: device int32
  * [M] absolute positions (distinct).  adam_mu/adam_nu: device f32 [M];
- * adam_count: device int32 [1] (ScaleByAdamState). */
+ * adam_count: device int32 [1] (ScaleByAdamState).  logit_buf (may be
+ * NULL): the dqz_logit_buffer owning `logits`; its running log-sum-exp is
+ * then updated for the M writes (positions distinct), so the buffer's next
+ * add / sample needs no re-scan; with NULL the caller must call
+ * dqz_logits_invalidate. */
 int dqz_meta_update(dqz_meta* meta, const dqz_params* params, const dqz_store* store,
                     const int32_t* slots, const dqz_store* online_store, const int32_t* online_slot,
                     float* logits, const int32_t* pos, float* adam_mu, float* adam_nu,
-                    int32_t* adam_count, void* stream);
+                    int32_t* adam_count, dqz_logit_buffer* logit_buf, void* stream);
 
 /* Device copies of the last meta-update's intermediates (any may be NULL):
  * probs [M], dlogits [M] (d L / d logits), td [M] meta-batch TD errors,

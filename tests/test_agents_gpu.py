@@ -320,3 +320,20 @@ def test_mgsc_reservoir_agent_run_loop(device):
   # the second-order meta step (no stop_gradient on theta'', reservoir
   # agent.py:191) through the agent path, against the fp64 oracle
   _check_meta_step_against_oracle(agent, replay, stop_gradient=False)
+
+
+def test_agent_loop_reports_a_handoff_timeout(device):
+  """the agent reads the learner's health word at every target
+  sync (and every HEALTH_CHECK_PERIOD learn steps): a forced hand-off
+  timeout inside run_loop surfaces as a RuntimeError at the next check, the
+  words are reset by that read, and the loop then runs on cleanly."""
+  agent, _ = _make('dqn', seed=5)
+  steps = _run(agent, 60)  # past min replay: learning has started
+  assert steps
+  agent.learner.debug_stall(3, spin_max=4096)
+  with pytest.raises(RuntimeError, match='hand-off wait timed out'):
+    _run(agent, 200, seed=2)
+  agent.learner.debug_stall(-1)
+  _run(agent, 100, seed=3)
+  assert agent.check_learner_health() == 0
+  assert torch.isfinite(agent.learner.online).all()

@@ -90,6 +90,21 @@ def test_gpus2_spawns_two_ranks_gloo():
   assert out['per_rank_target_syncs'] == [2, 2]
   assert out['per_rank_stats_gathers'] == [3, 3]
   assert out['value'] > 0
+  # the gathered statistics are read back: every rank's step count at the
+  # last in-loop gather (the chunk that crossed step 24 ends at 25)
+  assert out['rccl']['backend'] == 'gloo' and out['rccl']['world'] == 2
+  assert out['rccl']['last_in_loop_gather']['steps_done'] == [25, 25]
+  assert len(out['rccl']['last_in_loop_gather']['value']) == 2
+
+
+def test_gpus1_forms_a_process_group():
+  """World 1 goes through the same collectives (a group of one)."""
+  p = _run_bench(['--gpus', '1', '--steps', '10', '--warmup', '0',
+                  '--stats-every', '5', '--selftest-cpu'])
+  assert p.returncode == 0, p.stderr[-2000:]
+  out = json.loads([l for l in p.stdout.splitlines() if l.startswith('{')][0])
+  assert out['rccl']['world'] == 1
+  assert out['rccl']['last_in_loop_gather']['steps_done'] == [10]
 
 
 def test_world_mismatch_fails():

@@ -1,0 +1,307 @@
+"""GPU parity at the BASELINE.json workloads (capacity 1,000,000, B = 32).
+
+The other GPU tests use small stores so the fp64 oracle can see everything;
+these run the device path over the full-size structures the bench uses and
+check the one step they take against the oracle on the transitions that step
+actually read:
+
+  config 2  synthetic 1M-transition episodic replay (synthetic.fill_episodic),
+            the fused Philox uniform draw + DQN step (dqz_learner_step_uniform)
+  config 3  MGSC reservoir: 1M N(0,1) f32 logits, softmax-CDF sample of the
+            learner batch (dqz_logits_sample, Generator uniforms), DQN step,
+            then one M = 100 second-order meta-update (the reservoir agent's
+            meta_loss_fn, no stop_gradient) writing the Adam-updated logits
+            back into the 1M-logit buffer
+  config 4  PER: 2^20-leaf fp64 sum tree over 1M alpha-exponentiated
+            priorities, the device sampler fed the reference's RandomState
+            draws (dqz_per_sample), the double-Q step with IS weights, and the
+            |td|^alpha write-back (dqz_per_write_back)
+
+Index work (slots, sampled ids, probabilities, sum-tree nodes) is compared
+bit for bit; Q / TD within 1e-4 and parameters within 2e-6 (the tolerances of
+tests/test_learner_gpu.py, BASELINE north_star 1e-4 fp32).  Each batch is
+chosen kink-free (tests/helpers.kink_free_slots) by advancing the sampler's
+own stream deterministically, not by filtering the device's output.
+Reference: replay.py:119-125,200-206,680-716; replay_circular.py:205-217,
+526-545; dqn/agent.py:85-119; prioritized/agent.py:86-127,201-206;
+dqn_mgsc_batched/agent.py:104-220.
+"""
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner_ref
+from oracle import replay_ref
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+CAP = 1_000_000
+B = 32
+A = 6
+Q_ATOL = 1e-4
+P_ATOL = 2e-6
+MARGIN = 1e-6
+
+
+@pytest.fixture(scope='module')
+def store(device):
+  from dqn_mgsc_zoo_amd import synthetic
+  st = synthetic.fill_episodic(CAP, A, seed=0, device=device)
+  torch.cuda.synchronize()
+  return st
+
+
+def _host_batch(st, slots):
+  """Host copies of the transitions at `slots`: (s_tm1, a, r, d, s_t).
+
+  Frames are copied back row by row through the fidx table (the checker's
+  own gather, independent of dqz_gather_stacks)."""
+  s = torch.as_tensor(np.asarray(slots, np.int64), device=st.fidx.device)
+  fidx = st.fidx[s].cpu().numpy()
+  rows = np.unique(fidx[fidx >= 0])
+  frames = st.frames[torch.as_tensor(rows, device=st.frames.device)].cpu().numpy()
+  where = {int(f): i for i, f in enumerate(rows)}
+
+  def stacks(which):
+    out = np.zeros((len(slots), 84, 84, 4), np.uint8)
+    for b in range(len(slots)):
+      for c in range(4):
+        f = int(fidx[b, which * 4 + c])
+        if f >= 0:
+          out[b, :, :, c] = frames[where[f]].reshape(84, 84)
+    return out
+
+  return (stacks(0), st.action[s].cpu().numpy(), st.reward[s].cpu().numpy(),
+          st.discount[s].cpu().numpy(), stacks(1))
+
+
+def _compare_tree(got, want, atol, rtol=0.0, what=''):
+  for m in want:
+    for n in want[m]:
+      np.testing.assert_allclose(got[m][n], want[m][n], atol=atol, rtol=rtol,
+                                 err_msg='%s %s/%s' % (what, m, n))
+
+
+def _check_step(lrn, ref, target):
+  q, td, loss = lrn.fetch_outputs()
+  torch.cuda.synchronize()
+  np.testing.assert_allclose(q.cpu().numpy(), ref['q_tm1'], atol=Q_ATOL)
+  np.testing.assert_allclose(td.cpu().numpy(), ref['td'], atol=Q_ATOL)
+  np.testing.assert_allclose(loss.cpu().numpy()[0], ref['loss'], rtol=1e-4,
+                             atol=1e-7)
+  _compare_tree(lrn.params_tree('online'), ref['params'], P_ATOL, what='params')
+  _compare_tree(lrn.params_tree('mu'), ref['mu'], 1e-9, 1e-3, what='mu')
+  _compare_tree(lrn.params_tree('nu'), ref['nu'], 1e-12, 2e-3, what='nu')
+  _compare_tree(lrn.params_tree('target'), target, 0.0, what='target')
+  assert lrn.sync_status() == 0
+
+
+def test_config2_uniform_fifo_1m_step(device, store):
+  """Config 2: the bench's own step (Philox draw fused into conv1) on the
+  1M-transition synthetic replay, checked against the oracle on the slots it
+  drew; the device gather of those slots equals the host restack."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  net = networks.dqn_atari_network(A)
+  online = net.init(1)
+  target = helpers.perturbed_tree(online, 2)
+  lrn = learner_lib.Learner(net, B, algo='dqn', device=device)
+  lrn.set_params(online, target)
+  seed = 1234
+  counter = torch.zeros((1,), dtype=torch.int64, device=device)
+  preview = torch.empty((B,), dtype=torch.int32, device=device)
+  for _ in range(32):  # advance the Philox stream to a kink-free batch
+    c = counter.clone()
+    learner_lib.sample_uniform(0, CAP, CAP, B, seed, c, preview)
+    slots = preview.cpu().numpy()
+    batch = _host_batch(store, slots)
+    if learner_ref.relu_margin(online, batch[0]) >= MARGIN:
+      break
+    counter.copy_(c)
+  else:
+    raise AssertionError('no kink-free batch')
+  assert slots.min() >= 0 and slots.max() < CAP
+  out = torch.empty((B,), dtype=torch.int32, device=device)
+  lrn.step_uniform(store, 0, CAP, CAP, seed, counter, out)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(out.cpu().numpy(), slots)
+  for which, want in ((0, batch[0]), (1, batch[4])):
+    got = store.gather_stacks(out, which).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t)
+  _check_step(lrn, ref, target)
+
+
+def _f64(tree):
+  return {m: {n: np.asarray(v, np.float64) for n, v in t.items()}
+          for m, t in tree.items()}
+
+
+def test_config3_mgsc_reservoir_1m_sample_step_and_meta(device, store):
+  """Config 3: 1M N(0,1) logits.  The learner batch is the softmax-CDF
+  choice for Generator uniforms (bit-exact given the device's p; at most one
+  of 32 draws may differ from numpy's own f32 exp, the documented last-ulp
+  gap); the DQN step on it matches the oracle; one M = 100 second-order
+  meta-update on a without-replacement meta batch matches the oracle and
+  writes only its 100 logits."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  rng = np.random.default_rng(3)
+  logits = rng.standard_normal(CAP).astype(np.float32)
+  dev = rc._DeviceLogits(CAP, device, max_queries=512)  # pylint: disable=protected-access
+  dev.load(logits)
+  net = networks.dqn_atari_network(A)
+  online = net.init(4)
+  target = helpers.perturbed_tree(online, 5)
+  lrn = learner_lib.Learner(net, B, algo='dqn', device=device)
+  lrn.set_params(online, target)
+  gen = np.random.default_rng(6)  # the replay's PCG64 Generator
+  for _ in range(32):
+    u = gen.random(B)
+    idx = dev.sample_abs(u).cpu().numpy()
+    batch = _host_batch(store, idx)
+    if learner_ref.relu_margin(online, batch[0]) >= MARGIN:
+      break
+  else:
+    raise AssertionError('no kink-free batch')
+  p_dev = dev.probs()[0].cpu().numpy()
+  cdf = np.cumsum(p_dev.astype(np.float64))
+  cdf /= cdf[-1]
+  np.testing.assert_array_equal(idx, np.searchsorted(cdf, u, side='right'))
+  assert (idx != replay_ref.softmax_choice(logits, u)).sum() <= 1
+  slots = torch.as_tensor(idx.astype(np.int32), device=device)
+  lrn.step(store, slots)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t)
+  _check_step(lrn, ref, target)
+
+  # one meta-update (reservoir agent: second order) over the same logits
+  m = 100
+  theta, mu, nu = (lrn.params_tree(w) for w in ('online', 'mu', 'nu'))
+  meta = learner_lib.MetaLearner(lrn, m, learner_lib.adam(2.5e-4),
+                                 second_order=True)
+  pos = np.sort(rng.choice(CAP, m, replace=False)).astype(np.int32)
+  mb = dict(zip(('s_tm1', 'a_tm1', 'r_t', 'discount_t', 's_t'),
+                _host_batch(store, pos)))
+  ot = replay_lib.Transition(rng.integers(0, 256, (84, 84, 4), dtype=np.uint8),
+                             2, 1.0, 0.99,
+                             rng.integers(0, 256, (84, 84, 4), dtype=np.uint8))
+  meta.set_online_transition(ot)
+  before = dev.logits.clone()
+  pos_d = torch.as_tensor(pos, device=device)
+  meta.update(store, pos_d, dev.logits, pos_d, logit_buffer=dev)
+  probs, dlogits, td, loss = [t.cpu().numpy() for t in meta.fetch_outputs()]
+  want = learner_ref.meta_update(
+      _f64(theta), _f64(lrn.params_tree('target')), _f64(mu), _f64(nu), mb,
+      logits[pos], dict(s_tm1=ot.s_tm1, a_tm1=2, r_t=1.0, discount_t=0.99,
+                        s_t=ot.s_t),
+      np.zeros(m), np.zeros(m), 0, stop_gradient=False)
+  np.testing.assert_allclose(probs, want['probs'], rtol=1e-5)
+  np.testing.assert_allclose(td, want['td'], atol=Q_ATOL)
+  np.testing.assert_allclose(loss[0], want['loss'], rtol=2e-5)
+  scale = np.abs(want['dlogits']).max()
+  np.testing.assert_allclose(dlogits, want['dlogits'], atol=2e-5 * scale)
+  after = dev.logits.cpu().numpy()
+  np.testing.assert_allclose(after[pos], want['new_logits'], atol=1e-6)
+  keep = np.ones(CAP, bool)
+  keep[pos] = False
+  np.testing.assert_array_equal(after[keep], before.cpu().numpy()[keep])
+  # the buffer's running log-sum-exp followed the meta-update's 100 writes
+  run = dev.run_state()
+  assert run['valid'] == 1 and run['known'] == 1
+  a64 = after.astype(np.float64)
+  want_lse = a64.max() + np.log(np.exp(a64 - a64.max()).sum())
+  assert abs(run['c'] + np.log(run['S']) - want_lse) < 1e-9
+
+
+def test_config4_per_1m_sample_step_write_back(device, store):
+  """Config 4: PER over 1M priorities (2^20 leaves).  Device sampler fed the
+  reference's RandomState draws returns the host distribution's ids and fp64
+  probabilities bit for bit; the double-Q step with those IS weights matches
+  the oracle; the |td|^alpha write-back equals the host SumTree.set."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  alpha, usp, beta = 0.6, 1e-3, 0.4
+  host = replay_lib.PrioritizedDistribution(
+      alpha, usp, np.random.RandomState(0), min_capacity=CAP, max_capacity=CAP)
+  ids = np.arange(CAP)
+  host._assign_indices(ids)  # pylint: disable=protected-access
+  rng = np.random.default_rng(7)
+  index = host.index_of(ids)
+  leaves = np.zeros(CAP)
+  leaves[index] = replay_lib._power(rng.uniform(0.01, 2.0, CAP), alpha)  # pylint: disable=protected-access
+  leaves[index[rng.integers(0, CAP, 2000)]] = 0.0  # some zero priorities
+  host.sum_tree.set_all(leaves)
+  assert host.sum_tree.capacity == 1 << 20
+  dist = copy.deepcopy(host)
+  dist.to_device(device)
+  tree = dist.sum_tree
+  tree.index_to_slot[torch.as_tensor(index, device=device)] = torch.as_tensor(
+      ids.astype(np.int32), device=device)
+  np.testing.assert_array_equal(tree.storage[1:], host.sum_tree.storage[1:])
+
+  net = networks.double_dqn_atari_network(A)
+  online = net.init(8)
+  target = helpers.perturbed_tree(online, 9)
+  lrn = learner_lib.Learner(net, B, algo='per', device=device)
+  lrn.set_params(online, target)
+  for seed in range(32):
+    host._random_state = np.random.RandomState(seed)  # pylint: disable=protected-access
+    want_ids, want_probs = host.sample(B)
+    batch = _host_batch(store, want_ids)
+    if learner_ref.relu_margin(online, batch[0]) >= MARGIN:
+      break
+  else:
+    raise AssertionError('no kink-free batch')
+  dist._random_state = np.random.RandomState(seed)  # pylint: disable=protected-access
+  uniform_idx, u = dist.draw(B)
+  idx = torch.empty((B,), dtype=torch.int32, device=device)
+  slots = torch.empty((B,), dtype=torch.int32, device=device)
+  w = torch.empty((B,), dtype=torch.float32, device=device)
+  probs = torch.empty((B,), dtype=torch.float64, device=device)
+  _native.check(_native.lib().dqz_per_sample(
+      _native.ptr(tree.tree), tree.capacity, 0, CAP, CAP, B, usp, beta, 1, 0,
+      None, _native.ptr(torch.from_numpy(uniform_idx).to(device)),
+      _native.ptr(torch.from_numpy(u).to(device)), _native.ptr(tree.index_to_slot),
+      _native.ptr(idx), _native.ptr(slots), _native.ptr(w), _native.ptr(probs),
+      _native.stream_handle()))
+  torch.cuda.synchronize()
+  got_idx = idx.cpu().numpy()
+  assert dist.index_to_id(got_idx).tolist() == want_ids.tolist()
+  assert slots.cpu().numpy().tolist() == want_ids.tolist()
+  assert probs.cpu().numpy().tolist() == want_probs.tolist()  # fp64, bit-exact
+  want_w = replay_lib.importance_sampling_weights(want_probs, 1.0 / CAP, beta, True)
+  np.testing.assert_allclose(w.cpu().numpy(), want_w.astype(np.float32), rtol=2e-7)
+
+  lrn.step(store, slots, w)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t,
+                                 algo='per', weights=w.cpu().numpy())
+  _check_step(lrn, ref, target)
+
+  max_seen = torch.ones((1,), dtype=torch.float64, device=device)
+  _native.check(_native.lib().dqz_per_write_back(
+      lrn._h, _native.ptr(tree.tree), tree.capacity, _native.ptr(idx), alpha,  # pylint: disable=protected-access
+      _native.ptr(max_seen), _native.stream_handle()))
+  _, td, _ = lrn.fetch_outputs()
+  torch.cuda.synchronize()
+  p = np.abs(td.cpu().numpy().astype(np.float64))
+  last = {}
+  for i, v in zip(got_idx.tolist(), p.tolist()):
+    last[i] = v  # a tree index drawn twice keeps its last value
+  host.sum_tree.set(list(last), replay_lib._power(np.array(list(last.values())), alpha))  # pylint: disable=protected-access
+  np.testing.assert_allclose(tree.storage[1:], host.sum_tree.storage[1:],
+                             rtol=1e-15, atol=0)
+  assert max_seen.item() == max(1.0, p.max())

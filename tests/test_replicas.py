@@ -43,9 +43,16 @@ def test_replicas_gloo_world2():
 
 
 def test_replicas_single_process():
+  """World 1 still forms a process group (bench.py's 1-GPU run goes
+  through the same collectives as an N-GPU one)."""
   from dqn_mgsc_zoo_amd import replicas  # pylint: disable=g-import-not-at-top
-  for k in ('WORLD_SIZE', 'RANK'):
+  for k in ('WORLD_SIZE', 'RANK', 'MASTER_ADDR', 'MASTER_PORT'):
     os.environ.pop(k, None)
-  r = replicas.Replicas()
-  assert r.world == 1 and r.max_over_ranks(3.5) == 3.5
-  assert r.gather_stats([1.0, 2.0]).shape == (1, 2)
+  r = replicas.Replicas(backend='gloo')
+  try:
+    assert r.dist.is_initialized() and r.dist.get_world_size() == 1
+    assert r.backend == 'gloo'
+    assert r.world == 1 and r.max_over_ranks(3.5) == 3.5
+    np.testing.assert_array_equal(r.gather_stats([1.0, 2.0]), [[1.0, 2.0]])
+  finally:
+    r.close()

@@ -490,3 +490,60 @@ def test_running_logsumexp_matches_full_recompute(device, reservoir):
       np.testing.assert_allclose(got[live], ref[live], rtol=0, atol=1e-5)
       ref[live] = got[live]  # re-anchor so errors do not compound across checks
   assert worst < 1e-5
+
+
+def test_fused_logit_sampler_equals_philox_then_choice(device):
+  """dqz_logits_sample_slots (one launch: Philox uniforms + block sums + CDF
+  search behind an in-launch hand-off) draws exactly what
+  dqz_uniform_philox + dqz_logits_sample draw, as int32 slots, advances the
+  counter once per call, and stays exact under hipGraph replay (the launch
+  resets its own hand-off words)."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap, n = 1_000_000, 32
+  rng = np.random.default_rng(12)
+  logits = rng.standard_normal(cap).astype(np.float32)
+  logits[rng.integers(0, cap, 500)] = -np.inf
+  dev = rc._DeviceLogits(cap, max_queries=n)  # pylint: disable=protected-access
+  dev.load(logits)
+  lib = _native.lib()
+  c_fused = torch.zeros((1,), dtype=torch.int64, device=device)
+  c_ref = torch.zeros((1,), dtype=torch.int64, device=device)
+  slots = torch.empty((n,), dtype=torch.int32, device=device)
+  idx = torch.empty((n,), dtype=torch.int64, device=device)
+  uni = torch.empty((n,), dtype=torch.float64, device=device)
+  seed = 99
+
+  def ref_draw():
+    _native.check(lib.dqz_uniform_philox(seed, _native.ptr(c_ref), n, _native.ptr(uni),
+                                         _native.stream_handle()))
+    return dev.sample_abs(uni.cpu().numpy()).clone()
+
+  for _ in range(4):
+    dev.sample_slots_philox(seed, c_fused, slots, idx)
+    want = ref_draw()
+    torch.cuda.synchronize()
+    assert torch.equal(idx, want)
+    assert torch.equal(slots.long(), want)
+    assert int(c_fused.item()) == int(c_ref.item())
+  # the choice is numpy's given the device's p
+  p = dev.probs()[0].cpu().numpy()
+  np.testing.assert_array_equal(idx.cpu().numpy(), _choice_from_p(p, uni.cpu().numpy()))
+  # graph replay: 5 captured draws, replayed twice
+  side = torch.cuda.Stream(device)
+  side.wait_stream(torch.cuda.current_stream(device))
+  with torch.cuda.stream(side):
+    dev.sample_slots_philox(seed, c_fused, slots, idx)
+  torch.cuda.current_stream(device).wait_stream(side)
+  ref_draw()
+  g = torch.cuda.CUDAGraph()
+  outs = [torch.empty((n,), dtype=torch.int64, device=device) for _ in range(5)]
+  with torch.cuda.graph(g):
+    for o in outs:
+      dev.sample_slots_philox(seed, c_fused, slots, o)
+  for _ in range(2):
+    g.replay()
+    torch.cuda.synchronize()
+    for o in outs:
+      assert torch.equal(o, ref_draw())
+  assert int(c_fused.item()) == int(c_ref.item())
