@@ -153,7 +153,15 @@ class DeviceDqnAgent(parts.Agent):
 
   @property
   def online_params(self):
-    """Current online parameters (flat device tensor, dqz layout)."""
+    """Current online parameters as the reference returns them
+    (dqn/agent.py:192-194): the Haiku tree {module: {'w', 'b'}}, each leaf a
+    device view of the learner's live buffer (no copy).  The runners hand it
+    to the eval actor (dqn/run_atari.py:264)."""
+    return self._network.device_tree(self._learner.online)
+
+  @property
+  def online_params_flat(self):
+    """The same parameters as one flat device tensor (dqz layout)."""
     return self._learner.online
 
   @property

@@ -188,10 +188,19 @@ class Learner:
     return out
 
   def _params_tensor(self, params):
+    """Flat device parameters from None (online), a flat tensor, a device
+    tree of views (agent.online_params: no copy) or a host tree."""
     if params is None:
       return self.online
     if isinstance(params, torch.Tensor):
       return params
+    leaf = next(iter(next(iter(params.values())).values()))
+    if isinstance(leaf, torch.Tensor):
+      flat = self.network.flat_of_device_tree(params)
+      if flat is not None:
+        return flat
+      params = {m: {n: v.detach().cpu().numpy() for n, v in d.items()}
+                for m, d in params.items()}
     return torch.from_numpy(self.network.flatten(params)).to(self.device)
 
   def q_values_host(self, observation, params=None):

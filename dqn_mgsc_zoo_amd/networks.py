@@ -111,6 +111,38 @@ class NetworkSpec(typing.NamedTuple):
           flat[off:off + size].reshape(shape).astype(np.float32).copy())
     return tree
 
+  def device_tree(self, flat):
+    """Flat device tensor -> Haiku-named tree of device views (no copies):
+    what the reference's `online_params` is (dqn/agent.py:192-194), with
+    every leaf aliasing `flat` so the actor reads the learner's live
+    parameters."""
+    offsets, sizes, total = self.layout()
+    if flat.dim() != 1 or flat.numel() != total:
+      raise ValueError('flat parameter tensor must have %d elements' % total)
+    tree = collections.OrderedDict()
+    for (mod, name), shape, off, size in zip(
+        self.leaf_paths(), self.leaf_shapes(), offsets, sizes):
+      tree.setdefault(mod, collections.OrderedDict())[name] = (
+          flat[off:off + size].view(shape))
+    return tree
+
+  def flat_of_device_tree(self, tree):
+    """The flat tensor a device_tree() aliases, or None if `tree` is not one
+    (then the caller flattens it)."""
+    offsets, _, total = self.layout()
+    paths = self.leaf_paths()
+    first = tree[paths[0][0]][paths[0][1]]
+    base = getattr(first, '_base', None)
+    if base is None or base.dim() != 1 or base.numel() != total:
+      return None
+    esz = base.element_size()
+    for (mod, name), off in zip(paths, offsets):
+      leaf = tree[mod][name]
+      if getattr(leaf, '_base', None) is not base or (
+          leaf.data_ptr() != base.data_ptr() + off * esz):
+        return None
+    return base
+
   @property
   def num_params(self):
     return int(sum(np.prod(s) for s in self.leaf_shapes()))

@@ -756,6 +756,7 @@ class PrioritizedDistribution:
     self._inactive_indices = list(range(min_capacity))
     self._active_indices = []
     self._active_indices_location = {}
+    self._positive_written = False
 
   @property
   def sum_tree(self) -> SumTree:
@@ -779,17 +780,37 @@ class PrioritizedDistribution:
       self._sum_tree = _DeviceSumTree(self._sum_tree, device)
 
   def draw(self, size: int):
-    """The three random streams of sample(), in the reference's order
+    """The random streams of sample(), in the reference's order
     (replay.py:684-697): tree indices of the uniform picks, target
-    fractions, usp-mix uniforms.  The target fractions are drawn whatever
-    the root (the reference skips them only while every priority is 0)."""
+    fractions, usp-mix uniforms -> (uniform_idx, [targets, mix]).  The
+    reference skips the target draw while the tree's root is 0; the host
+    knows that without reading the device tree as long as no positive
+    priority has been written (`_positive_written`), and then draws the mix
+    stream only (targets 0: with root 0 every draw is its uniform pick).
+    Once a positive priority was written the root is taken as positive: a
+    tree whose positive leaves were all removed or written back as 0 again
+    would draw the target stream where the reference does not (stated in
+    INTEGRATION.md)."""
     if self.size == 0:
       raise RuntimeError('No IDs to sample.')
     rs = self._random_state
     uniform_idx = np.array([self._active_indices[j]
                             for j in rs.randint(self.size, size=size)], np.int32)
-    u = np.concatenate([rs.uniform(size=size), rs.uniform(size=size)])
+    if self.on_device:
+      root_zero = not self._positive_written
+    else:
+      root_zero = self._sum_tree.root() == 0.0
+    if root_zero:
+      u = np.concatenate([np.zeros(size), rs.uniform(size=size)])
+    else:
+      u = np.concatenate([rs.uniform(size=size), rs.uniform(size=size)])
     return uniform_idx, u
+
+  def note_priorities(self, priorities) -> None:
+    """Host bookkeeping of draw(): a positive priority (or a device value,
+    the agent's running max_seen_priority >= 1) makes the root positive."""
+    if priorities is None or np.any(np.asarray(priorities) > 0.0):
+      self._positive_written = True
 
   def index_to_id(self, indices) -> np.ndarray:
     return np.array([self._index_to_id[int(i)] for i in indices], dtype=np.int64)
@@ -842,6 +863,7 @@ class PrioritizedDistribution:
     return indices
 
   def add_priorities(self, ids: Sequence[int], priorities: Sequence[float]) -> None:
+    self.note_priorities(priorities)
     indices = self._assign_indices(ids)
     self._sum_tree.set(indices, _power(priorities, self._priority_exponent))
     return indices
@@ -852,6 +874,7 @@ class PrioritizedDistribution:
     return indices
 
   def update_priorities(self, ids: Sequence[int], priorities: Sequence[float]) -> None:
+    self.note_priorities(priorities)
     indices = []
     for i in ids:
       if i not in self._id_to_index:
@@ -907,7 +930,8 @@ class PrioritizedDistribution:
             'id_to_index': self._id_to_index, 'index_to_id': self._index_to_id,
             'inactive_indices': self._inactive_indices,
             'active_indices': self._active_indices,
-            'active_indices_location': self._active_indices_location}
+            'active_indices_location': self._active_indices_location,
+            'positive_written': self._positive_written}
 
   def set_state(self, state: Mapping[str, Any]) -> None:
     self._sum_tree.set_state(state['sum_tree'])
@@ -916,6 +940,8 @@ class PrioritizedDistribution:
     self._inactive_indices = state['inactive_indices']
     self._active_indices = state['active_indices']
     self._active_indices_location = state['active_indices_location']
+    self._positive_written = state.get(
+        'positive_written', bool(self._sum_tree.root() > 0.0))
 
   def check_valid(self) -> Tuple[bool, str]:
     if len(self._id_to_index) != len(self._index_to_id):
@@ -1020,6 +1046,9 @@ class PrioritizedTransitionReplay(_StorageMixin):
       backend.drop(self._slot(oldest_id))
     item_id = self._t
     add = dist._assign_indices([item_id])[0]  # pylint: disable=protected-access
+    dist.note_priorities(
+        priority if isinstance(priority, (int, float, np.floating, np.integer))
+        else None)
     if isinstance(priority, (int, float, np.floating, np.integer)):
       # host priority: exponentiated here with numpy, like the reference
       # (SumTree leaves bit-equal to the host path); the kernel's ** 1 is exact
@@ -1077,6 +1106,7 @@ class PrioritizedTransitionReplay(_StorageMixin):
     the sampled tree indices (prioritized/agent.py:201-206), one launch."""
     from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
     tree = self._device_tree()
+    self._distribution.note_priorities(None)
     _native.check(_native.lib().dqz_per_write_back(
         learner._h, _native.ptr(tree.tree), tree.capacity, _native.ptr(indices),  # pylint: disable=protected-access
         float(self._distribution.priority_exponent), _native.ptr(max_seen_dev),

@@ -337,3 +337,38 @@ def test_agent_loop_reports_a_handoff_timeout(device):
   _run(agent, 100, seed=3)
   assert agent.check_learner_health() == 0
   assert torch.isfinite(agent.learner.online).all()
+
+
+def test_online_params_is_the_haiku_tree_and_feeds_the_eval_actor(device):
+  """agent.online_params is the reference's parameter tree
+  (dqn/agent.py:192-194): Haiku module/leaf names and shapes, each leaf a
+  device view of the learner's live buffer; handed to an
+  EpsilonGreedyActor as dqn/run_atari.py:264 does, it acts with exactly the
+  learner's network (no copy, so later learning is seen too)."""
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import parts
+  agent, _ = _make('dqn', seed=7)
+  _run(agent, 80)
+  tree = agent.online_params
+  net = networks.dqn_atari_network(6)
+  assert [(m, n) for m in tree for n in tree[m]] == net.leaf_paths()
+  for (m, n), shape in zip(net.leaf_paths(), net.leaf_shapes()):
+    assert tuple(tree[m][n].shape) == shape
+  flat = agent.online_params_flat
+  assert net.flat_of_device_tree(tree) is flat
+  host = {m: {n: v.cpu().numpy() for n, v in d.items()} for m, d in tree.items()}
+  np.testing.assert_array_equal(net.flatten(host), flat.cpu().numpy())
+  actor = parts.EpsilonGreedyActor(fake_env.FrameStacker(), net, 0.0,
+                                   np.array([0, 3], np.uint32),
+                                   learner=agent.learner)
+  actor.network_params = tree
+  rng = np.random.default_rng(0)
+  for _ in range(5):
+    obs = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+    q = agent.learner.q_values_host(obs)
+    a, v = agent.learner.act(obs, 0.0, 1, 0, params=tree)
+    assert a == int(np.argmax(q)) and v == np.float32(q.max())
+  _run(agent, 40, seed=4)  # more learning: the view sees the new params
+  np.testing.assert_array_equal(net.flatten(
+      {m: {n: v.cpu().numpy() for n, v in d.items()} for m, d in tree.items()}),
+      agent.online_params_flat.cpu().numpy())

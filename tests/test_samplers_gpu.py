@@ -547,3 +547,38 @@ def test_fused_logit_sampler_equals_philox_then_choice(device):
     for o in outs:
       assert torch.equal(o, ref_draw())
   assert int(c_fused.item()) == int(c_ref.item())
+
+
+def test_device_per_all_zero_priorities_follow_the_reference_stream(device):
+  """while every priority is 0 the reference skips the target
+  draw (replay.py:689-697: prio_idx = uniform_idx, one uniform stream for
+  the usp mix).  The device replay draws the same ids with probabilities
+  1/N and leaves its RandomState exactly where the host replay's is; after
+  a positive priority both draw both streams again."""
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+
+  def make(seed=4):
+    return replay_lib.PrioritizedTransitionReplay(
+        capacity=8, structure=replay_lib.Transition(None, None, None, None, None),
+        priority_exponent=0.6, importance_sampling_exponent=lambda t: 0.4,
+        uniform_sample_probability=0.1, normalize_weights=True,
+        random_state=np.random.RandomState(seed))
+
+  dev, host = make(), make()
+  for i in range(6):
+    dev.add(replay_lib.Transition(_frame(i), 0, 0.0, 1.0, _frame(i)), priority=0.0)
+    host.add(replay_lib.Transition(i, 0, 0.0, 1.0, i), priority=0.0)
+  assert dev.on_device
+  for _ in range(3):
+    indices, _, weights = dev.sample_device(5)
+    _, host_ids, host_w = host.sample(5)
+    assert dev.distribution.index_to_id(indices.cpu().numpy()).tolist() == host_ids.tolist()
+    np.testing.assert_allclose(weights.cpu().numpy(), host_w, rtol=1e-6)
+    st_d, st_h = dev._random_state.get_state(), host._random_state.get_state()  # pylint: disable=protected-access
+    assert st_d[2] == st_h[2] and np.array_equal(st_d[1], st_h[1])
+  dev.update_priorities([2], [1.5])
+  host.update_priorities([2], [1.5])
+  indices, _, _ = dev.sample_device(5)
+  _, host_ids, _ = host.sample(5)
+  assert dev.distribution.index_to_id(indices.cpu().numpy()).tolist() == host_ids.tolist()
+  assert dev._random_state.get_state()[2] == host._random_state.get_state()[2]  # pylint: disable=protected-access
