@@ -532,8 +532,19 @@ class Workload:
     return out
 
 
+def _json_stdout():
+  """A private handle on the real stdout for the one JSON line; fd 1 itself
+  goes to stderr, so whatever RCCL / HIP print at communicator creation
+  cannot land on the line the driver parses."""
+  out = os.fdopen(os.dup(1), 'w')
+  sys.stdout.flush()
+  os.dup2(2, 1)
+  return out
+
+
 def run_gpu(args, g, rem):
   from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
+  json_out = _json_stdout()
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
   torch.cuda.set_device(local_rank)
   reps = replicas_lib.Replicas('nccl')  # RCCL; replicas only, no grad exchange
@@ -575,8 +586,9 @@ def run_gpu(args, g, rem):
     stats_vec[0].fill_(float(done))
     stats_vec[1].copy_(lrn.loss[0])
     stats_vec[2].fill_(time.perf_counter() - clock['t0'])
-    pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
-                                                    async_op=True))
+    if reps.dist is not None:
+      pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
+                                                      async_op=True))
 
   runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
                       args.stats_every, on_stats)
@@ -714,7 +726,7 @@ def run_gpu(args, g, rem):
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
   else:
     out['cpu_baseline'] = None
-  print(json.dumps(out), flush=True)
+  print(json.dumps(out), file=json_out, flush=True)
   reps.close()
   if out['handoff_status'] != 0 or out['nonfinite_loss'] or not finite:
     print('bench.py: hand-off status %d, non-finite loss %s, params finite %s: '

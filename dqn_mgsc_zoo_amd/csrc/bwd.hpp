@@ -56,19 +56,31 @@ __device__ __forceinline__ int w2p_src(int i) {
 }
 constexpr int W3P_N = 4 * 9 * 1024, W2P_N = 8 * 4 * 1024;  // 36864, 32768
 
-constexpr int FC1B_LD = 528;  // LDS row stride of the dz1 chunk: 528 = 16 (mod 32) banks apart
+// LDS row stride of the dz1 chunk.  The dW path's ds_read_b32 of rows
+// 4 kk + kq (lanes n, kq) needs rows 16 (mod 32) banks apart: 528.  The dX
+// path's ds_read_b128 A fragments (lane n reads row 16 mt + n at column
+// 4 kq) are conflict-free in every 16-lane group only with a stride of 8
+// (mod 64) dwords: 520 (528 put two lanes on each bank quad: 4 extra LDS
+// cycles per read, the 1.67 conflict cycles per LDS instruction of round 2's
+// counters).
+#ifndef DQZ_FC1DX_LD
+#define DQZ_FC1DX_LD 520
+#endif
+constexpr int FC1B_LD = 528;
+constexpr int FC1X_LD = DQZ_FC1DX_LD;
 
 // DX: dy3 = (dz1 @ W1^T) relu'(y3) (the critical path: conv3 backward waits on
 // it).  DW: dW1 + RMSProp, which only has to finish before the next step and
 // runs on the learner's side stream beside the conv backward kernels.  DW
 // must start after DX: it overwrites the W1 rows DX reads.
-constexpr int FC1B_SMEM = 32 * FC1B_LD + 4 * 2 * 256;  // floats: dz1 chunk (later the dW block) + dX partials
+constexpr int FC1B_SMEM = 32 * (FC1B_LD > FC1X_LD ? FC1B_LD : FC1X_LD) + 4 * 2 * 256;  // floats: dz1 chunk (later the dW block) + dX partials
 
 template <bool DX, bool DW>
 __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, int blk) {
   DQZ_STAMP(DW ? 11 : 5, 0);
+  constexpr int LD = DW ? FC1B_LD : FC1X_LD;
   float* s_dz = smem;
-  float(*s_red)[2][256] = reinterpret_cast<float(*)[2][256]>(smem + 32 * FC1B_LD);
+  float(*s_red)[2][256] = reinterpret_cast<float(*)[2][256]>(smem + 32 * LD);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = 16 * blk;
@@ -112,7 +124,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int f = t + 256 * i;
-        *reinterpret_cast<float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127)) = v[i];
+        *reinterpret_cast<float4*>(s_dz + (f >> 7) * LD + 4 * (f & 127)) = v[i];
       }
       __syncthreads();
       if constexpr (DX) {
@@ -120,7 +132,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
       f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const float* d = s_dz + (16 * mt + n) * FC1B_LD + 128 * w + 4 * kq;
+        const float* d = s_dz + (16 * mt + n) * LD + 128 * w + 4 * kq;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
@@ -139,7 +151,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
       // dW over the chunk: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const float* d = s_dz + (4 * kk + kq) * FC1B_LD + 128 * w + n;
+        const float* d = s_dz + (4 * kk + kq) * LD + 128 * w + n;
 #pragma unroll
         for (int q = 0; q < 8; ++q) gacc[q] = mfma4(yv[kk], d[16 * q], gacc[q]);
       }
@@ -165,7 +177,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
 #pragma unroll
   for (int q = 0; q < 8; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s_dz[(4 * kq + r) * FC1B_LD + 128 * w + 16 * q + n] = gacc[q][r];
+    for (int r = 0; r < 4; ++r) s_dz[(4 * kq + r) * LD + 128 * w + 16 * q + n] = gacc[q][r];
   __syncthreads();
   // RMSProp on this thread's 32 parameters of the 16 x 512 block, as float4
   // f = t + 256 i: row f / 128, columns 4 (f % 128) .. +3; every operand load
@@ -176,7 +188,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
   for (int i = 0; i < 8; ++i) {
     const int f = t + 256 * i;
     const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
-    gv[i] = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * FC1B_LD + 4 * (f & 127));
+    gv[i] = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * LD + 4 * (f & 127));
     if (upd) {
       o_th[i] = *reinterpret_cast<const float4*>(a.th + e);
       o_mu[i] = *reinterpret_cast<const float4*>(a.mu + e);

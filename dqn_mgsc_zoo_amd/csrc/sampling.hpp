@@ -27,15 +27,18 @@ __device__ __forceinline__ double load_fresh(const double* p) {
 }
 constexpr int SM_CHUNK = 4096;  // logits per block in the reduction / CDF passes
 
+__device__ __forceinline__ double run_term(float x, float c) { return x == -INFINITY ? 0.0 : exp((double)x - (double)c); }
+
 struct MaxSum {
-  float m, s;  // running max and sum of exp(x - m)
+  float m;   // running max
+  double s;  // float64 sum of exp(x - m) (the seed of the running state)
 };
 
 __device__ __forceinline__ MaxSum ms_combine(MaxSum a, MaxSum b) {
   if (a.m == -INFINITY) return b;
   if (b.m == -INFINITY) return a;
   const float m = fmaxf(a.m, b.m);
-  return MaxSum{m, a.s * expf(a.m - m) + b.s * expf(b.m - m)};
+  return MaxSum{m, a.s * exp((double)a.m - (double)m) + b.s * exp((double)b.m - (double)m)};
 }
 
 __device__ __forceinline__ MaxSum block_reduce_ms(MaxSum v, MaxSum* sbuf) {
@@ -99,10 +102,10 @@ __global__ __launch_bounds__(SM_THREADS) void lse_partial_kernel(float* __restri
   float m = -INFINITY;
 #pragma unroll
   for (int i = 0; i < SM_CHUNK / SM_THREADS; ++i) m = fmaxf(m, v[i]);
-  float sum = 0.f;
+  double sum = 0.0;
   if (m != -INFINITY) {
 #pragma unroll
-    for (int i = 0; i < SM_CHUNK / SM_THREADS; ++i) sum += v[i] == -INFINITY ? 0.f : expf(v[i] - m);
+    for (int i = 0; i < SM_CHUNK / SM_THREADS; ++i) sum += run_term(v[i], m);
   }
   const MaxSum acc = block_reduce_ms(MaxSum{m, sum}, sbuf);
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -138,7 +141,6 @@ __device__ __forceinline__ float logmeanexp_item(float lse, int64_t size) {
   return size == 0 ? 0.f : (float)((double)lse - log((double)size));
 }
 
-__device__ __forceinline__ double run_term(float x, float c) { return x == -INFINITY ? 0.0 : exp((double)x - (double)c); }
 
 // Pass 2 (one block): lse = m + log(s); optional logit write of a new item:
 // logits[write_pos] = size == 0 ? 0 : lse - log(size) (log-mean-exp); seeds
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
   const MaxSum acc = combine_parts(part, nparts, sbuf);
   if (threadIdx.x == 0) {
     // the f32 lse every sampler and add uses: c + log(S) of the running state
-    const float lse = acc.m == -INFINITY ? -INFINITY : (float)((double)acc.m + log((double)acc.s));
+    const float lse = acc.m == -INFINITY ? -INFINITY : (float)((double)acc.m + log(acc.s));
     if (lse_out) *lse_out = lse;
     float item = -INFINITY;
     if (logits && write_pos >= 0) {
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
       logits[write_pos] = item;
     }
     if (run) {
-      LogitRun r{acc.m == -INFINITY ? 0.0 : (double)acc.s, acc.m == -INFINITY ? 0.f : acc.m, 1};
+      LogitRun r{acc.m == -INFINITY ? 0.0 : acc.s, acc.m == -INFINITY ? 0.f : acc.m, 1};
       r.S += run_term(item, r.c);  // the slot was -inf during the scan
       *run = r;
     }
@@ -346,37 +348,51 @@ __global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float*
   if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
 }
 
-// Inclusive scan of one double per thread over the block, in a fixed
-// (Hillis-Steele) order: deterministic run to run.
-__device__ __forceinline__ double block_scan_incl_f64(double v, double* s) {
-  const int t = threadIdx.x;
-  s[t] = v;
-  __syncthreads();
+// Scan of one double per thread over the block in a fixed order
+// (deterministic run to run): a Hillis-Steele scan inside each wave by
+// shuffles, then each wave adds the totals of the waves before it, summed in
+// wave order.  Returns the exclusive prefix; *tot gets the block total with
+// exactly the bits the last lane's inclusive prefix has.  Two barriers.
+__device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, double* tot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double incl = v;
 #pragma unroll
-  for (int o = 1; o < SM_THREADS; o <<= 1) {
-    const double add = t >= o ? s[t - o] : 0.0;
-    __syncthreads();
-    v += add;
-    s[t] = v;
-    __syncthreads();
+  for (int o = 1; o < 64; o <<= 1) {
+    const double up = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += up;
   }
-  return v;
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  double pre = 0.0, all = 0.0;
+  constexpr int W = SM_THREADS / 64;
+#pragma unroll
+  for (int w = 0; w < W - 1; ++w) {
+    if (w < wave) pre += s_wave[w];
+    all += s_wave[w];
+  }
+  const double last_incl = s_wave[W - 1] + all;  // the last lane's incl + pre, same operands
+  double excl = __shfl_up(incl, 1, 64);
+  excl = lane == 0 ? 0.0 : excl;
+  excl = wave == 0 ? excl : (lane == 0 ? pre : excl + pre);
+  *tot = last_incl;
+  __syncthreads();
+  return excl;
 }
 
-// One block per query u: find the chunk whose normalised cumulative sum
-// first exceeds u, then inside the chunk the lane (16 logits each) and the
-// logit.  Both levels are parallel: each lane sums a contiguous run of block
-// sums / holds 16 logits, a block-wide scan gives the exclusive prefixes,
-// and the first crossing is the minimum index any lane finds.  Returns the
-// first index with cdf > u (searchsorted side='right'); cdf = cumsum(float64
-// p) / total.
+// One query u: find the chunk whose normalised cumulative sum first exceeds
+// u, then inside the chunk the lane (16 logits each) and the logit.  Both
+// levels are parallel: each lane sums a contiguous run of block sums / holds
+// 16 logits (four float4 loads), a block-wide scan gives the exclusive
+// prefixes, and the first crossing is the minimum index any lane finds.
+// Returns the first index with cdf > u (searchsorted side='right'); cdf =
+// cumsum(float64 p) / total.
 constexpr int SM_PER_LANE = SM_CHUNK / SM_THREADS;  // 16
 
 // bsum is read with agent-scope (L2-bypassing) loads: in the fused sampler
 // its producers are other workgroups of the same launch.
 __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, float L,
                                                        const double* bsum, int nblocks, double u) {
-  __shared__ double s_scan[SM_THREADS];
+  __shared__ double s_wave[SM_THREADS / 64];
   __shared__ double s_before;
   __shared__ int s_blk;
   __shared__ unsigned long long s_idx;
@@ -395,10 +411,10 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
     s_blk = nblocks - 1;
     s_idx = ~0ull;
   }
-  const double incl = block_scan_incl_f64(mine, s_scan);
-  const double tot = s_scan[SM_THREADS - 1];
+  double tot;
+  const double excl = block_scan_excl_f64(mine, s_wave, &tot);
   {
-    double run = incl - mine;
+    double run = excl;
     for (int b = b0; b < b1; ++b) {
       const double v = b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
       if ((run + v) / tot > u) {
@@ -408,25 +424,41 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
       run += v;
     }
   }
+  // level 2 loads do not depend on the crossing lane's prefix: issue them
+  // as soon as the chunk is known
   __syncthreads();
   const int blk = s_blk;
+  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
+  float xv[SM_PER_LANE];
+  if (base + SM_PER_LANE <= n && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < SM_PER_LANE / 4; ++q) {
+      const float4 f = *reinterpret_cast<const float4*>(x + base + 4 * q);
+      xv[4 * q] = f.x;
+      xv[4 * q + 1] = f.y;
+      xv[4 * q + 2] = f.z;
+      xv[4 * q + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < SM_PER_LANE; ++i) xv[i] = base + i < n ? x[base + i] : -INFINITY;
+  }
   if (blk >= b0 && blk < b1) {  // the owner of the crossing block publishes the mass before it
-    double run = incl - mine;
+    double run = excl;
     for (int b = b0; b < blk; ++b) run += b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
     s_before = run;
   }
   // level 2: the chunk's 256 lanes x 16 logits
-  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
   double p[SM_PER_LANE];
   double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) {
-    p[i] = base + i < n ? (double)prob_f32(x[base + i], L) : 0.0;
+    p[i] = xv[i] == -INFINITY ? 0.0 : (double)prob_f32(xv[i], L);
     lane += p[i];
   }
-  __syncthreads();  // s_before published
-  const double lincl = block_scan_incl_f64(lane, s_scan);
-  double run = s_before + (lincl - lane);
+  double tot2;
+  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);  // its barriers publish s_before
+  double run = s_before + lexcl;
   if (run / tot <= u && (run + lane) / tot > u) {
     for (int i = 0; i < SM_PER_LANE; ++i) {
       run += p[i];
@@ -565,13 +597,14 @@ __device__ __forceinline__ void sumtree_set_small_body(double* tree, int levels,
   const bool live = i < n && leaf >= 0;
   if (!live) leaf = -1;
   const double leaf_v = v;
-  for (int l0 = 0; l0 < levels; l0 += 8) {  // one batch of loads per 8 levels
-    double t8[8];
+  constexpr int kBatch = 24;  // every sibling of a 2^24-leaf path in one round trip
+  for (int l0 = 0; l0 < levels; l0 += kBatch) {
+    double tb[kBatch];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) t8[j] = live && l0 + j < levels ? tree[(leaf >> (l0 + j)) ^ 1] : 0.0;
+    for (int j = 0; j < kBatch; ++j) tb[j] = live && l0 + j < levels ? tree[(leaf >> (l0 + j)) ^ 1] : 0.0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (l0 + j < levels) s_sib[l0 + j][i] = t8[j];
+    for (int j = 0; j < kBatch; ++j)
+      if (l0 + j < levels) s_sib[l0 + j][i] = tb[j];
   }
   for (int l = 0; l < levels; ++l) s_rep[l][i] = -1;
   s_leaf[i] = leaf;
@@ -617,14 +650,17 @@ __global__ __launch_bounds__(ST_FAST) void per_write_back_kernel(double* tree, i
                                                                  const int32_t* slots, const float* td, double alpha,
                                                                  int n, double* max_seen) {
   __shared__ double s_max[ST_FAST / 64];
+  __shared__ int32_t s_slot[ST_FAST];
   const int i = threadIdx.x;
   int64_t leaf = -1;
   double p = 0.0;
+  const int32_t s = i < n ? slots[i] : -1;
+  if (i < n) p = fabs((double)td[i]);
+  s_slot[i] = s;
+  __syncthreads();
   if (i < n) {
-    const int32_t s = slots[i];
-    p = fabs((double)td[i]);
-    bool last = true;
-    for (int j = i + 1; j < n; ++j) last &= slots[j] != s;
+    bool last = true;  // the last draw of a repeated slot wins (SumTree.set order)
+    for (int j = i + 1; j < n; ++j) last &= s_slot[j] != s;
     if (last) leaf = cap + s;
   }
   double m = p;
@@ -739,10 +775,26 @@ struct PerSampleArgs {
   double* out_probs;
 };
 
+// Depths 0 .. PS_TOPD of the tree (2047 nodes, 16 KB) are staged in LDS once
+// per launch and shared by every draw; below them a half-wave descends five
+// levels per global round trip (lane l holds relative nodes l and l + 32 of
+// the 62 below the current node: depth k = floor(log2(q + 2)), j = q + 2 -
+// 2^k) and takes the decisions from registers.  At 2^20 leaves: one shared
+// 16 KB load + two dependent rounds instead of five.  Same compare-and-
+// subtract arithmetic as SumTree._query_single (replay.py:539-559), so the
+// same node sequence bit for bit.
+constexpr int PS_TOPD = 10;
+
 __global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
+  __shared__ double s_top[2 << PS_TOPD];  // node i at s_top[i], i in [1, 2^(dtop + 1))
   __shared__ double s_w[1024];
   const bool inj = a.inj_u != nullptr;
   const uint64_t ctr = inj ? 0 : *a.counter;
+  const int dtop = min(a.levels, PS_TOPD);
+  const int ntop = (2 << dtop) - 1;
+  for (int q = threadIdx.x; q < ntop; q += blockDim.x) s_top[1 + q] = a.tree[1 + q];
+  __syncthreads();
+  const double root = s_top[1];
   const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
   for (int i = h; i < a.n; i += 32) {
     double u_target, u_mix;
@@ -759,20 +811,62 @@ __global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
       uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
     }
     const bool use_uniform = u_mix < a.usp;
-    // t = u_target * root inside the descent (the root arrives with the first round)
-    Descent d = halfwave_descend(a.tree, a.cap, a.levels, 0.0, use_uniform ? 0.0 : u_target, l);
-    const double root = d.root;
     int64_t idx = uni;
     double leaf;
     if (root > 0.0 && !use_uniform) {
-      idx = d.slot;
-      leaf = d.leaf;
+      double t = u_target * root;  // u in [0, 1): t < root in fp64 (no range check, as the serial descent)
+      int64_t node = 1;
+      int depth = 0;
+      for (; depth < dtop; ++depth) {
+        const double left = s_top[2 * node];
+        if (t < left) {
+          node = 2 * node;
+        } else {
+          t -= left;
+          node = 2 * node + 1;
+        }
+      }
+      double lv = s_top[node];  // the leaf itself when the whole tree sits in LDS
+      while (depth < a.levels) {
+        const int K = min(5, a.levels - depth);
+        double v0 = 0.0, v1 = 0.0;
+        {
+          const int k0 = 31 - __builtin_clz(l + 2), k1 = 31 - __builtin_clz(l + 34);
+          if (k0 <= K) v0 = a.tree[(node << k0) + (l + 2 - (1 << k0))];
+          if (k1 <= K) v1 = a.tree[(node << k1) + (l + 34 - (1 << k1))];
+        }
+        int64_t pos = 0;
+        for (int k = 1; k <= K; ++k) {
+          const int q = (1 << k) - 2 + 2 * (int)pos;  // left child at relative depth k
+          const double left = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
+          if (t < left) {
+            pos = 2 * pos;
+          } else {
+            t -= left;
+            pos = 2 * pos + 1;
+          }
+        }
+        const int q = (1 << K) - 2 + (int)pos;
+        lv = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
+        node = (node << K) + pos;
+        depth += K;
+      }
+      idx = node - a.cap;
+      leaf = lv;
     } else {
       leaf = a.tree[a.cap + idx];
     }
     const double up = 1.0 / (double)a.size;
     const double pp = root > 0.0 ? leaf / root : up;
-    const double prob = __dadd_rn(__dmul_rn(1.0 - a.usp, pp), __dmul_rn(a.usp, up));
+    double prob;
+    {
+      // numpy rounds the product and the sum separately: no fma (hipcc
+      // contracts even __dmul_rn + __dadd_rn under its default fp-contract)
+#pragma clang fp contract(off)
+      const double x1 = (1.0 - a.usp) * pp;
+      const double x2 = a.usp * up;
+      prob = x1 + x2;
+    }
     const double w = pow(up / prob, a.beta);
     if (l == 0) {
       if (a.out_indices) a.out_indices[i] = (int32_t)idx;

@@ -33,6 +33,9 @@ class Replicas:
     self.rank = int(os.environ.get('RANK', '0'))
     self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     self.dist = None
+    self.backend = None
+    if self.world == 1 and os.environ.get('DQZ_BENCH_NO_GROUP') == '1':
+      return  # diagnostic A/B only: a lone rank without a process group
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
     if not dist.is_initialized():
       if self.world == 1 and 'MASTER_ADDR' not in os.environ:

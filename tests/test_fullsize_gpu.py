@@ -242,7 +242,8 @@ def test_config4_per_1m_sample_step_write_back(device, store):
   leaves = np.zeros(CAP)
   leaves[index] = replay_lib._power(rng.uniform(0.01, 2.0, CAP), alpha)  # pylint: disable=protected-access
   leaves[index[rng.integers(0, CAP, 2000)]] = 0.0  # some zero priorities
-  host.sum_tree.set_all(leaves)
+  host.sum_tree.set_all(leaves)  # the bulk form of add_priorities
+  host.note_priorities(leaves)
   assert host.sum_tree.capacity == 1 << 20
   dist = copy.deepcopy(host)
   dist.to_device(device)

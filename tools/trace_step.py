@@ -7,19 +7,16 @@ the median of the named intervals between stamps (10 ns ticks -> us).
 """
 import ctypes
 import os
-import subprocess
 import sys
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')
-subprocess.check_call(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-shared', '-fPIC',
-                       '-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split(),
-                       '-I' + os.path.join(ROOT, 'include'), '-o', LIB,
-                       os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'csrc', 'learner.hip')])
-os.environ['DQZ_LIB'] = LIB
 sys.path.insert(0, ROOT)
+import __graft_entry__  # noqa: E402
+__graft_entry__._compile_lib(LIB, ['-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split()])  # pylint: disable=protected-access
+os.environ['DQZ_LIB'] = LIB
 import torch  # noqa: E402
 from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
 
