@@ -489,10 +489,14 @@ class Workload:
             stream()))
 
       def one_step():
+        # the |td|^alpha write-back runs inside the learner's backward launch
         per_sample()
-        lrn.step(store, slots, w)
-        per_write_back()
-      self.samplers = {'per_sample': per_sample, 'per_write_back': per_write_back}
+        lrn.step(store, slots, w,
+                 write_back=(tree, tcap, slots, PER_ALPHA, max_seen))
+      # per_write_back is timed as a stand-alone launch for reference only:
+      # the step runs it inside the backward launch
+      self.samplers = {'per_sample': per_sample,
+                       'per_write_back_standalone': per_write_back}
     elif algo == 'mgsc':
       from dqn_mgsc_zoo_amd import replay_circular as rc  # pylint: disable=g-import-not-at-top
       gen = torch.Generator(device=dev)
@@ -547,11 +551,7 @@ def run_gpu(args, g, rem):
   json_out = _json_stdout()
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
   torch.cuda.set_device(local_rank)
-  reps = replicas_lib.Replicas('nccl')  # RCCL; replicas only, no grad exchange
-  world, rank = reps.world, reps.rank
-  if world != args.gpus:
-    print('bench.py: world %d != --gpus %d' % (world, args.gpus), file=sys.stderr)
-    return 2
+  rank = int(os.environ.get('RANK', '0'))
   dev = torch.device('cuda', local_rank)
 
   algo = args.algo
@@ -572,6 +572,16 @@ def run_gpu(args, g, rem):
         with torch.cuda.graph(graphs[k]):
           for _ in range(k):
             one_step()
+
+  # The RCCL group (replicas only, no gradient exchange) is formed after the
+  # graphs are captured: formed before, its mere existence slowed every
+  # replayed step by ~9 % (14,381 vs 15,775 steps/s, tools/ab_group.sh;
+  # tools/rccl_overhead.py times both orders).
+  reps = replicas_lib.Replicas('nccl')
+  world = reps.world
+  if world != args.gpus or reps.rank != rank:
+    print('bench.py: world %d != --gpus %d' % (world, args.gpus), file=sys.stderr)
+    return 2
 
   # Statistics vector [steps done, last loss, seconds since the timed region
   # began], all-gathered over RCCL every stats_every steps: enqueued on the

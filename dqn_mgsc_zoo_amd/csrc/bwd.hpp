@@ -4,6 +4,7 @@
 #include "conv1.hpp"
 #include "fwd.hpp"
 #include "head.hpp"
+#include "sampling.hpp"
 
 namespace dqz {
 
@@ -784,16 +785,29 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // retire instead of spinning from the start.  Sample jobs keep the XCD-aware
 // decode (each range starts at a multiple of 8, so producer and consumer
 // share an L2).
+// With a PER write-back (wb.tree set, dqz_learner_step_per) the grid gets 8
+// leading workgroups: wave 0 of the first runs per_write_back_wave beside the
+// whole backward (the TD errors are final since the head), the other seven
+// exit at once (the sample ranges keep their XCD alignment).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
-    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1) {
+    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
   constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
   constexpr int kW2 = C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN;
   constexpr int kW3 = C2V_WIN > C1H_SMEM ? C2V_WIN : C1H_SMEM;
   constexpr int kWA = kW > kW2 ? kW : kW2;
-  __shared__ __attribute__((aligned(16))) float smem[kWA > kW3 ? kWA : kW3];
+  constexpr int kSmem = kWA > kW3 ? kWA : kW3;
+  static_assert(kSmem * 4 >= PWB_LDS_BYTES, "the write-back's LDS comes out of the backward's buffer");
+  __shared__ __attribute__((aligned(16))) float smem[kSmem];
   const int B8 = (c3.B + 7) / 8 * 8;
   constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
   int i = blockIdx.x;
+  if (wb.tree) {
+    if (i < 8) {
+      if (i == 0 && threadIdx.x < 64) per_write_back_wave(wb, reinterpret_cast<char*>(smem));
+      return;
+    }
+    i -= 8;
+  }
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
     if (!sj.valid) return;

@@ -270,6 +270,7 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
 // lane's four k for steps e = 0..3 are contiguous: one float4 A load per
 // (row tile, 16-block).  Partials [Z][FC1_S][B][512] are reduced by the head.
 constexpr int FC1_S = 7, FC1_KS = FLAT / FC1_S, FC1_KW = FC1_KS / 4;  // 448, 112
+constexpr int Z_MAX_FC1 = 3;  // network copies of one fc1 launch (online, target, online(s_t))
 
 struct Fc1FwdArgs {
   const float* in;  // [Z][B][3136]
@@ -277,6 +278,12 @@ struct Fc1FwdArgs {
   int64_t w_off;
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
+  // In-launch split-K reduce (or null: the head sums the FC1_S partials):
+  // the last of a tile's FC1_S split blocks to arrive sums them in split
+  // order into sum[Z][B][512] (pre-activation, no bias), so the head loads
+  // one row per sample instead of FC1_S.
+  float* sum;
+  int* cnt;         // [Z * MG * 32] tile arrival counters (x Handoff::kStride ints), zero between launches
 };
 
 // The MFMA body of one fc1 block: its (z, split s, column tile nt, row group
@@ -337,6 +344,58 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   fc1_fwd_tile(a, s_red, z, s, nt, mg);
   DQZ_STAMP(3, 2);
   const int t = threadIdx.x;
+  if (a.sum) {
+    // 128 threads x 4 columns: row t / 4, columns 16 nt + 4 (t % 4) .. + 3.
+    // Partials go out write-through (16-B sc1 stores) and are read back with
+    // sc1 loads by the tile's last block (the guide's hand-off row: one lane
+    // per storing workgroup adds to one counter after every wave drained;
+    // the workgroup whose add came last reads).  The other blocks' tiles
+    // share this block's XCD (the block -> tile map above), so the reads are
+    // served from that L2's backing MALL lines at worst.
+    __shared__ int s_last;
+    const int row = t >> 2, c4 = 4 * (t & 3);
+    const int mt = row >> 4, r16 = row & 15;
+    const int64_t colo = 16 * nt + c4;
+    const int64_t pbytes = (int64_t)Z_MAX_FC1 * FC1_S * a.B * HID * 4;  // buffer range for the rsrc
+    if (t < 128) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = mt * 256 + r16 * 16 + c4 + e;
+        v[e] = (s_red[k] + s_red[512 + k]) + (s_red[1024 + k] + s_red[1536 + k]);
+      }
+      if (32 * mg + row < a.B) {
+        const int64_t off = ((((int64_t)z * FC1_S + s) * a.B + 32 * mg + row) * HID + colo) * 4;
+        store_sc1_f4(a.part, (int)min(pbytes, (int64_t)INT32_MAX), (int)off, v);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* cnt = a.cnt + ((z * a.MG + mg) * (HID / 16) + nt) * Handoff::kStride;
+    if (t == 0) s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FC1_S - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (t < 128 && 32 * mg + row < a.B) {
+      float4 pv[FC1_S];
+#pragma unroll
+      for (int ss = 0; ss < FC1_S; ++ss) {
+        const int64_t e = (((int64_t)z * FC1_S + ss) * a.B + 32 * mg + row) * HID + colo;
+        pv[ss] = load_sc1_f4(reinterpret_cast<const float4*>(a.part), (int)min(pbytes, (int64_t)INT32_MAX), (int)(e / 4));
+      }
+      float4 acc = pv[0];
+#pragma unroll
+      for (int ss = 1; ss < FC1_S; ++ss) {
+        acc.x += pv[ss].x;
+        acc.y += pv[ss].y;
+        acc.z += pv[ss].z;
+        acc.w += pv[ss].w;
+      }
+      *reinterpret_cast<float4*>(a.sum + ((int64_t)z * a.B + 32 * mg + row) * HID + colo) = acc;
+    }
+    if (t == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DQZ_STAMP(3, 3);
+    return;
+  }
   // 512 outputs (32 rows x 16 cols), 2 per thread
 #pragma unroll
   for (int h = 0; h < 2; ++h) {

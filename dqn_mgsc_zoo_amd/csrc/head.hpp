@@ -260,10 +260,16 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
 // Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.
 inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
   if (h.S > 7) return hipErrorInvalidValue;
-  if (h.A <= 8)
+  if (h.S == 1) {  // fc1 sums reduced in fc1_fwd_kernel: one row per sample
+    if (h.A <= 8)
+      hipLaunchKernelGGL((head_kernel<8, 1>), dim3(grid), dim3(HID), 0, st, h);
+    else
+      hipLaunchKernelGGL((head_kernel<MAXA, 1>), dim3(grid), dim3(HID), 0, st, h);
+  } else if (h.A <= 8) {
     hipLaunchKernelGGL((head_kernel<8, 7>), dim3(grid), dim3(HID), 0, st, h);
-  else
+  } else {
     hipLaunchKernelGGL((head_kernel<MAXA, 7>), dim3(grid), dim3(HID), 0, st, h);
+  }
   return hipGetLastError();
 }
 

@@ -56,12 +56,22 @@ struct dqz_learner {
   int64_t off[10], sz[10], total;
   int S_fc1, S2, S3;
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
+  float* fc1sum;  // [Z][B][512] fc1 pre-activations summed by fc1_fwd_kernel's last split block
+  int32_t* fc1cnt;  // its tile arrival counters
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
+
+// fc1 split-K partials summed inside fc1_fwd_kernel by each tile's last split
+// block (the head then loads one pre-activation row per sample) instead of by
+// the head (DQZ_FC1_REDUCE=0).
+#ifndef DQZ_FC1_REDUCE
+#define DQZ_FC1_REDUCE 1
+#endif
+constexpr bool kFc1Reduce = DQZ_FC1_REDUCE != 0;
 
 static int g_attr_done = 0;
 
@@ -114,10 +124,12 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N};
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
+                           (int64_t)Z_MAX_FC1 * MAXB * HID, (int64_t)Z_MAX_FC1 * (MAXB / 32) * (HID / 16) * Handoff::kStride};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
-                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p};
+                    &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p,
+                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -245,6 +257,8 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   f1.B = B;
   f1.MG = (B + 31) / 32;
   f1.part = L->fc1p;
+  f1.sum = kFc1Reduce ? L->fc1sum : nullptr;
+  f1.cnt = L->fc1cnt;
   DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
@@ -253,8 +267,8 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
 static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
   HeadArgs h{};
   memset(&h, 0, sizeof(h));
-  h.fc1p = L->fc1p;
-  h.S = L->S_fc1;
+  h.fc1p = kFc1Reduce ? L->fc1sum : L->fc1p;
+  h.S = kFc1Reduce ? 1 : L->S_fc1;
   h.h1 = L->h1;
   h.nz = nz;
   h.b1_off = L->off[7];
@@ -276,7 +290,7 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
-                     int gacc = 0) {
+                     int gacc = 0, const PerWbArgs* wb = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -382,8 +396,14 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
                        L->spin_max};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
-  const int grid = 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 16 * B8;
-  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw);
+  PerWbArgs wbk{};
+  if (wb) {
+    wbk = *wb;
+    wbk.td = L->td;
+    wbk.n = B;
+  }
+  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 16 * B8;
+  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
@@ -423,6 +443,19 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
 int dqz_learner_step(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream) {
   return step_impl(L, P, S, slots, is_weights, stream, kNoProfile);
+}
+
+int dqz_learner_step_per(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
+                         const float* is_weights, double* tree, int64_t cap, const int32_t* indices, double alpha,
+                         double* max_seen_dev, void* stream) {
+  if (!L || !tree || !indices || !max_seen_dev) return fail(DQZ_ERR_INVALID, "null argument");
+  if (L->cfg.batch > 64) return fail(DQZ_ERR_INVALID, "the fused write-back takes batch <= 64 (use dqz_per_write_back)");
+  if (cap < 1 || (cap & (cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two");
+  int levels = 0;
+  while (((int64_t)1 << levels) < cap) ++levels;
+  if (levels > PWB_LEVELS) return fail(DQZ_ERR_INVALID, "cap must be <= 2^%d for the fused write-back", PWB_LEVELS);
+  PerWbArgs wb{tree, cap, levels, indices, nullptr, alpha, 0, max_seen_dev};
+  return step_impl(L, P, S, slots, is_weights, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0, &wb);
 }
 
 int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_store* S, int64_t base, int64_t size,
@@ -1209,6 +1242,8 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, C), dim3(256), 0, st, c3);
     DQZ_HIP(hipGetLastError());
     Fc1FwdArgs f1;
+    f1.sum = nullptr;
+    f1.cnt = nullptr;
     f1.in = L->y3;
     f1.nz = nv;
     f1.w_off = L->off[6];

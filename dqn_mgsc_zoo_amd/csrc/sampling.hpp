@@ -675,6 +675,86 @@ __global__ __launch_bounds__(ST_FAST) void per_write_back_kernel(double* tree, i
   }
 }
 
+// The PER priority write-back run by ONE wave inside another launch
+// (bwd_bc_kernel's first workgroup, dqz_learner_step_per): the same
+// arithmetic as per_write_back_kernel (|td| -> max_seen, p^alpha, the last
+// draw of a repeated slot wins, ancestors rebuilt as left + right through the
+// levels where another updated leaf's path joins), for n <= 64 leaves, with
+// its LDS carved from the host launch's buffer (`lds`, >= PWB_LDS_BYTES), so
+// the host kernel's LDS footprint does not grow.  Lanes are the draws; one
+// wave runs in lockstep, so LDS writes of one level are read by the next
+// after a wave barrier.
+constexpr int PWB_LEVELS = 24;  // trees of up to 2^24 leaves
+constexpr int PWB_LDS_BYTES = 64 * (8 * PWB_LEVELS + 8 + 8 + 4 + 2 * PWB_LEVELS);
+
+struct PerWbArgs {
+  double* tree;          // null: no write-back in this launch
+  int64_t cap;
+  int levels;
+  const int32_t* slots;  // tree indices of the batch (dqz_per_sample's out_indices)
+  const float* td;       // the learner's TD errors of this step
+  double alpha;
+  int n;
+  double* max_seen;
+};
+
+__device__ __forceinline__ void per_write_back_wave(const PerWbArgs& a, char* lds) {
+  double* s_sib = reinterpret_cast<double*>(lds);      // [PWB_LEVELS][64]
+  double* s_val = s_sib + PWB_LEVELS * 64;             // [64]
+  int64_t* s_leaf = reinterpret_cast<int64_t*>(s_val + 64);  // [64]
+  int32_t* s_slot = reinterpret_cast<int32_t*>(s_leaf + 64); // [64]
+  short* s_rep = reinterpret_cast<short*>(s_slot + 64);       // [PWB_LEVELS][64]
+  const int i = threadIdx.x & 63;
+  const int n = a.n, levels = a.levels;
+  const int32_t sl = i < n ? a.slots[i] : -1;
+  const double p = i < n ? fabs((double)a.td[i]) : 0.0;
+  s_slot[i] = sl;
+  __builtin_amdgcn_wave_barrier();
+  int64_t leaf = -1;
+  if (i < n) {
+    bool last = true;
+    for (int j = i + 1; j < n; ++j) last &= s_slot[j] != sl;
+    if (last) leaf = a.cap + sl;
+  }
+  const bool live = leaf >= 0;
+  double tb[PWB_LEVELS];
+#pragma unroll
+  for (int l = 0; l < PWB_LEVELS; ++l) tb[l] = live && l < levels ? a.tree[(leaf >> l) ^ 1] : 0.0;
+  double m = p;
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  double v = p == 0.0 ? 0.0 : pow(p, a.alpha);
+  const double leaf_v = v;
+  s_leaf[i] = leaf;
+  s_val[i] = v;
+  for (int l = 0; l < levels; ++l) s_rep[l * 64 + i] = -1;
+  __builtin_amdgcn_wave_barrier();
+  if (live)
+    for (int j = 0; j < n; ++j) {
+      const int64_t o = s_leaf[j];
+      const uint64_t d = (uint64_t)(leaf ^ o);
+      if (o >= 0 && d != 0) s_rep[(63 - __builtin_clzll(d)) * 64 + i] = (short)j;
+    }
+#pragma unroll
+  for (int l = 0; l < PWB_LEVELS; ++l)
+    if (l < levels) s_sib[l * 64 + i] = tb[l];
+  __builtin_amdgcn_wave_barrier();
+  for (int l = 0; l < levels; ++l) {
+    const int r = s_rep[l * 64 + i];
+    const double other = r >= 0 ? s_val[r] : s_sib[l * 64 + i];
+    const double parent = ((leaf >> l) & 1) ? other + v : v + other;
+    __builtin_amdgcn_wave_barrier();  // every lane has read level l before any writes level l + 1
+    v = parent;
+    s_val[i] = v;
+    s_sib[l * 64 + i] = v;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (live) {
+    a.tree[leaf] = leaf_v;
+    for (int l = 0; l < levels; ++l) a.tree[leaf >> (l + 1)] = s_sib[l * 64 + i];
+  }
+  if (i == 0) *a.max_seen = fmax(*a.max_seen, m);
+}
+
 // Descent of SumTree._query_single (replay.py:539-559) by one half-wave (32
 // lanes), four tree levels per global round trip.  In the implicit layout
 // the descendants of `node` at relative depth k are the contiguous indices

@@ -108,12 +108,24 @@ class Learner:
 
   # -- hot path ------------------------------------------------------------
 
-  def step(self, store, slots, weights=None, stream=None):
-    """One learner step on replay `slots` (device int32 [B])."""
+  def step(self, store, slots, weights=None, stream=None, write_back=None):
+    """One learner step on replay `slots` (device int32 [B]).
+
+    write_back (PER only): (tree, cap, indices, alpha, max_seen_dev) — the
+    priority write-back of this step's |td| (dqz_per_write_back's arguments)
+    folded into the backward launch (dqz_learner_step_per)."""
     if slots.dtype != torch.int32 or slots.numel() != self.batch_size:
       raise ValueError('slots must be a device int32 tensor of batch size')
     if self.algo == 'per' and weights is None:
       raise ValueError('PER step needs importance weights')
+    if write_back is not None:
+      tree, cap, indices, alpha, max_seen = write_back
+      _native.check(_native.lib().dqz_learner_step_per(
+          self._h, ctypes.byref(self._params_c), store.c_ref(),
+          _native.ptr(slots), _native.ptr(weights), _native.ptr(tree), int(cap),
+          _native.ptr(indices), float(alpha), _native.ptr(max_seen),
+          _native.stream_handle(stream)))
+      return
     _native.check(_native.lib().dqz_learner_step(
         self._h, ctypes.byref(self._params_c), store.c_ref(),
         _native.ptr(slots), _native.ptr(weights), _native.stream_handle(stream)))

@@ -4,10 +4,11 @@ Double-Q loss weighted by importance-sampling weights, new transitions get
 the running max priority, learned priorities are |td| (agent.py:187-206).
 
 With frame transitions the replay's sum tree lives in HBM and a learn is
-three device calls with no host synchronisation: `sample_device` (the
+two device calls with no host synchronisation: `sample_device` (the
 replay's RandomState draws, resolved on device: tree indices, slots, IS
-weights), the learner step, and `write_back` (|td| -> max_seen_priority ->
-p ** alpha into the tree).  `max_seen_priority` is then a device scalar,
+weights) and the learner step with the write-back (|td| ->
+max_seen_priority -> p ** alpha into the tree) folded into its backward
+launch (dqz_learner_step_per).  `max_seen_priority` is then a device scalar,
 read back only when asked for.  Host-stored items keep the reference's host
 path.
 """
@@ -44,8 +45,10 @@ class PrioritizedDqn(agent_base.DeviceDqnAgent):
     if self._replay.on_device:
       indices, slots, weights = self._replay.sample_device(
           self._batch_size, out=self._sample_out)
-      self._learner.step(self._store(), slots, weights)
-      self._replay.write_back(self._learner, indices, self._max_seen_dev)
+      wb = self._replay.write_back_args(indices, self._max_seen_dev)
+      self._learner.step(self._store(), slots, weights, write_back=wb)
+      if wb is None:
+        self._replay.write_back(self._learner, indices, self._max_seen_dev)
       return
     ids, slots, weights = self._replay.sample_slots(self._batch_size)
     self._w.copy_(torch.from_numpy(np.asarray(weights, np.float32)))

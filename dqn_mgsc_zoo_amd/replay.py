@@ -1112,6 +1112,18 @@ class PrioritizedTransitionReplay(_StorageMixin):
         float(self._distribution.priority_exponent), _native.ptr(max_seen_dev),
         _native.stream_handle()))
 
+  def write_back_args(self, indices, max_seen_dev):
+    """The write-back of `indices` as Learner.step(write_back=...) folds it
+    into the learner's backward launch (dqz_learner_step_per), or None when
+    the batch or the tree is past that path's limits (then call
+    write_back after the step)."""
+    tree = self._device_tree()
+    if indices.numel() > 64 or tree.capacity > (1 << 24):
+      return None
+    self._distribution.note_priorities(None)
+    return (tree.tree, tree.capacity, indices,
+            float(self._distribution.priority_exponent), max_seen_dev)
+
   def sample_ids(self, size: int):
     """(ids, normalised importance weights) as the reference computes them."""
     if self._distribution.on_device:

@@ -132,6 +132,19 @@ int dqz_learner_step_uniform(dqz_learner* learner, const dqz_params* params, con
                              int64_t base, int64_t size, int64_t capacity, uint64_t seed,
                              uint64_t* counter_dev, int32_t* slots_out, void* stream);
 
+/* PER learner step with the priority write-back folded in
+ * (prioritized/agent.py:187-206): dqz_learner_step on `slots` with the IS
+ * weights, then — inside the same backward launch, in its first workgroup,
+ * beside the backward pass — what dqz_per_write_back(tree, cap, indices,
+ * alpha, max_seen_dev) does after it: p = |td|, *max_seen_dev = max(...,
+ * max p), leaf[indices[i]] = p^alpha with the last draw of a repeated index
+ * winning, ancestors rebuilt (bit-identical sums).  indices: device int32
+ * [B] tree indices (dqz_per_sample's out_indices).  cap: a power of two <=
+ * 2^24; batch <= 64.  Saves the write-back's own launch. */
+int dqz_learner_step_per(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                         const int32_t* slots, const float* is_weights, double* tree, int64_t cap,
+                         const int32_t* indices, double alpha, double* max_seen_dev, void* stream);
+
 /* Gradient only: d loss / d params of the same step into grad_out (device
  * f32, dqz_param_layout order, padding untouched); params->online / mu / nu
  * are not modified and mu / nu may be NULL.  = jax.grad(loss_fn) at

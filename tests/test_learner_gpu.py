@@ -351,3 +351,61 @@ def test_handoff_timeout_is_reported_and_cleared(device):
   assert lrn.sync_status() == 0 and ref.sync_status() == 0
   for which in ('online', 'mu', 'nu'):
     assert torch.equal(getattr(lrn, which), getattr(ref, which)), which
+
+
+def test_fused_per_write_back_equals_the_separate_launch(device):
+  """dqz_learner_step_per (write-back folded into the backward launch) ==
+  dqz_learner_step + dqz_per_write_back: same parameters, the same sum tree
+  bit for bit (duplicate draws keep the last), the same running max, also
+  under hipGraph replay."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  batch, alpha = 32, 0.6
+  _, a, st, _, _, _, _, _ = _setup('per', batch, seed=41)
+  _, b, _, _, _, _, _, _ = _setup('per', batch, seed=41)
+  rng = np.random.default_rng(42)
+  host = replay_lib.SumTree()
+  host.set_all(rng.random(1000))
+  ta = torch.from_numpy(host.storage.copy()).to(device)
+  tb = ta.clone()
+  ma = torch.tensor([0.5], dtype=torch.float64, device=device)
+  mb = ma.clone()
+  w = torch.rand((batch,), device=device) + 0.5
+
+  def draw():
+    s = rng.integers(0, st.capacity, size=batch).astype(np.int32)
+    s[3] = s[17]  # a repeated draw
+    return torch.from_numpy(s).to(device)
+
+  for _ in range(3):
+    s = draw()
+    a.step(st, s, w)
+    _native.check(_native.lib().dqz_per_write_back(
+        a._h, _native.ptr(ta), host.capacity, _native.ptr(s), alpha,  # pylint: disable=protected-access
+        _native.ptr(ma), _native.stream_handle()))
+    b.step(st, s, w, write_back=(tb, host.capacity, s, alpha, mb))
+  torch.cuda.synchronize()
+  assert torch.equal(ta, tb) and torch.equal(ma, mb)
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(a, which), getattr(b, which))
+  s = draw()
+  g = torch.cuda.CUDAGraph()
+  side = torch.cuda.Stream(device)
+  side.wait_stream(torch.cuda.current_stream(device))
+  with torch.cuda.stream(side):
+    b.step(st, s, w, write_back=(tb, host.capacity, s, alpha, mb))
+  torch.cuda.current_stream(device).wait_stream(side)
+  a.step(st, s, w)
+  _native.check(_native.lib().dqz_per_write_back(
+      a._h, _native.ptr(ta), host.capacity, _native.ptr(s), alpha,  # pylint: disable=protected-access
+      _native.ptr(ma), _native.stream_handle()))
+  with torch.cuda.graph(g):
+    b.step(st, s, w, write_back=(tb, host.capacity, s, alpha, mb))
+  g.replay()
+  a.step(st, s, w)
+  _native.check(_native.lib().dqz_per_write_back(
+      a._h, _native.ptr(ta), host.capacity, _native.ptr(s), alpha,  # pylint: disable=protected-access
+      _native.ptr(ma), _native.stream_handle()))
+  torch.cuda.synchronize()
+  assert torch.equal(ta, tb) and torch.equal(ma, mb)
+  assert a.sync_status() == 0 and b.sync_status() == 0

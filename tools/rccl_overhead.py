@@ -20,6 +20,13 @@ import bench  # noqa: E402
 def main():
   dev = torch.device('cuda:0')
   torch.cuda.set_device(dev)
+  out = {}
+  before = len(sys.argv) > 1 and sys.argv[1] == 'before'
+  import torch.distributed as dist  # pylint: disable=g-import-not-at-top
+  os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+  os.environ.setdefault('MASTER_PORT', str(bench.free_port()))
+  if before:  # the group exists while the workload is built and captured
+    dist.init_process_group('nccl', rank=0, world_size=1)
   wl = bench.Workload('dqn', 1_000_000, 0, dev)
   side = torch.cuda.Stream(dev)
   side.wait_stream(torch.cuda.current_stream(dev))
@@ -41,12 +48,10 @@ def main():
     torch.cuda.synchronize()
     return 50 * reps / (time.perf_counter() - t0)
 
-  out = {}
-  out['no_group'] = (rate(), len(os.sched_getaffinity(0)))
-  os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-  os.environ.setdefault('MASTER_PORT', str(bench.free_port()))
-  import torch.distributed as dist  # pylint: disable=g-import-not-at-top
-  dist.init_process_group('nccl', rank=0, world_size=1)
+  out['mode'] = 'group before capture' if before else 'group after capture'
+  out['first'] = (rate(), len(os.sched_getaffinity(0)))
+  if not before:
+    dist.init_process_group('nccl', rank=0, world_size=1)
   out['after_init'] = (rate(), len(os.sched_getaffinity(0)))
   t = torch.ones((2,), device=dev)
   dist.all_reduce(t)

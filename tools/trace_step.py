@@ -17,6 +17,8 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 __graft_entry__._compile_lib(LIB, ['-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split()])  # pylint: disable=protected-access
 os.environ['DQZ_LIB'] = LIB
+from dqn_mgsc_zoo_amd import _native as _nat  # noqa: E402
+_nat.LIB_PATH = LIB  # imported by the build above, before DQZ_LIB was set
 import torch  # noqa: E402
 from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, synthetic  # noqa: E402
 
