@@ -357,14 +357,26 @@ def main(argv=None):
   return run_gpu(args, g, rem)
 
 
-def _timed(reps, runner, steps, g, rem, sync):
+def _barrier(reps):
+  mode = os.environ.get('DQZ_BENCH_BARRIER', 'barrier')  # diagnostic A/B only
+  if mode == 'none' or reps.dist is None:
+    return
+  if mode == 'allreduce':
+    t = torch.zeros((1,), device=torch.device('cuda', torch.cuda.current_device()))
+    reps.dist.all_reduce(t)
+    torch.cuda.synchronize()
+    return
   reps.barrier()
+
+
+def _timed(reps, runner, steps, g, rem, sync):
+  _barrier(reps)
   sync()
   t0 = time.perf_counter()
   n = runner.run(steps, g, rem)
   sync()
   elapsed = time.perf_counter() - t0
-  reps.barrier()
+  _barrier(reps)
   if n != steps:
     raise RuntimeError('timed %d steps, asked for %d' % (n, steps))
   return elapsed

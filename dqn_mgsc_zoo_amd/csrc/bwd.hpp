@@ -236,6 +236,7 @@ struct Conv3BwdArgs {
   float* part;       // [B][577][64]
   int B;
   Handoff sync;      // per-sample dy2 arrival counters (bwd_bc_kernel)
+  int* dwcnt;        // XCD-group dW reduce counters [8][4] (x Handoff::kStride), or null
 };
 
 // PUB: dy2 is handed to conv2 dX inside the same launch (bwd_bc_kernel): every
@@ -334,6 +335,68 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
   if constexpr (PUB) a.sync.arrive(b);
 }
 
+// XCD-group pre-reduction of per-sample dW partials.  A dW job of sample b
+// runs on XCD b % 8 (xcd_sample_job), so the jobs (b, job) of the samples
+// g, g + 8, ... (g = b % 8) share one L2.  After its own piece is stored
+// (plain stores: the lines stay in that L2) and drained, each job adds to
+// the (g, job) counter; the last of the group's n_g jobs to arrive reads the
+// n_g pieces back with sc1 loads (L1 bypassed, served by the shared L2; the
+// guide's last-arriver hand-off row) and writes their sum, in sample order,
+// over sample g's piece.  update_kernel then reduces min(8, B) slabs instead
+// of B: 8.9 MB -> 2.2 MB of partial reads at B = 32 for conv2 + conv3.
+// NV float4s per lane at byte offsets off[v] of the slab, plus (if nb > 0)
+// nb scalar bias values at float offsets boff[k] of the slab.
+template <int NV, int NB>
+__device__ __forceinline__ void dw_xcd_reduce(float* part, int64_t slab_floats, int b, int B, int* cnt,
+                                              const int (&off)[NV], int nb, const int (&boff)[NB]) {
+  __shared__ int s_last;
+  const int g = b & 7, ng = (B - g + 7) / 8;
+  if (ng <= 1) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+  __syncthreads();
+  if (!s_last) return;
+  const int bytes = (int)min((int64_t)INT32_MAX, (int64_t)B * slab_floats * 4);
+  const float4* base = reinterpret_cast<const float4*>(part);
+  f32x4 acc[NV];
+  float bacc[NB > 0 ? NB : 1];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NB; ++k) bacc[k] = 0.f;
+  for (int j = 0; j < ng; ++j) {  // sample order g, g + 8, ...
+    const int64_t sb = (int64_t)(g + 8 * j) * slab_floats;
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = load_sc1_f4(base, bytes, (int)((sb * 4 + off[v]) / 16));
+    float y[NB > 0 ? NB : 1];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (k < nb) y[k] = load_sc1_f1(part, bytes, (int)(sb + boff[k]));
+    if (j == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] = f32x4{x[v].x, x[v].y, x[v].z, x[v].w};
+#pragma unroll
+      for (int k = 0; k < NB; ++k) bacc[k] = k < nb ? y[k] : 0.f;
+    } else {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] += f32x4{x[v].x, x[v].y, x[v].z, x[v].w};
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+        if (k < nb) bacc[k] += y[k];
+    }
+  }
+  float* dst = part + (int64_t)g * slab_floats;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(dst) + off[v]) = acc[v];
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    if (k < nb) dst[boff[k]] = bacc[k];
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -395,6 +458,14 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
     sb += __shfl_xor(sb, 32, 64);
     if (kq == 0) part[C3KK * C3CO] = sb;
   }
+  if (a.dwcnt) {
+    int off[9];
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) off[tp] = ((tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) * 4;
+    const int boff[1] = {C3KK * C3CO + 16 * nq + n};
+    dw_xcd_reduce<9, 1>(a.part, (int64_t)(C3KK + 1) * C3CO, b, a.B,
+                        a.dwcnt + ((b & 7) * 4 + nq) * Handoff::kStride, off, (w == 0 && kq == 0) ? 1 : 0, boff);
+  }
 }
 
 // ---- conv2 backward: dX by stride phase and per-sample dW partials --------
@@ -418,6 +489,7 @@ struct Conv2BwdArgs {
   int B;
   Handoff sync;      // dy2 arrival counters (WAIT)
   Handoff sync1;     // dy1 arrival counters (PUB)
+  int* dwcnt;        // XCD-group dW reduce counters [8][8] (x Handoff::kStride), or null
 };
 
 // WAIT: dy2 of sample b is produced by the 8 conv3 dX jobs of the same launch
@@ -636,6 +708,18 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
       sb += __shfl_xor(sb, 32, 64);
       if (kq == 0) part[C2KK * C2CO + 16 * ct] = sb;
     }
+  }
+  if (a.dwcnt) {
+    int off[4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+        off[2 * mt + ct] = (((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq) * 4;
+    const int boff[2] = {C2KK * C2CO + 32 * ch + n, C2KK * C2CO + 32 * ch + 16 + n};
+    dw_xcd_reduce<4, 2>(a.part, (int64_t)(C2KK + 1) * C2CO, b, a.B,
+                        a.dwcnt + ((b & 7) * 8 + 2 * kh + ch) * Handoff::kStride, off,
+                        (kh == 0 && w == 0 && kq == 0) ? 2 : 0, boff);
   }
 }
 

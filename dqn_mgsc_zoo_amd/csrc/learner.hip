@@ -58,6 +58,7 @@ struct dqz_learner {
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
   float* fc1sum;  // [Z][B][512] fc1 pre-activations summed by fc1_fwd_kernel's last split block
   int32_t* fc1cnt;  // its tile arrival counters
+  int32_t* dwcnt;   // XCD-group dW reduce counters: conv3 [8][4], conv2 [8][8] (x Handoff::kStride)
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
@@ -69,9 +70,16 @@ struct dqz_learner {
 // block (the head then loads one pre-activation row per sample) instead of by
 // the head (DQZ_FC1_REDUCE=0).
 #ifndef DQZ_FC1_REDUCE
-#define DQZ_FC1_REDUCE 1
+#define DQZ_FC1_REDUCE 0
 #endif
 constexpr bool kFc1Reduce = DQZ_FC1_REDUCE != 0;
+
+// conv2 / conv3 dW partials pre-reduced per XCD group inside the backward
+// launch (bwd.hpp dw_xcd_reduce), so update_kernel reads min(8, B) slabs.
+#ifndef DQZ_DW_XCD
+#define DQZ_DW_XCD 1
+#endif
+constexpr bool kDwXcd = DQZ_DW_XCD != 0;
 
 static int g_attr_done = 0;
 
@@ -125,11 +133,12 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
                            n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
-                           (int64_t)Z_MAX_FC1 * MAXB * HID, (int64_t)Z_MAX_FC1 * (MAXB / 32) * (HID / 16) * Handoff::kStride};
+                           (int64_t)Z_MAX_FC1 * MAXB * HID, (int64_t)Z_MAX_FC1 * (MAXB / 32) * (HID / 16) * Handoff::kStride,
+                           (int64_t)(8 * 4 + 8 * 8) * Handoff::kStride};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p,
-                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt)};
+                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt), reinterpret_cast<float**>(&L->dwcnt)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -371,6 +380,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.w3p = L->w3p;
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
+  c3b.dwcnt = kDwXcd ? L->dwcnt : nullptr;
   c3b.B = B;
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
@@ -383,6 +393,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.w2p = L->w2p;
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
+  c2b.dwcnt = kDwXcd ? L->dwcnt + 8 * 4 * Handoff::kStride : nullptr;
   c2b.B = B;
   c2b.sync = c3b.sync;
   Conv1DwArgs c1dw;
@@ -419,8 +430,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.p2 = L->p2;
   u.p3 = L->p3;
   u.S1 = B * C1_BLOCKS;
-  u.S2 = B;
-  u.S3 = B;
+  u.S2 = kDwXcd ? min(8, B) : B;  // XCD-group sums in slabs 0..7
+  u.S3 = kDwXcd ? min(8, B) : B;
   u.h1 = L->h1;
   u.dz1 = L->dz1;
   u.gq = L->gq;

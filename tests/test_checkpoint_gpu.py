@@ -172,3 +172,34 @@ def test_reservoir_store_holds_last_write_per_slot(device):
     assert float(g.r_t) == np.float32(want.r_t)
     assert float(g.discount_t) == np.float32(want.discount_t)
   assert torch.isfinite(agent.learner.online).all()
+
+
+@pytest.mark.parametrize('kind', ['dqn', 'per', 'mgsc_fifo', 'mgsc_reservoir'])
+def test_checkpoint_does_not_perturb_the_saver(device, tmp_path, kind):
+  """Saving is observation-free: two agents with the same seed
+  run the same 100 frames; one of them is checkpointed through
+  parts.Checkpoint; over the next 60 frames both act, learn and (MGSC)
+  sample / meta-update identically, bit for bit — the learned-logit
+  buffer's running log-sum-exp is read out, not invalidated, by get_state
+  (replay_circular.CircularLogitBuffer.get_state)."""
+  from dqn_mgsc_zoo_amd import parts
+  a1, r1 = _agent(kind, seed=4)
+  a2, r2 = _agent(kind, seed=4)
+  first = _timesteps(100, 5, 19)
+  assert _drive(a1, first) == _drive(a2, first)
+  ck = parts.Checkpoint(str(tmp_path / 'saver.chkpt'))
+  ck.state.train_agent = a1
+  ck.save()
+  more = _timesteps(60, 6, 17)
+  assert _drive(a1, more) == _drive(a2, more)
+  for which in ('online', 'target', 'mu', 'nu'):
+    assert torch.equal(getattr(a1.learner, which), getattr(a2.learner, which)), which
+  if kind.startswith('mgsc'):
+    d1, d2 = r1.device_logits, r2.device_logits
+    assert torch.equal(d1.logits, d2.logits)
+    assert d1.run_state() == d2.run_state()
+    assert d1.run_state()['known'] == 1  # nothing forced a re-scan
+    m1, m2 = a1.meta_learner.get_state(), a2.meta_learner.get_state()
+    np.testing.assert_array_equal(m1['mu'], m2['mu'])
+  if kind == 'per':
+    assert a1.max_seen_priority == a2.max_seen_priority

@@ -9,8 +9,9 @@ C transitions:
                   fp64 sum tree (alpha-exponentiated random priorities, usp
                   1e-3, beta 0.4, normalised weights) + double-Q learner step
                   with IS weights + |td|^alpha priority write-back (hipGraph)
-  mgsc_learn      MGSC config (2) learner part: softmax sample over C logits
-                  (N(0,1), Philox uniforms) + DQN learner step (hipGraph)
+  mgsc_learn      MGSC config (3) learner part: one-launch softmax sample over
+                  C logits (N(0,1), Philox uniforms, int32 slots) + DQN
+                  learner step (hipGraph)
   mgsc_meta_*     one meta_update (M = 100 and M = 300, first / second
                   order) on a fixed meta batch (stream-timed, not captured)
 Times are device time from HIP events around K steps on one stream.
@@ -108,9 +109,8 @@ def main():
         _native.ptr(tree), tcap, 0, cap, cap, B, ctypes.c_double(1e-3), ctypes.c_double(0.4), 1, 11,
         _native.ptr(p_ctr), None, None, None, None, _native.ptr(p_slots), _native.ptr(p_w), None,
         _native.stream_handle()))
-    lrn_p.step(store, p_slots, p_w)
-    _native.check(lib.dqz_per_write_back(lrn_p._h, _native.ptr(tree), tcap, _native.ptr(p_slots),  # pylint: disable=protected-access
-                                         ctypes.c_double(0.6), _native.ptr(max_seen), _native.stream_handle()))
+    # write-back folded into the backward launch (dqz_learner_step_per)
+    lrn_p.step(store, p_slots, p_w, write_back=(tree, tcap, p_slots, 0.6, max_seen))
   print('per_double ...', file=sys.stderr, flush=True)
   out['per_double'] = timed(per_step, args.steps, 20, dev, graph_steps=50)
 
@@ -118,20 +118,15 @@ def main():
   net = networks.dqn_atari_network(A)
   lrn = learner_lib.Learner(net, B, algo='dqn', device=dev)
   lrn.set_params(net.init(seed=3))
-  logits = torch.from_numpy(rng.standard_normal(cap).astype(np.float32)).to(dev)
-  lb = ctypes.c_void_p()
-  _native.check(lib.dqz_logit_buffer_create(cap, B, ctypes.byref(lb)))
-  uni = torch.zeros((B,), dtype=torch.float64, device=dev)
+  from dqn_mgsc_zoo_amd import replay_circular as rc  # pylint: disable=g-import-not-at-top
+  lbuf = rc._DeviceLogits(cap, dev, max_queries=B)  # pylint: disable=protected-access
+  lbuf.load(rng.standard_normal(cap).astype(np.float32))
+  logits = lbuf.logits
   u_ctr = torch.zeros((1,), dtype=torch.int64, device=dev)
-  m_idx = torch.zeros((B,), dtype=torch.int64, device=dev)
   m_slots = torch.zeros((B,), dtype=torch.int32, device=dev)
 
   def mgsc_learn():
-    _native.check(lib.dqz_uniform_philox(13, _native.ptr(u_ctr), B, _native.ptr(uni),
-                                         _native.stream_handle()))
-    _native.check(lib.dqz_logits_sample(lb, _native.ptr(logits), _native.ptr(uni), B, _native.ptr(m_idx),
-                                        _native.stream_handle()))
-    m_slots.copy_(m_idx)
+    lbuf.sample_slots_philox(13, u_ctr, m_slots)  # one launch: draws + choice + int32 slots
     lrn.step(store, m_slots)
   print('mgsc_learn ...', file=sys.stderr, flush=True)
   out['mgsc_learn'] = timed(mgsc_learn, args.steps, 20, dev, graph_steps=50)
@@ -146,11 +141,10 @@ def main():
       meta.set_online_transition(ot)
       ms = torch.from_numpy(rng.choice(cap, m_batch, replace=False).astype(np.int32)).to(dev)
       mp = ms.clone()
-      t = timed(lambda: meta.update(store, ms, logits, mp), max(20, args.steps // 20), 3, dev)
+      t = timed(lambda: meta.update(store, ms, logits, mp, logit_buffer=lbuf), max(20, args.steps // 20), 3, dev)
       out['mgsc_meta_M%d_%s' % (m_batch, 'second' if order else 'first')] = t
       print('mgsc_meta M=%d order=%d %s' % (m_batch, order, t), file=sys.stderr, flush=True)
       del meta
-  _native.check(lib.dqz_logit_buffer_destroy(lb))
   print(json.dumps(out))
 
 
