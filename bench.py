@@ -603,14 +603,27 @@ def run_gpu(args, g, rem):
   pending = []
   clock = {'t0': time.perf_counter()}
 
+  stats_mode = os.environ.get('DQZ_BENCH_STATS', 'sync')  # diagnostic A/B: sync | async
+
   def on_stats(done):
     lrn.fetch_outputs()
     stats_vec[0].fill_(float(done))
     stats_vec[1].copy_(lrn.loss[0])
     stats_vec[2].fill_(time.perf_counter() - clock['t0'])
-    if reps.dist is not None:
+    if reps.dist is None:
+      return
+    if stats_mode == 'async':
       pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
                                                       async_op=True))
+      return
+    # Drain the learner's queue first, then gather on an idle device: an
+    # async gather enqueued behind the replayed graphs cost ~7 ms each
+    # (13,200 against 14,630 steps/s over 20,000 steps, tools/ab_rccl.sh);
+    # draining costs one pipeline refill per stats interval.
+    torch.cuda.synchronize(dev)
+    pending.append(reps.dist.all_gather_into_tensor(gathered, stats_vec,
+                                                    async_op=True))
+    pending[-1].wait()
 
   runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
                       args.stats_every, on_stats)

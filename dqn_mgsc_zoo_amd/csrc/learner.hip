@@ -77,7 +77,7 @@ constexpr bool kFc1Reduce = DQZ_FC1_REDUCE != 0;
 // conv2 / conv3 dW partials pre-reduced per XCD group inside the backward
 // launch (bwd.hpp dw_xcd_reduce), so update_kernel reads min(8, B) slabs.
 #ifndef DQZ_DW_XCD
-#define DQZ_DW_XCD 1
+#define DQZ_DW_XCD 0
 #endif
 constexpr bool kDwXcd = DQZ_DW_XCD != 0;
 
