@@ -517,14 +517,15 @@ class Workload:
       lb.logits.copy_(torch.randn((capacity,), generator=gen, device=dev))
       lb.invalidate()
 
-      def mgsc_sample():
-        lb.sample_slots_philox(seed, counter, slots)
+      self.sampler_counter = sc = torch.zeros((1,), dtype=torch.int64, device=dev)
+
+      def mgsc_sample():  # the stand-alone one-launch sampler, timed for reference
+        lb.sample_slots_philox(seed, sc, slots)
 
       def one_step():
-        mgsc_sample()
-        lrn.step(store, slots)
-      self.samplers = {'logits_sample': mgsc_sample}
-      self.sampler_bytes = {'logits_sample': 4 * capacity}
+        # the draw runs inside the learner's forward launch
+        lrn.step_logits(store, lb, slots, seed=seed, counter=counter)
+      self.samplers = {'logits_sample_standalone': mgsc_sample}
     else:
       raise ValueError(algo)
     self.one_step = one_step

@@ -131,6 +131,10 @@ SIGNATURES = {
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
          _vp, _i64, _vp, ctypes.c_double, _vp, _vp]),
+    'dqz_learner_step_logits': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
+         ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     'dqz_learner_grad': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,

@@ -10,6 +10,7 @@
 // ds_read_b32 at compile-time immediate offsets.  Stacks never exist in HBM.
 #pragma once
 #include "common.hpp"
+#include "sampling.hpp"
 
 namespace dqz {
 
@@ -18,8 +19,10 @@ struct Conv1Src {
   const int32_t* fidx;    // [capacity][8]
   const int32_t* slots;   // [B]
   const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
-  int fused;              // 1: slots come from the fused uniform sampler `draw`
+  int fused;              // 1: slots come from the fused uniform sampler `draw`;
+                          // 2: from the fused learned-logit draw `sm`
   UniformDraw draw;
+  SoftmaxDraw sm;
   // Batch record: block (rb 0, z 0) of sample b also copies action / reward /
   // discount of its slot into rec[b] = {a as int bits, r, d, 0}, so the head
   // reads one record per sample instead of the slot -> record chain.
@@ -117,9 +120,12 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
     // slot -> 4 frame ids -> 504 16-byte pieces (2 per thread), all loads in
     // flight before the first LDS store.
     int slot;
-    if (src.fused) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
+    if (src.fused == 1) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
       slot = uniform_slot(*src.draw.counter, b, src.draw);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.draw.slots_out[b] = slot;
+    } else if (src.fused == 2) {  // fused learned-logit draw (every block of b runs the search)
+      slot = softmax_draw_slot(src.sm, b);
+      if (threadIdx.x == 0 && rb == 0 && z == 0) src.sm.slots_out[b] = slot;
     } else {
       slot = src.slots[b];
     }

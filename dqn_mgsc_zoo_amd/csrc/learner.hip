@@ -246,8 +246,9 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
     c2.wait = c1.pub;
     c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, 4, 4};
     c3.wait = c2.pub;
-    DQZ_PHASE(0, hipLaunchKernelGGL(fwd_conv_kernel, dim3(3 * xcd_grid(4, Z * B).x), dim3(256), kConv1FwdSmem, st, c1,
-                                    c2, c3);
+    const unsigned npro = src.fused == 2 ? (unsigned)((src.sm.nblocks + 7) / 8 * 8) : 0u;
+    DQZ_PHASE(0, hipLaunchKernelGGL(fwd_conv_kernel, dim3(npro + 3 * xcd_grid(4, Z * B).x), dim3(256), kConv1FwdSmem,
+                                    st, c1, c2, c3);
               DQZ_HIP(hipGetLastError()));
     if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
   } else {
@@ -299,7 +300,7 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
-                     int gacc = 0, const PerWbArgs* wb = nullptr) {
+                     int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -318,10 +319,18 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   src.reward = S->reward;
   src.discount = S->discount;
   src.rec = reinterpret_cast<float4*>(L->rec);
-  if (draw) {  // conv1 draws the batch itself; later kernels read the published slots
+  if (draw || sm) {  // conv1 draws the batch itself; later kernels read the published slots
     Conv1Src fsrc = src;
-    fsrc.fused = 1;
-    fsrc.draw = *draw;
+    if (draw) {
+      fsrc.fused = 1;
+      fsrc.draw = *draw;
+    } else {
+      fsrc.fused = 2;
+      fsrc.sm = *sm;
+      // the draw's hand-off word and error word live with the learner's
+      fsrc.sm.sync = Handoff{L->sync + (16 * B + 1) * Handoff::kStride, L->sync + (16 * B + 2) * Handoff::kStride,
+                             L->sync + 16 * B * Handoff::kStride, sm->nblocks, C1_BLOCKS * Z * B, L->spin_max};
+    }
     if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, true)) return rc;
   } else {
     if (int rc = forward_impl(L, nz, Z, B, src, st, pe, true)) return rc;
@@ -344,7 +353,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
   h.meta_p = meta_p;
   h.rec = reinterpret_cast<const float4*>(L->rec);
-  h.advance = draw ? draw->counter : nullptr;
+  h.advance = draw ? draw->counter : sm ? sm->counter : nullptr;  // null with injected uniforms
   h.unit = unit;
   h.bound = L->cfg.grad_error_bound;
   h.td = L->td;
@@ -858,6 +867,20 @@ int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, flo
   DQZ_HIP(hipGetLastError());
   if (lse_out) DQZ_HIP(hipMemcpyAsync(lse_out, b->lse, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
+}
+
+int dqz_learner_step_logits(dqz_learner* L, const dqz_params* P, const dqz_store* S, dqz_logit_buffer* buf,
+                            const float* logits, uint64_t seed, uint64_t* counter_dev, const double* uniforms,
+                            int32_t* slots_out, void* stream) {
+  if (!L || !buf || !logits || (!counter_dev && !uniforms) || !slots_out)
+    return fail(DQZ_ERR_INVALID, "null argument");
+  if (L->cfg.algo == DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "PER samples by priority, not by learned logits");
+  if (buf->capacity > INT32_MAX) return fail(DQZ_ERR_INVALID, "int32 slots need capacity < 2^31");
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = ensure_run(buf, logits, st)) return rc;
+  SoftmaxDraw sm{logits,      buf->capacity, buf->run, buf->bsum, buf->nblocks, Handoff{}, seed,
+                 uniforms ? nullptr : counter_dev, uniforms, slots_out};
+  return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0, nullptr, &sm);
 }
 
 int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream) {

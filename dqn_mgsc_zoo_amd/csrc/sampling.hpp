@@ -486,6 +486,49 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
   return s_out;
 }
 
+// The learned-logit draw fused into the learner's forward launch
+// (dqz_learner_step_logits): fwd_conv_kernel gets `nblocks` producer blocks
+// in front (chunk_prob_sum, as softmax_sample_kernel's producers) and every
+// conv1 block of sample b waits for their arrivals, draws uniform b of step
+// *counter (the dqz_uniform_philox stream) and runs the CDF search itself
+// before its frame gather.  The head advances *counter once every conv1
+// block has read it.
+struct SoftmaxDraw {
+  const float* x;        // logits [n]
+  int64_t n;
+  const LogitRun* run;
+  double* bsum;          // [nblocks] chunk sums (written by the producers)
+  int nblocks;
+  Handoff sync;          // one word: need = nblocks, consumers = the conv1 blocks
+  uint64_t seed;
+  uint64_t* counter;     // Philox step counter (null when `uniforms` is set)
+  const double* uniforms;  // the caller's uniforms [B] (a host Generator's draws), or null
+  int32_t* slots_out;    // [B]: block (rb 0, z 0) of sample b publishes its slot
+};
+
+__device__ __forceinline__ void softmax_draw_produce(const SoftmaxDraw& d, int blk) {
+  __shared__ double dbuf[SM_THREADS / 64];
+  const float L = sample_lse(d.x, d.n, d.run);
+  const double acc = chunk_prob_sum(d.x, d.n, blk, L, nullptr, dbuf);
+  if (threadIdx.x == 0) __hip_atomic_store(d.bsum + blk, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  d.sync.arrive(0);
+}
+
+__device__ __forceinline__ int32_t softmax_draw_slot(const SoftmaxDraw& d, int b) {
+  double u;
+  if (d.uniforms) {
+    u = d.uniforms[b];
+  } else {
+    const uint64_t ctr = *d.counter;
+    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)b, 0x50F7u),
+                               make_uint2((unsigned)d.seed, (unsigned)(d.seed >> 32)));
+    u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+  }
+  const float L = sample_lse(d.x, d.n, d.run);
+  d.sync.wait(0);
+  return (int32_t)softmax_choice_body(d.x, d.n, L, d.bsum, d.nblocks, u);
+}
+
 // Learned-logit batch draw in one launch (replay_circular.py:205-217,
 // 540-545: Generator.choice(C, n, p=softmax(logits))).  Blocks [0, nb) are
 // producers: chunk b's float64 sum of p, stored agent-scope, then an arrival

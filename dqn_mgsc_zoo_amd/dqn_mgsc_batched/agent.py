@@ -13,6 +13,8 @@ logit buffer and are updated in place (update_priorities, agent.py:334).
 
 from typing import Any, Mapping
 
+import numpy as np
+
 from dqn_mgsc_zoo_amd import agent_base
 from dqn_mgsc_zoo_amd import learner as learner_lib
 
@@ -91,9 +93,19 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
     self._meta.update(self._store(), slots, dl.logits, pos, logit_buffer=dl)
 
   def _learn(self) -> None:
-    """agent.py:341-360: softmax(logits)-sampled batch, DQN update."""
-    slots = self._replay.sample_slots(self._batch_size)
-    self._learner.step(self._store(), slots)
+    """agent.py:341-360: softmax(logits)-sampled batch, DQN update — one
+    call: the replay Generator's uniforms are resolved into slots inside the
+    learner's forward launch (Learner.step_logits)."""
+    import torch  # pylint: disable=g-import-not-at-top
+    u = self._replay.draw_uniforms(self._batch_size)
+    dev = self._learner.device
+    if self._slots_cache is None:
+      self._slots_cache = (torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
+                           torch.zeros((self._batch_size,), dtype=torch.float64, device=dev))
+    slots, u_dev = self._slots_cache
+    u_dev.copy_(torch.from_numpy(np.asarray(u, np.float64)))
+    self._learner.step_logits(self._store(), self._replay.device_logits, slots,
+                              uniforms=u_dev)
 
   @property
   def meta_learner(self) -> learner_lib.MetaLearner:

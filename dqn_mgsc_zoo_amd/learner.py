@@ -144,6 +144,23 @@ class Learner:
         int(size), int(capacity), int(seed) & (2**64 - 1), _native.ptr(counter),
         _native.ptr(slots_out), _native.stream_handle(stream)))
 
+  def step_logits(self, store, logit_buffer, slots_out, seed=0, counter=None,
+                  uniforms=None, stream=None):
+    """Learned-logit sample + learner step, the draw inside the forward
+    launch (dqz_learner_step_logits): draws what
+    logit_buffer.sample_slots_philox(seed, counter, slots_out) — or, given
+    device f64 `uniforms` [B] (a Generator's draws), sample_abs(uniforms) —
+    would, writes them to `slots_out` and (Philox) advances `counter`."""
+    if slots_out.dtype != torch.int32 or slots_out.numel() != self.batch_size:
+      raise ValueError('slots_out must be a device int32 tensor of batch size')
+    if (counter is None) == (uniforms is None):
+      raise ValueError('pass exactly one of counter (Philox) and uniforms')
+    _native.check(_native.lib().dqz_learner_step_logits(
+        self._h, ctypes.byref(self._params_c), store.c_ref(),
+        logit_buffer.handle, _native.ptr(logit_buffer.logits),
+        int(seed) & (2**64 - 1), _native.ptr(counter), _native.ptr(uniforms),
+        _native.ptr(slots_out), _native.stream_handle(stream)))
+
   def grad(self, store, slots, weights=None, out=None, stream=None):
     """jax.grad(loss_fn) of the same step into a flat tensor (no update)."""
     if slots.dtype != torch.int32 or slots.numel() != self.batch_size:

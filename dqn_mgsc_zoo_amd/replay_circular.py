@@ -245,12 +245,17 @@ class CircularLogitBuffer:
     t = self._dev.logits
     return (t - self._dev._torch.logsumexp(t, 0)).exp()  # pylint: disable=protected-access
 
-  def sample_slots(self, size: int):
-    """Absolute slots (device int64), drawn like Generator.choice(p=softmax)."""
+  def draw_uniforms(self, size: int) -> np.ndarray:
+    """The Generator draws sample(size) consumes (same checks), for a caller
+    that resolves them on device itself (Learner.step_logits)."""
     if self._size < size:
       raise BufferError('Cannot sample from buffer with length %d when '
                         'requested sample size was %d.' % (self._size, size))
-    return self._dev.sample_abs(self._rng_state.random(size))
+    return self._rng_state.random(size)
+
+  def sample_slots(self, size: int):
+    """Absolute slots (device int64), drawn like Generator.choice(p=softmax)."""
+    return self._dev.sample_abs(self.draw_uniforms(size))
 
   def sample(self, size: int) -> np.ndarray:
     """Relative indices, as the reference returns them."""
@@ -466,6 +471,11 @@ class MGSCFiFoTransitionReplay:
   def device_logits(self):
     return self._distribution.device_logits
 
+  def draw_uniforms(self, size: int):
+    """Host Generator draws of sample(size), resolved on device by
+    Learner.step_logits (absolute slots = item slots)."""
+    return self._distribution.draw_uniforms(size)
+
   @property
   def size(self) -> int:
     return self._ring.size
@@ -547,11 +557,14 @@ class MGSCReservoirDistribution:
     t = self._dev.logits
     return (t - self._dev._torch.logsumexp(t, 0)).exp()  # pylint: disable=protected-access
 
-  def sample_slots(self, size: int):
+  def draw_uniforms(self, size: int) -> np.ndarray:
     if self._size < size:
       raise BufferError('Cannot sample a batch of size %d from buffer with '
                         'size %d.' % (size, self._size))
-    return self._dev.sample_abs(self._rng_state.random(size))
+    return self._rng_state.random(size)
+
+  def sample_slots(self, size: int):
+    return self._dev.sample_abs(self.draw_uniforms(size))
 
   def sample(self, size: int) -> np.ndarray:
     return self.sample_slots(size).cpu().numpy()
@@ -641,6 +654,11 @@ class MGSCReservoirTransitionReplay:
   @property
   def device_logits(self):
     return self._distribution.device_logits
+
+  def draw_uniforms(self, size: int):
+    """Host Generator draws of sample(size), resolved on device by
+    Learner.step_logits (absolute slots = item slots)."""
+    return self._distribution.draw_uniforms(size)
 
   @property
   def size(self) -> int:

@@ -145,6 +145,21 @@ int dqz_learner_step_per(dqz_learner* learner, const dqz_params* params, const d
                          const int32_t* slots, const float* is_weights, double* tree, int64_t cap,
                          const int32_t* indices, double alpha, double* max_seen_dev, void* stream);
 
+/* MGSC learner step with the batch drawn inside the learner's forward
+ * launch (dqn_mgsc_batched/agent.py:341-360: replay.sample(batch) from
+ * softmax(logits), then the DQN update): the draw is exactly
+ * dqz_logits_sample_slots(buf, logits, seed, counter_dev, NULL, B,
+ * slots_out, ...) — Philox uniform b of step *counter_dev (or uniforms[b]
+ * when `uniforms`, device f64 [B], is given: the replay Generator's own
+ * draws), the CDF search of dqz_logits_sample — computed by the forward's
+ * conv1 workgroups behind in-launch producer blocks (no sampler launch);
+ * slots_out (device int32 [B]) receives the slots and *counter_dev advances
+ * by one (Philox mode).  buf / logits: the replay's learned-logit buffer. */
+typedef struct dqz_logit_buffer dqz_logit_buffer;
+int dqz_learner_step_logits(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                            dqz_logit_buffer* buf, const float* logits, uint64_t seed, uint64_t* counter_dev,
+                            const double* uniforms, int32_t* slots_out, void* stream);
+
 /* Gradient only: d loss / d params of the same step into grad_out (device
  * f32, dqz_param_layout order, padding untouched); params->online / mu / nu
  * are not modified and mu / nu may be NULL.  = jax.grad(loss_fn) at
@@ -263,7 +278,6 @@ int dqz_gather_stacks(const dqz_store* store, const int32_t* slots, int n, int w
  * logits: device f32 [capacity], -inf marks an empty slot
  * (CircularLogitBuffer / MGSCReservoirDistribution, replay_circular.py:148-248,
  * 500-565).  A dqz_logit_buffer owns only the reduction scratch. */
-typedef struct dqz_logit_buffer dqz_logit_buffer;
 int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out);
 int dqz_logit_buffer_destroy(dqz_logit_buffer* buf);
 

@@ -409,3 +409,57 @@ def test_fused_per_write_back_equals_the_separate_launch(device):
   torch.cuda.synchronize()
   assert torch.equal(ta, tb) and torch.equal(ma, mb)
   assert a.sync_status() == 0 and b.sync_status() == 0
+
+
+def test_fused_logit_draw_step_equals_sampler_then_step(device):
+  """dqz_learner_step_logits (the learned-logit draw inside the forward
+  launch) == dqz_logits_sample_slots / dqz_logits_sample + dqz_learner_step,
+  bit for bit: slots, counter, parameters — Philox draws, the caller's
+  uniforms, and under hipGraph replay (the in-launch words reset)."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  batch = 32
+  _, a, st, _, _, _, _, _ = _setup('dqn', batch, seed=51)
+  _, b, _, _, _, _, _, _ = _setup('dqn', batch, seed=51)
+  rng = np.random.default_rng(52)
+  logits = rng.standard_normal(st.capacity).astype(np.float32)
+  logits[rng.integers(0, st.capacity, 20)] = -np.inf
+  dl = rc._DeviceLogits(st.capacity, device, max_queries=batch)  # pylint: disable=protected-access
+  dl.load(logits)
+  ca = torch.zeros((1,), dtype=torch.int64, device=device)
+  cb = torch.zeros((1,), dtype=torch.int64, device=device)
+  sa = torch.zeros((batch,), dtype=torch.int32, device=device)
+  sb = torch.zeros((batch,), dtype=torch.int32, device=device)
+  for _ in range(3):
+    dl.sample_slots_philox(9, ca, sa)
+    a.step(st, sa)
+    b.step_logits(st, dl, sb, seed=9, counter=cb)
+    torch.cuda.synchronize()
+    assert torch.equal(sa, sb)
+  assert int(ca.item()) == int(cb.item()) == 3
+  for _ in range(2):  # the replay Generator's own uniforms
+    u = rng.random(batch)
+    sa.copy_(dl.sample_abs(u).to(torch.int32))
+    a.step(st, sa)
+    b.step_logits(st, dl, sb, uniforms=torch.from_numpy(u).to(device))
+    torch.cuda.synchronize()
+    assert torch.equal(sa, sb)
+  side = torch.cuda.Stream(device)
+  side.wait_stream(torch.cuda.current_stream(device))
+  with torch.cuda.stream(side):
+    b.step_logits(st, dl, sb, seed=9, counter=cb)
+  torch.cuda.current_stream(device).wait_stream(side)
+  dl.sample_slots_philox(9, ca, sa)
+  a.step(st, sa)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    for _ in range(3):
+      b.step_logits(st, dl, sb, seed=9, counter=cb)
+  g.replay()
+  for _ in range(3):
+    dl.sample_slots_philox(9, ca, sa)
+    a.step(st, sa)
+  torch.cuda.synchronize()
+  assert torch.equal(sa, sb) and int(ca.item()) == int(cb.item())
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(a, which), getattr(b, which)), which
+  assert a.sync_status() == 0 and b.sync_status() == 0
