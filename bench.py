@@ -489,25 +489,32 @@ class Workload:
       self.weights = w = torch.zeros((BATCH,), dtype=torch.float32, device=dev)
       self.max_seen = max_seen = torch.ones((1,), dtype=torch.float64, device=dev)
 
-      def per_sample():
-        _native.check(lib.dqz_per_sample(
-            ptr(tree), tcap, 0, capacity, capacity, BATCH, PER_USP, PER_BETA,
-            1, seed, ptr(counter), None, None, None, None, ptr(slots), ptr(w),
-            None, stream()))
-
       def per_write_back():
         _native.check(lib.dqz_per_write_back(
             lrn._h, ptr(tree), tcap, ptr(slots), PER_ALPHA, ptr(max_seen),  # pylint: disable=protected-access
             stream()))
 
+      self.per_idx = idx = torch.zeros((BATCH,), dtype=torch.int32, device=dev)
+      self.per_probs = probs = torch.zeros((BATCH,), dtype=torch.float64, device=dev)
+      self.draw = _native.DqzPerDraw(
+          tree.data_ptr(), tcap, 0, capacity, capacity, PER_USP, PER_BETA, 1,
+          seed, counter.data_ptr(), None, None, None, PER_ALPHA,
+          max_seen.data_ptr(), idx.data_ptr(), slots.data_ptr(),
+          probs.data_ptr(), w.data_ptr())
+      self.sampler_counter = sc = torch.zeros((1,), dtype=torch.int64, device=dev)
+
+      def per_sample_standalone():
+        _native.check(lib.dqz_per_sample(
+            ptr(tree), tcap, 0, capacity, capacity, BATCH, PER_USP, PER_BETA,
+            1, seed, ptr(sc), None, None, None, None, ptr(slots), ptr(w),
+            None, stream()))
+
       def one_step():
-        # the |td|^alpha write-back runs inside the learner's backward launch
-        per_sample()
-        lrn.step(store, slots, w,
-                 write_back=(tree, tcap, slots, PER_ALPHA, max_seen))
-      # per_write_back is timed as a stand-alone launch for reference only:
-      # the step runs it inside the backward launch
-      self.samplers = {'per_sample': per_sample,
+        # one call: the draw in the forward's conv1 workgroups, the IS
+        # weights in the head, the |td|^alpha write-back in the backward
+        lrn.step_per_draw(store, self.draw)
+      # the stand-alone sampler and write-back launches, timed for reference
+      self.samplers = {'per_sample_standalone': per_sample_standalone,
                        'per_write_back_standalone': per_write_back}
     elif algo == 'mgsc':
       from dqn_mgsc_zoo_amd import replay_circular as rc  # pylint: disable=g-import-not-at-top
@@ -586,15 +593,17 @@ def run_gpu(args, g, rem):
           for _ in range(k):
             one_step()
 
-  # The RCCL group (replicas only, no gradient exchange) is formed after the
-  # graphs are captured: formed before, its mere existence slowed every
-  # replayed step by ~9 % (14,381 vs 15,775 steps/s, tools/ab_group.sh;
-  # tools/rccl_overhead.py times both orders).
+  # The RCCL group (replicas only, no gradient exchange).  Its communicator
+  # is created by the first collective, here, before the warm-up steps: the
+  # first graph replays after communicator creation are slow, and with the
+  # driver's --steps 20 that one-off cost landed inside the timed region
+  # (13,980 against 15,555 steps/s at 5,000 steps).
   reps = replicas_lib.Replicas('nccl')
   world = reps.world
   if world != args.gpus or reps.rank != rank:
     print('bench.py: world %d != --gpus %d' % (world, args.gpus), file=sys.stderr)
     return 2
+  _barrier(reps)
 
   # Statistics vector [steps done, last loss, seconds since the timed region
   # began], all-gathered over RCCL every stats_every steps: enqueued on the
@@ -629,8 +638,8 @@ def run_gpu(args, g, rem):
   runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
                       args.stats_every, on_stats)
   runner.run(args.warmup, 1, 0)
-  for k in graphs:  # first replay of each graph uploads it: keep it untimed
-    runner.run(k, k, 0)
+  for k in graphs:  # first replays of each graph upload it: keep them untimed
+    runner.run(2 * k, k, 0)
   warm_steps = runner.done
   pending.clear()  # warm-up gathers are not reported
   torch.cuda.synchronize(dev)

@@ -102,6 +102,30 @@ class DqzTransitionPut(ctypes.Structure):
   ]
 
 
+class DqzPerDraw(ctypes.Structure):
+  _fields_ = [
+      ('tree', ctypes.c_void_p),
+      ('cap', ctypes.c_int64),
+      ('live_base', ctypes.c_int64),
+      ('size', ctypes.c_int64),
+      ('capacity', ctypes.c_int64),
+      ('uniform_sample_probability', ctypes.c_double),
+      ('importance_sampling_exponent', ctypes.c_double),
+      ('normalize_weights', ctypes.c_int),
+      ('seed', ctypes.c_uint64),
+      ('counter_dev', ctypes.c_void_p),
+      ('injected_uniform', ctypes.c_void_p),
+      ('injected_u', ctypes.c_void_p),
+      ('index_to_slot', ctypes.c_void_p),
+      ('alpha', ctypes.c_double),
+      ('max_seen_dev', ctypes.c_void_p),
+      ('out_indices', ctypes.c_void_p),
+      ('out_slots', ctypes.c_void_p),
+      ('out_probs', ctypes.c_void_p),
+      ('out_weights', ctypes.c_void_p),
+  ]
+
+
 # name -> (restype, argtypes); must match include/dqz.h exactly.
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -135,6 +159,10 @@ SIGNATURES = {
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,
          ctypes.c_uint64, _vp, _vp, _vp, _vp]),
+    'dqz_learner_step_per_draw': (
+        _int,
+        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore),
+         ctypes.POINTER(DqzPerDraw), _vp]),
     'dqz_learner_grad': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,

@@ -20,9 +20,11 @@ struct Conv1Src {
   const int32_t* slots;   // [B]
   const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
   int fused;              // 1: slots come from the fused uniform sampler `draw`;
-                          // 2: from the fused learned-logit draw `sm`
+                          // 2: from the fused learned-logit draw `sm`;
+                          // 3: from the fused prioritized draw `per`
   UniformDraw draw;
   SoftmaxDraw sm;
+  PerSampleArgs per;
   // Batch record: block (rb 0, z 0) of sample b also copies action / reward /
   // discount of its slot into rec[b] = {a as int bits, r, d, 0}, so the head
   // reads one record per sample instead of the slot -> record chain.
@@ -126,6 +128,8 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
     } else if (src.fused == 2) {  // fused learned-logit draw (every block of b runs the search)
       slot = softmax_draw_slot(src.sm, b);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.sm.slots_out[b] = slot;
+    } else if (src.fused == 3) {  // fused prioritized draw (the tree top staged in s_in first)
+      slot = per_draw_slot(src.per, b, reinterpret_cast<double*>(s_in), rb == 0 && z == 0);
     } else {
       slot = src.slots[b];
     }

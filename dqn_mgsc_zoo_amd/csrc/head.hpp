@@ -17,6 +17,13 @@ struct HeadArgs {
   const float* reward;
   const float* discount;
   const float* weights;  // PER importance weights or null
+  // fused PER draw (or null): the B sampling probabilities conv1 published;
+  // w_b = (up / p_b)^beta, normalised by the batch maximum if per_normalize
+  // (importance_sampling_weights, replay.py:344-376), also written to per_w_out
+  const double* per_probs;
+  double per_up, per_beta;
+  int per_normalize;
+  float* per_w_out;
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
   const float4* rec;     // batch records {a, r, d, 0} written by conv1, or null (slot chain)
   uint64_t* advance;     // fused sampler's step counter, advanced once here (or null)
@@ -116,6 +123,18 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     const int zc = min(zq, Z - 1), a = min(aq, A - 1);
     b2v = h.nz.p[zc][h.b2_off + (h.shared_bias ? 0 : a)];
   }
+  float wper = 1.f;
+  if (h.per_probs && wave == 0) {  // the batch's IS weights (the fused PER draw)
+    double m = 0.0;
+    for (int j = lane; j < B; j += 64) m = fmax(m, pow(h.per_up / h.per_probs[j], h.per_beta));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (lane == 0) {
+      const double wb = pow(h.per_up / h.per_probs[b], h.per_beta);
+      wper = (float)(h.per_normalize ? wb / m : wb);
+      if (h.per_w_out) h.per_w_out[b] = wper;
+    }
+  }
   if (!h.fwd_only && n == 0) {  // second hop of the batch record chain, needed only for the TD
     if (chain) {
       a_tm1 = h.action[slot];
@@ -127,6 +146,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
       d = rv.z;
     }
     if (h.weights) w = h.weights[b];
+    if (h.per_probs) w = wper;
     if (h.meta_p) pm = h.meta_p[b];
   }
   DQZ_STAMP(4, 1);

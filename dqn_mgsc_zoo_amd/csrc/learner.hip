@@ -300,11 +300,12 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
 static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
-                     int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr) {
+                     int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr,
+                     const PerSampleArgs* pd = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
-  if (L->cfg.algo == DQZ_ALGO_PER && !is_weights) return fail(DQZ_ERR_INVALID, "PER step needs is_weights");
+  if (L->cfg.algo == DQZ_ALGO_PER && !is_weights && !pd) return fail(DQZ_ERR_INVALID, "PER step needs is_weights");
   hipStream_t st = (hipStream_t)stream;
   const int B = L->cfg.batch, Z = L->Z, A = L->cfg.num_actions;
   NetZ nz;
@@ -319,11 +320,14 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   src.reward = S->reward;
   src.discount = S->discount;
   src.rec = reinterpret_cast<float4*>(L->rec);
-  if (draw || sm) {  // conv1 draws the batch itself; later kernels read the published slots
+  if (draw || sm || pd) {  // conv1 draws the batch itself; later kernels read the published slots
     Conv1Src fsrc = src;
     if (draw) {
       fsrc.fused = 1;
       fsrc.draw = *draw;
+    } else if (pd) {
+      fsrc.fused = 3;
+      fsrc.per = *pd;
     } else {
       fsrc.fused = 2;
       fsrc.sm = *sm;
@@ -350,10 +354,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.action = S->action;
   h.reward = S->reward;
   h.discount = S->discount;
-  h.weights = L->cfg.algo == DQZ_ALGO_PER ? is_weights : nullptr;
+  h.weights = L->cfg.algo == DQZ_ALGO_PER && !pd ? is_weights : nullptr;
+  if (pd) {
+    h.per_probs = pd->out_probs;
+    h.per_up = 1.0 / (double)pd->size;
+    h.per_beta = pd->beta;
+    h.per_normalize = pd->normalize;
+    h.per_w_out = pd->out_weights;
+  }
   h.meta_p = meta_p;
   h.rec = reinterpret_cast<const float4*>(L->rec);
-  h.advance = draw ? draw->counter : sm ? sm->counter : nullptr;  // null with injected uniforms
+  h.advance = draw ? draw->counter : sm ? sm->counter : pd ? (pd->inj_u ? nullptr : pd->counter) : nullptr;
   h.unit = unit;
   h.bound = L->cfg.grad_error_bound;
   h.td = L->td;
@@ -972,6 +983,47 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
   hipLaunchKernelGGL(per_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
+}
+
+int dqz_learner_step_per_draw(dqz_learner* L, const dqz_params* P, const dqz_store* S, const dqz_per_draw* d,
+                              void* stream) {
+  if (!L || !d || !d->tree || !d->out_indices || !d->out_slots || !d->out_probs || !d->max_seen_dev)
+    return fail(DQZ_ERR_INVALID, "null argument");
+  if (L->cfg.algo != DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "the learner is not a PER learner");
+  if (!d->injected_u && !d->counter_dev) return fail(DQZ_ERR_INVALID, "Philox draws need counter_dev");
+  if ((d->injected_u == nullptr) != (d->injected_uniform == nullptr))
+    return fail(DQZ_ERR_INVALID, "injected_uniform and injected_u go together");
+  if (d->cap < d->capacity || (d->cap & (d->cap - 1))) return fail(DQZ_ERR_INVALID, "cap must be a power of two >= capacity");
+  if (d->size < 1) return fail(DQZ_ERR_INVALID, "No IDs to sample.");
+  const double beta = d->importance_sampling_exponent, usp = d->uniform_sample_probability;
+  if (!(beta >= 0.0 && beta <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= exponent <= 1.");
+  if (!(usp >= 0.0 && usp <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= uniform_sample_probability <= 1.");
+  const int levels = tree_levels(d->cap);
+  if (L->cfg.batch > 64 || levels > PWB_LEVELS)
+    return fail(DQZ_ERR_INVALID, "the fused PER step takes batch <= 64 and cap <= 2^%d", PWB_LEVELS);
+  PerSampleArgs a;
+  a.tree = d->tree;
+  a.cap = d->cap;
+  a.levels = levels;
+  a.live_base = d->live_base;
+  a.size = d->size;
+  a.capacity = d->capacity;
+  a.n = L->cfg.batch;
+  a.usp = usp;
+  a.beta = beta;
+  a.normalize = d->normalize_weights;
+  a.seed = d->seed;
+  a.counter = d->counter_dev;
+  a.inj_uniform = d->injected_uniform;
+  a.inj_u = d->injected_u;
+  a.index_to_slot = d->index_to_slot;
+  a.out_indices = d->out_indices;
+  a.out_slots = d->out_slots;
+  a.out_weights = d->out_weights;
+  a.out_probs = d->out_probs;
+  PerWbArgs wb{d->tree, d->cap, levels, d->out_indices, nullptr, d->alpha, 0, d->max_seen_dev};
+  return step_impl(L, P, S, d->out_slots, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0, &wb, nullptr,
+                   &a);
 }
 
 int dqz_per_add(double* tree, int64_t cap, int32_t remove_index, int32_t add_index, double priority,

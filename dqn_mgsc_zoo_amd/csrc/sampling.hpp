@@ -907,94 +907,119 @@ struct PerSampleArgs {
 // subtract arithmetic as SumTree._query_single (replay.py:539-559), so the
 // same node sequence bit for bit.
 constexpr int PS_TOPD = 10;
+constexpr int PS_TOP_NODES = 2 << PS_TOPD;  // LDS doubles of the staged top
 
-__global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
-  __shared__ double s_top[2 << PS_TOPD];  // node i at s_top[i], i in [1, 2^(dtop + 1))
-  __shared__ double s_w[1024];
-  const bool inj = a.inj_u != nullptr;
-  const uint64_t ctr = inj ? 0 : *a.counter;
+// Stages tree nodes 1 .. 2^(dtop + 1) - 1 into s_top[1 ..] (whole block) and
+// returns dtop.
+__device__ __forceinline__ int per_stage_top(const PerSampleArgs& a, double* s_top) {
   const int dtop = min(a.levels, PS_TOPD);
   const int ntop = (2 << dtop) - 1;
   for (int q = threadIdx.x; q < ntop; q += blockDim.x) s_top[1 + q] = a.tree[1 + q];
   __syncthreads();
+  return dtop;
+}
+
+// Draw i of PrioritizedDistribution.sample (replay.py:680-716) by one
+// half-wave (lane l): the tree index and its sampling probability.
+struct PerPick {
+  int64_t idx;
+  double prob;
+};
+
+__device__ __forceinline__ PerPick per_pick(const PerSampleArgs& a, int i, int l, const double* s_top, int dtop,
+                                            uint64_t ctr) {
   const double root = s_top[1];
-  const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
-  for (int i = h; i < a.n; i += 32) {
-    double u_target, u_mix;
-    int64_t uni;
-    if (inj) {
-      u_target = a.inj_u[i];
-      u_mix = a.inj_u[a.n + i];
-      uni = a.inj_uniform[i];
-    } else {
-      const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
-                                 make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32)));
-      u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
-      u_mix = (double)(r.z >> 8) * 0x1.0p-24;
-      uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
+  double u_target, u_mix;
+  int64_t uni;
+  if (a.inj_u) {
+    u_target = a.inj_u[i];
+    u_mix = a.inj_u[a.n + i];
+    uni = a.inj_uniform[i];
+  } else {
+    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
+                               make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32)));
+    u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+    u_mix = (double)(r.z >> 8) * 0x1.0p-24;
+    uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
+  }
+  const bool use_uniform = u_mix < a.usp;
+  int64_t idx = uni;
+  double leaf;
+  if (root > 0.0 && !use_uniform) {
+    double t = u_target * root;  // u in [0, 1): t < root in fp64 (no range check, as the serial descent)
+    int64_t node = 1;
+    int depth = 0;
+    for (; depth < dtop; ++depth) {
+      const double left = s_top[2 * node];
+      if (t < left) {
+        node = 2 * node;
+      } else {
+        t -= left;
+        node = 2 * node + 1;
+      }
     }
-    const bool use_uniform = u_mix < a.usp;
-    int64_t idx = uni;
-    double leaf;
-    if (root > 0.0 && !use_uniform) {
-      double t = u_target * root;  // u in [0, 1): t < root in fp64 (no range check, as the serial descent)
-      int64_t node = 1;
-      int depth = 0;
-      for (; depth < dtop; ++depth) {
-        const double left = s_top[2 * node];
+    double lv = s_top[node];  // the leaf itself when the whole tree sits in LDS
+    while (depth < a.levels) {
+      const int K = min(5, a.levels - depth);
+      double v0 = 0.0, v1 = 0.0;
+      {
+        const int k0 = 31 - __builtin_clz(l + 2), k1 = 31 - __builtin_clz(l + 34);
+        if (k0 <= K) v0 = a.tree[(node << k0) + (l + 2 - (1 << k0))];
+        if (k1 <= K) v1 = a.tree[(node << k1) + (l + 34 - (1 << k1))];
+      }
+      int64_t pos = 0;
+      for (int k = 1; k <= K; ++k) {
+        const int q = (1 << k) - 2 + 2 * (int)pos;  // left child at relative depth k
+        const double left = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
         if (t < left) {
-          node = 2 * node;
+          pos = 2 * pos;
         } else {
           t -= left;
-          node = 2 * node + 1;
+          pos = 2 * pos + 1;
         }
       }
-      double lv = s_top[node];  // the leaf itself when the whole tree sits in LDS
-      while (depth < a.levels) {
-        const int K = min(5, a.levels - depth);
-        double v0 = 0.0, v1 = 0.0;
-        {
-          const int k0 = 31 - __builtin_clz(l + 2), k1 = 31 - __builtin_clz(l + 34);
-          if (k0 <= K) v0 = a.tree[(node << k0) + (l + 2 - (1 << k0))];
-          if (k1 <= K) v1 = a.tree[(node << k1) + (l + 34 - (1 << k1))];
-        }
-        int64_t pos = 0;
-        for (int k = 1; k <= K; ++k) {
-          const int q = (1 << k) - 2 + 2 * (int)pos;  // left child at relative depth k
-          const double left = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
-          if (t < left) {
-            pos = 2 * pos;
-          } else {
-            t -= left;
-            pos = 2 * pos + 1;
-          }
-        }
-        const int q = (1 << K) - 2 + (int)pos;
-        lv = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
-        node = (node << K) + pos;
-        depth += K;
-      }
-      idx = node - a.cap;
-      leaf = lv;
-    } else {
-      leaf = a.tree[a.cap + idx];
+      const int q = (1 << K) - 2 + (int)pos;
+      lv = q < 32 ? __shfl(v0, q, 32) : __shfl(v1, q - 32, 32);
+      node = (node << K) + pos;
+      depth += K;
     }
-    const double up = 1.0 / (double)a.size;
-    const double pp = root > 0.0 ? leaf / root : up;
-    double prob;
-    {
-      // numpy rounds the product and the sum separately: no fma (hipcc
-      // contracts even __dmul_rn + __dadd_rn under its default fp-contract)
+    idx = node - a.cap;
+    leaf = lv;
+  } else {
+    leaf = a.tree[a.cap + idx];
+  }
+  const double up = 1.0 / (double)a.size;
+  const double pp = root > 0.0 ? leaf / root : up;
+  double prob;
+  {
+    // numpy rounds the product and the sum separately: no fma (hipcc
+    // contracts even __dmul_rn + __dadd_rn under its default fp-contract)
 #pragma clang fp contract(off)
-      const double x1 = (1.0 - a.usp) * pp;
-      const double x2 = a.usp * up;
-      prob = x1 + x2;
-    }
-    const double w = pow(up / prob, a.beta);
+    const double x1 = (1.0 - a.usp) * pp;
+    const double x2 = a.usp * up;
+    prob = x1 + x2;
+  }
+  return PerPick{idx, prob};
+}
+
+// importance_sampling_weights (replay.py:344-376) of one draw, unnormalised.
+__device__ __forceinline__ double per_weight(double up, double prob, double beta) { return pow(up / prob, beta); }
+
+__global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
+  __shared__ double s_top[PS_TOP_NODES];  // node i at s_top[i], i in [1, 2^(dtop + 1))
+  __shared__ double s_w[1024];
+  const bool inj = a.inj_u != nullptr;
+  const uint64_t ctr = inj ? 0 : *a.counter;
+  const int dtop = per_stage_top(a, s_top);
+  const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
+  const double up = 1.0 / (double)a.size;
+  for (int i = h; i < a.n; i += 32) {
+    const PerPick pk = per_pick(a, i, l, s_top, dtop, ctr);
+    const double w = per_weight(up, pk.prob, a.beta);
     if (l == 0) {
-      if (a.out_indices) a.out_indices[i] = (int32_t)idx;
-      a.out_slots[i] = a.index_to_slot ? a.index_to_slot[idx] : (int32_t)idx;
-      if (a.out_probs) a.out_probs[i] = prob;
+      if (a.out_indices) a.out_indices[i] = (int32_t)pk.idx;
+      a.out_slots[i] = a.index_to_slot ? a.index_to_slot[pk.idx] : (int32_t)pk.idx;
+      if (a.out_probs) a.out_probs[i] = pk.prob;
       s_w[i] = w;
     }
   }
@@ -1005,6 +1030,33 @@ __global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) a.out_weights[i] = (float)(a.normalize ? s_w[i] / m : s_w[i]);
   __syncthreads();
   if (threadIdx.x == 0 && !inj) *a.counter = ctr + 1;
+}
+
+// PER draw b fused into the learner's conv1 workgroups (dqz_learner_step_per_draw):
+// the block stages the tree's top in `lds` (conv1's input buffer, before its
+// frame gather), its first half-wave descends, and the block gets the slot;
+// the publishing block (rb 0, z 0) writes the tree index, slot and
+// probability of draw b (the head turns the B probabilities into normalised
+// IS weights, the backward's write-back uses the indices).  The Philox
+// counter is advanced by the head once every conv1 block has read it.
+__device__ __forceinline__ int32_t per_draw_slot(const PerSampleArgs& a, int b, double* lds, bool publish) {
+  __shared__ int32_t s_slot;
+  const int dtop = per_stage_top(a, lds);
+  if (threadIdx.x < 32) {
+    const uint64_t ctr = a.inj_u ? 0 : *a.counter;
+    const PerPick pk = per_pick(a, b, threadIdx.x, lds, dtop, ctr);
+    if (threadIdx.x == 0) {
+      const int32_t slot = a.index_to_slot ? a.index_to_slot[pk.idx] : (int32_t)pk.idx;
+      s_slot = slot;
+      if (publish) {
+        a.out_indices[b] = (int32_t)pk.idx;
+        a.out_slots[b] = slot;
+        a.out_probs[b] = pk.prob;
+      }
+    }
+  }
+  __syncthreads();  // s_slot published; every read of lds done before the frame gather reuses it
+  return s_slot;
 }
 
 // PrioritizedTransitionReplay.add on device (replay.py:1068-1096 with

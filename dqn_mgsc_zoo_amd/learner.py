@@ -161,6 +161,18 @@ class Learner:
         int(seed) & (2**64 - 1), _native.ptr(counter), _native.ptr(uniforms),
         _native.ptr(slots_out), _native.stream_handle(stream)))
 
+  def step_per_draw(self, store, draw, stream=None):
+    """A whole prioritized learn in one learner step
+    (dqz_learner_step_per_draw): the PER draw inside the forward launch, the
+    IS weights in the head, the write-back inside the backward launch.
+    `draw` is a _native.DqzPerDraw (see
+    replay.PrioritizedTransitionReplay.per_draw)."""
+    if self.algo != 'per':
+      raise ValueError('step_per_draw needs a PER learner')
+    _native.check(_native.lib().dqz_learner_step_per_draw(
+        self._h, ctypes.byref(self._params_c), store.c_ref(), ctypes.byref(draw),
+        _native.stream_handle(stream)))
+
   def grad(self, store, slots, weights=None, out=None, stream=None):
     """jax.grad(loss_fn) of the same step into a flat tensor (no update)."""
     if slots.dtype != torch.int32 or slots.numel() != self.batch_size:

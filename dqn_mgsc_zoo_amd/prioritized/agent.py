@@ -4,11 +4,11 @@ Double-Q loss weighted by importance-sampling weights, new transitions get
 the running max priority, learned priorities are |td| (agent.py:187-206).
 
 With frame transitions the replay's sum tree lives in HBM and a learn is
-two device calls with no host synchronisation: `sample_device` (the
-replay's RandomState draws, resolved on device: tree indices, slots, IS
-weights) and the learner step with the write-back (|td| ->
-max_seen_priority -> p ** alpha into the tree) folded into its backward
-launch (dqz_learner_step_per).  `max_seen_priority` is then a device scalar,
+one device call with no host synchronisation (dqz_learner_step_per_draw):
+the replay's RandomState draws are resolved into tree indices and slots by
+the learner's conv1 workgroups, the head forms the IS weights, and the
+write-back (|td| -> max_seen_priority -> p ** alpha into the tree) runs
+inside the backward launch.  `max_seen_priority` is then a device scalar,
 read back only when asked for.  Host-stored items keep the reference's host
 path.
 """
@@ -34,6 +34,11 @@ class PrioritizedDqn(agent_base.DeviceDqnAgent):
         torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
         torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
         self._w)
+    self._draw_out = (
+        torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
+        torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
+        torch.zeros((self._batch_size,), dtype=torch.float64, device=dev),
+        self._w)
 
   def _add(self, transition) -> None:
     if self._replay.stores_on_device(transition):
@@ -43,12 +48,15 @@ class PrioritizedDqn(agent_base.DeviceDqnAgent):
 
   def _learn(self) -> None:
     if self._replay.on_device:
+      pd = self._replay.per_draw(self._batch_size, self._max_seen_dev,
+                                 out=self._draw_out)
+      if pd is not None:  # draw, weights, step and write-back: one call
+        self._learner.step_per_draw(self._store(), pd[0])
+        return
       indices, slots, weights = self._replay.sample_device(
           self._batch_size, out=self._sample_out)
-      wb = self._replay.write_back_args(indices, self._max_seen_dev)
-      self._learner.step(self._store(), slots, weights, write_back=wb)
-      if wb is None:
-        self._replay.write_back(self._learner, indices, self._max_seen_dev)
+      self._learner.step(self._store(), slots, weights)
+      self._replay.write_back(self._learner, indices, self._max_seen_dev)
       return
     ids, slots, weights = self._replay.sample_slots(self._batch_size)
     self._w.copy_(torch.from_numpy(np.asarray(weights, np.float32)))

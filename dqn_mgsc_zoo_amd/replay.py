@@ -1112,6 +1112,43 @@ class PrioritizedTransitionReplay(_StorageMixin):
         float(self._distribution.priority_exponent), _native.ptr(max_seen_dev),
         _native.stream_handle()))
 
+  def per_draw(self, size: int, max_seen_dev, out=None):
+    """The DqzPerDraw of one learn (Learner.step_per_draw): this replay's
+    RandomState draws for sample(size), in the reference's order, injected;
+    the step resolves them on device, forms the IS weights and writes the
+    priorities back.  Returns (draw, (indices, slots, probs, weights,
+    inj_idx, inj_u)) — keep the tensors alive until the step has run.
+    None when the batch or tree is past the fused step's limits."""
+    import torch  # pylint: disable=g-import-not-at-top
+    from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
+    tree = self._device_tree()
+    if size > 64 or tree.capacity > (1 << 24):
+      return None
+    dist = self._distribution
+    beta = self.importance_sampling_exponent
+    if not 0.0 <= beta <= 1.0:
+      raise ValueError('Require 0 <= exponent <= 1.')
+    dev = tree.tree.device
+    uniform_idx, u = dist.draw(size)
+    inj_i = torch.from_numpy(uniform_idx).pin_memory().to(dev, non_blocking=True)
+    inj_u = torch.from_numpy(u).pin_memory().to(dev, non_blocking=True)
+    if out is None:
+      out = (torch.empty((size,), dtype=torch.int32, device=dev),
+             torch.empty((size,), dtype=torch.int32, device=dev),
+             torch.empty((size,), dtype=torch.float64, device=dev),
+             torch.empty((size,), dtype=torch.float32, device=dev))
+    indices, slots, probs, weights = out
+    dist.note_priorities(None)  # the write-back may write positive priorities
+    p = _native.ptr
+    d = _native.DqzPerDraw(
+        p(tree.tree).value, tree.capacity, 0, self.size, self._capacity,
+        float(dist.uniform_sample_probability), float(beta),
+        int(bool(self._normalize_weights)), 0, None, p(inj_i).value,
+        p(inj_u).value, p(tree.index_to_slot).value,
+        float(dist.priority_exponent), p(max_seen_dev).value,
+        p(indices).value, p(slots).value, p(probs).value, p(weights).value)
+    return d, (indices, slots, probs, weights, inj_i, inj_u)
+
   def write_back_args(self, indices, max_seen_dev):
     """The write-back of `indices` as Learner.step(write_back=...) folds it
     into the learner's backward launch (dqz_learner_step_per), or None when

@@ -385,6 +385,38 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
                    int32_t* out_indices, int32_t* out_slots, float* out_weights, double* out_probs,
                    void* stream);
 
+/* A whole prioritized learn (prioritized/agent.py:187-206) in one learner
+ * step: the draw of dqz_per_sample (same streams: Philox (seed,
+ * *counter_dev) or the caller's RandomState draws injected, same node
+ * sequence, same fp64 probabilities) computed by the forward's conv1
+ * workgroups, the IS weights (importance_sampling_weights, normalised by the
+ * batch maximum if normalize_weights) formed by the head, the double-Q step
+ * with them, and the |td|^alpha write-back inside the backward launch
+ * (dqz_learner_step_per).  Outputs: out_indices (tree indices), out_slots,
+ * out_probs (f64), out_weights (f32, may be NULL), all device [B].  Batch
+ * <= 64, cap a power of two <= 2^24. */
+typedef struct dqz_per_draw {
+  double* tree;
+  int64_t cap;
+  int64_t live_base, size, capacity;
+  double uniform_sample_probability;
+  double importance_sampling_exponent;
+  int normalize_weights;
+  uint64_t seed;
+  uint64_t* counter_dev;
+  const int32_t* injected_uniform;
+  const double* injected_u;
+  const int32_t* index_to_slot;
+  double alpha;
+  double* max_seen_dev;
+  int32_t* out_indices;
+  int32_t* out_slots;
+  double* out_probs;
+  float* out_weights;
+} dqz_per_draw;
+int dqz_learner_step_per_draw(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
+                              const dqz_per_draw* draw, void* stream);
+
 /* PrioritizedTransitionReplay.add on device (replay.py:1068-1096 ->
  * PrioritizedDistribution.remove_priorities / add_priorities, :642-678): the
  * evicted tree index remove_index (-1: none) is set to 0, add_index to

@@ -463,3 +463,87 @@ def test_fused_logit_draw_step_equals_sampler_then_step(device):
   for which in ('online', 'mu', 'nu'):
     assert torch.equal(getattr(a, which), getattr(b, which)), which
   assert a.sync_status() == 0 and b.sync_status() == 0
+
+
+@pytest.mark.parametrize('injected', [False, True])
+def test_fused_per_draw_step_equals_sampler_then_step(device, injected):
+  """dqz_learner_step_per_draw (the PER draw in conv1, the IS weights in the
+  head, the write-back in the backward) == dqz_per_sample +
+  dqz_learner_step_per, bit for bit: indices, slots, probabilities,
+  weights, parameters, sum tree, max_seen — Philox draws or the reference's
+  RandomState draws injected, and under hipGraph replay."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  batch, alpha, usp, beta = 32, 0.6, 0.05, 0.4
+  _, a, st, _, _, _, _, _ = _setup('per', batch, seed=61)
+  _, b, _, _, _, _, _, _ = _setup('per', batch, seed=61)
+  rng = np.random.default_rng(62)
+  host = replay_lib.SumTree()
+  prios = rng.random(st.capacity) ** 2
+  prios[::17] = 0.0
+  host.set_all(prios)
+  cap = host.capacity
+  ta = torch.from_numpy(host.storage.copy()).to(device)
+  tb = ta.clone()
+  ma = torch.tensor([1.0], dtype=torch.float64, device=device)
+  mb = ma.clone()
+  ca = torch.zeros((1,), dtype=torch.int64, device=device)
+  cb = torch.zeros((1,), dtype=torch.int64, device=device)
+  i32 = lambda: torch.zeros((batch,), dtype=torch.int32, device=device)
+  ia, sa, ib, sb = i32(), i32(), i32(), i32()
+  wa = torch.zeros((batch,), dtype=torch.float32, device=device)
+  wb = wa.clone()
+  pa = torch.zeros((batch,), dtype=torch.float64, device=device)
+  pb = pa.clone()
+  lib = _native.lib()
+  inj = {}
+
+  def draws():
+    if injected:
+      inj['i'] = torch.from_numpy(rng.integers(0, st.capacity, batch).astype(np.int32)).to(device)
+      inj['u'] = torch.from_numpy(rng.random(2 * batch)).to(device)
+
+  def ref_step():
+    _native.check(lib.dqz_per_sample(
+        _native.ptr(ta), cap, 0, st.capacity, st.capacity, batch, usp, beta, 1, 7,
+        None if injected else _native.ptr(ca), _native.ptr(inj.get('i')),
+        _native.ptr(inj.get('u')), None, _native.ptr(ia), _native.ptr(sa),
+        _native.ptr(wa), _native.ptr(pa), _native.stream_handle()))
+    a.step(st, sa, wa, write_back=(ta, cap, ia, alpha, ma))
+
+  def fused_draw():
+    return _native.DqzPerDraw(
+        tb.data_ptr(), cap, 0, st.capacity, st.capacity, usp, beta, 1, 7,
+        None if injected else cb.data_ptr(),
+        inj['i'].data_ptr() if injected else None,
+        inj['u'].data_ptr() if injected else None, None, alpha, mb.data_ptr(),
+        ib.data_ptr(), sb.data_ptr(), pb.data_ptr(), wb.data_ptr())
+
+  for _ in range(3):
+    draws()
+    ref_step()
+    b.step_per_draw(st, fused_draw())
+    torch.cuda.synchronize()
+    for x, y in ((ia, ib), (sa, sb), (pa, pb), (wa, wb)):
+      assert torch.equal(x, y)
+  if not injected:  # graph replay of the Philox form
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    d = fused_draw()
+    with torch.cuda.stream(side):
+      b.step_per_draw(st, d)
+    torch.cuda.current_stream(device).wait_stream(side)
+    ref_step()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      for _ in range(3):
+        b.step_per_draw(st, d)
+    g.replay()
+    for _ in range(3):
+      ref_step()
+    assert int(ca.item()) == int(cb.item())
+  torch.cuda.synchronize()
+  assert torch.equal(ta, tb) and torch.equal(ma, mb)
+  for which in ('online', 'mu', 'nu'):
+    assert torch.equal(getattr(a, which), getattr(b, which)), which
+  assert a.sync_status() == 0 and b.sync_status() == 0
