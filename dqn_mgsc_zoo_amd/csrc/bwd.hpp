@@ -74,14 +74,20 @@ constexpr int FC1X_LD = DQZ_FC1DX_LD;
 // it).  DW: dW1 + RMSProp, which only has to finish before the next step and
 // runs on the learner's side stream beside the conv backward kernels.  DW
 // must start after DX: it overwrites the W1 rows DX reads.
-constexpr int FC1B_SMEM = 32 * (FC1B_LD > FC1X_LD ? FC1B_LD : FC1X_LD) + 4 * 2 * 256;  // floats: dz1 chunk (later the dW block) + dX partials
+constexpr int FC1X_RED = 256 + 4 * 16;  // one padded 16 x 16 dX partial tile
+constexpr int FC1B_SMEM = 32 * (FC1B_LD > FC1X_LD ? FC1B_LD : FC1X_LD) + 4 * 2 * FC1X_RED;  // floats: dz1 chunk (later the dW block) + dX partials
 
 template <bool DX, bool DW>
 __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, int blk) {
   DQZ_STAMP(DW ? 11 : 5, 0);
   constexpr int LD = DW ? FC1B_LD : FC1X_LD;
   float* s_dz = smem;
-  float(*s_red)[2][256] = reinterpret_cast<float(*)[2][256]>(smem + 32 * LD);
+  // dX partials [wave][mt][row 4 kq + r][n], 16 floats of padding after every
+  // 4 rows: the writes of lanes kq = 0 / 1 (and 2 / 3), one ds_write_b32
+  // lane group, land 16 banks apart instead of on the same banks; the
+  // reduction's reads stay conflict-free (a wave reads rows 4w .. 4w + 3).
+  float(*s_red)[2][FC1X_RED] = reinterpret_cast<float(*)[2][FC1X_RED]>(smem + 32 * LD);
+  auto red_at = [](int row, int col) { return row * 16 + 16 * (row >> 2) + col; };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = 16 * blk;
@@ -146,7 +152,7 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[w][mt][(4 * kq + r) * 16 + n] = xacc[mt][r];
+        for (int r = 0; r < 4; ++r) s_red[w][mt][red_at(4 * kq + r, n)] = xacc[mt][r];
       }
       if constexpr (DW) {
       // dW over the chunk: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
@@ -162,7 +168,8 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int sample = c + 16 * h + (t >> 4);
-        const float v2 = (s_red[0][h][t] + s_red[1][h][t]) + (s_red[2][h][t] + s_red[3][h][t]);
+        const int k = red_at(t >> 4, t & 15);
+        const float v2 = (s_red[0][h][k] + s_red[1][h][k]) + (s_red[2][h][k] + s_red[3][h][k]);
         if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
       }
       }

@@ -32,6 +32,14 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Cross-wave partial tiles [row][16] with 16 floats of padding after every
+// 4 rows: a 16x16x4 accumulator store (lane (n, kq) writes row 4 kq + r) puts
+// lanes kq = 0 / 1 (one ds_write_b32 lane group) 16 banks apart instead of on
+// the same banks; a 32-lane read group covers rows 2j, 2j + 1 of one 4-row
+// block, so the position-major reads stay conflict-free.
+__device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + 16 * (row >> 2) + col; }
+constexpr int red_rows(int rows) { return rows * 16 + 16 * ((rows + 3) / 4); }
+
 struct LayerFwdArgs {
   const float* in;  // [Z][B][...] layer input (NHWC)
   NetZ nz;
@@ -112,17 +120,20 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     last += __shfl_xor(last, 32, 64);
   }
   __syncthreads();
-  float* s_red = s_in;  // [4][96][16]
+  float* s_red = s_in;  // [4][96 rows, padded][16]
+  constexpr int RW = red_rows(96);
+  static_assert(4 * RW <= C2L_WIN, "conv2 partials fit the window");
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * 1536 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
-  if (DQZ_TRIM && kq == 0) s_red[w * 1536 + (C2M - 1) * 16 + n] = last;
+    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
+  if (DQZ_TRIM && kq == 0) s_red[w * RW + red_idx(C2M - 1, n)] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < C2M * 16; i += 256) {
-    const float v = ((s_red[i] + s_red[1536 + i]) + (s_red[3072 + i] + s_red[4608 + i])) + bv;
+    const int k = red_idx(i >> 4, i & 15);
+    const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
     if constexpr (PUB)
       __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -209,17 +220,20 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     last += __shfl_xor(last, 32, 64);
   }
   __syncthreads();
-  float* s_red = s_in;  // [4][64][16]
+  float* s_red = s_in;  // [4][64 rows, padded][16]
+  constexpr int RW = red_rows(64);
+  static_assert(4 * RW <= C3L_WIN, "conv3 partials fit the window");
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * 1024 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
-  if (DQZ_TRIM && kq == 0) s_red[w * 1024 + (C3M - 1) * 16 + n] = last;
+    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
+  if (DQZ_TRIM && kq == 0) s_red[w * RW + red_idx(C3M - 1, n)] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < C3M * 16; i += 256) {
-    const float v = ((s_red[i] + s_red[1024 + i]) + (s_red[2048 + i] + s_red[3072 + i])) + bv;
+    const int k = red_idx(i >> 4, i & 15);
+    const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
     out[(i >> 4) * C3CO + (i & 15)] = linear ? v : relu(v);
   }
   DQZ_STAMP(2, 3);
