@@ -99,6 +99,9 @@ __device__ __forceinline__ void store_bytes_as_bf16(uint16_t* dst, uint4 v) {
 
 // Stages input rows [20*rb, 20*rb + 24) of sample b, stack `which`, as
 // s_in[ci][row][col] = pixel (bf16).
+// F: the fused draw mode (src.fused), a template parameter so a launch only
+// carries the draw code it runs.
+template <int F>
 __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src& src, int b, int which, int rb,
                                                        int z = 0, int sk = -1) {
   const int row0 = rb * C1S * C1_ROWS;
@@ -122,13 +125,13 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
     // slot -> 4 frame ids -> 504 16-byte pieces (2 per thread), all loads in
     // flight before the first LDS store.
     int slot;
-    if (src.fused == 1) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
+    if constexpr (F == 1) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
       slot = uniform_slot(*src.draw.counter, b, src.draw);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.draw.slots_out[b] = slot;
-    } else if (src.fused == 2) {  // fused learned-logit draw (every block of b runs the search)
+    } else if constexpr (F == 2) {  // fused learned-logit draw (every block of b runs the search)
       slot = softmax_draw_slot(src.sm, b);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.sm.slots_out[b] = slot;
-    } else if (src.fused == 3) {  // fused prioritized draw (the tree top staged in s_in first)
+    } else if constexpr (F == 3) {  // fused prioritized draw (the tree top staged in s_in first)
       slot = per_draw_slot(src.per, b, reinterpret_cast<double*>(s_in), rb == 0 && z == 0);
     } else {
       slot = src.slots[b];
@@ -174,7 +177,7 @@ __device__ __forceinline__ float div255(float s) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, s), r, q);
 }
 
-template <bool PUB>
+template <bool PUB, int F>
 __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* smem, const SampleJob sj) {
   DQZ_STAMP(0, 0);
   uint16_t* s_in = reinterpret_cast<uint16_t*>(smem);  // [4][24][84] bf16
@@ -190,7 +193,7 @@ __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* sme
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) wv[s][j] = W[(((2 * wave + (s >> 1)) * C1K + j) * FC + 2 * (s & 1) + h) * C1CO + r];
-  stage_conv1_input(s_in, a.src, b, a.nz.which[z], rb, z, 14);
+  stage_conv1_input<F>(s_in, a.src, b, a.nz.which[z], rb, z, 14);
   bf16x8 wf[4][3];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -269,7 +272,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.Z * a.B);
   if (!sj.valid) return;
-  conv1_fwd_body<false>(a, smem, sj);
+  switch (a.src.fused) {  // the stand-alone conv1 launch (profile / debug layouts)
+    case 1: conv1_fwd_body<false, 1>(a, smem, sj); break;
+    case 2: conv1_fwd_body<false, 2>(a, smem, sj); break;
+    case 3: conv1_fwd_body<false, 3>(a, smem, sj); break;
+    default: conv1_fwd_body<false, 0>(a, smem, sj); break;
+  }
 }
 
 struct Conv1DwArgs {

@@ -87,8 +87,10 @@ static int init_kernel_attrs() {
   if (g_attr_done) return DQZ_OK;
   DQZ_HIP(hipFuncSetAttribute((const void*)conv1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kConv1FwdSmem));
-  DQZ_HIP(hipFuncSetAttribute((const void*)fwd_conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kConv1FwdSmem));
+  const void* fwd_kernels[] = {(const void*)fwd_conv_kernel<0>, (const void*)fwd_conv_kernel<1>,
+                               (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>};
+  for (const void* k : fwd_kernels)
+    DQZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kConv1FwdSmem));
   g_attr_done = 1;
   return DQZ_OK;
 }
@@ -247,9 +249,13 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
     c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, 4, 4};
     c3.wait = c2.pub;
     const unsigned npro = src.fused == 2 ? (unsigned)((src.sm.nblocks + 7) / 8 * 8) : 0u;
-    DQZ_PHASE(0, hipLaunchKernelGGL(fwd_conv_kernel, dim3(npro + 3 * xcd_grid(4, Z * B).x), dim3(256), kConv1FwdSmem,
-                                    st, c1, c2, c3);
-              DQZ_HIP(hipGetLastError()));
+    const dim3 grid(npro + 3 * xcd_grid(4, Z * B).x);
+    DQZ_PHASE(0, switch (src.fused) {
+      case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+      case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+      case 3: hipLaunchKernelGGL(fwd_conv_kernel<3>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+      default: hipLaunchKernelGGL(fwd_conv_kernel<0>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+    } DQZ_HIP(hipGetLastError()));
     if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
   } else {
     DQZ_PHASE(0, hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);

@@ -153,14 +153,14 @@ def test_per_priorities_after_learning(device):
   _run(agent, 100)
   assert replay.on_device and replay.distribution.on_device
   captured = {}
-  orig = replay.sample_device
+  orig = replay.per_draw
 
-  def spy(size, out=None):
-    res = orig(size, out=out)
-    captured['idx'] = res[0].clone()
+  def spy(size, max_seen_dev, out=None):
+    res = orig(size, max_seen_dev, out=out)
+    captured['idx'] = res[1][0]  # the tree indices the fused step writes
     return res
 
-  replay.sample_device = spy
+  replay.per_draw = spy
   before = agent.max_seen_priority
   agent._learn()  # pylint: disable=protected-access
   _, td, _ = agent.learner.fetch_outputs()
