@@ -46,9 +46,10 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32 = f32 vector pea
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 STEP_FLOP = {'dqn': 2182873088, 'double': 2781020160,
              'per': 2781020160, 'mgsc': 2182873088}
-# SURVEY.md §8(d); MGSC sampling adds one read of the 1M f32 logits
+# SURVEY.md §8(d); an MGSC draw adds, per sample, one read of the chunk sums
+# (245 f64) and of one chunk of 4096 f32 logits: 32 x 18,344 B
 STEP_BYTES = {'dqn': 49048488, 'double': 49048488, 'per': 49048488,
-              'mgsc': 53048488}
+              'mgsc': 49048488 + 32 * (4096 * 4 + 245 * 8)}
 LEARNER_ALGO = {'dqn': 'dqn', 'double': 'double', 'per': 'per', 'mgsc': 'dqn'}
 WORKLOAD = {
     'dqn': 'BASELINE config 2: dqn agent learner-only loop',

@@ -201,6 +201,7 @@ SIGNATURES = {
     'dqz_logits_sample_slots': (
         _int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _int, _vp, _vp, _vp]),
     'dqz_logits_probs': (_int, [_vp, _vp, _vp, _vp, _vp]),
+    'dqz_logits_terms': (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     'dqz_logits_write': (_int, [_vp, _vp, _vp, _vp, _int, _vp]),
     'dqz_logits_put': (_int, [_vp, _vp, _i64, ctypes.c_float, _vp]),
     'dqz_logits_invalidate': (_int, [_vp]),
@@ -208,7 +209,7 @@ SIGNATURES = {
         _int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float),
                ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int), _vp]),
     'dqz_logits_run_set': (
-        _int, [_vp, ctypes.c_double, ctypes.c_float, _int, _int, _int, _vp]),
+        _int, [_vp, _vp, ctypes.c_double, ctypes.c_float, _int, _int, _int, _vp]),
     'dqz_uniform_philox': (_int, [ctypes.c_uint64, _vp, _int, _vp, _vp]),
     'dqz_sumtree_set': (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
     'dqz_sumtree_query': (_int, [_vp, _i64, _vp, _int, _vp, _vp]),

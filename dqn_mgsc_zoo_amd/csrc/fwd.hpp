@@ -259,22 +259,12 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 // conv1 blocks retire).
 static_assert(C2L_WIN * sizeof(float) <= kConv1FwdSmem && C3L_WIN * sizeof(float) <= kConv1FwdSmem,
               "fwd_conv_kernel's dynamic LDS holds every body's window");
-// With the fused learned-logit draw (c1.src.fused == 2) the grid starts with
-// the draw's producer blocks (a multiple of 8, so the sample ranges keep
-// their XCD alignment): they are dispatched first and never wait.
+// F: the fused draw mode of the conv1 blocks (Conv1Src::fused).
 template <int F>
 __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int zb = c1.Z * c1.B, n = 4 * ((zb + 7) / 8 * 8);
   int i = blockIdx.x;
-  if constexpr (F == 2) {
-    const int np = (c1.src.sm.nblocks + 7) / 8 * 8;
-    if (i < np) {
-      if (i < c1.src.sm.nblocks) softmax_draw_produce(c1.src.sm, i);
-      return;
-    }
-    i -= np;
-  }
   if (i < n) {
     const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, zb);
     if (sj.valid) conv1_fwd_body<true, F>(c1, smem, sj);

@@ -248,8 +248,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
     c2.wait = c1.pub;
     c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, 4, 4};
     c3.wait = c2.pub;
-    const unsigned npro = src.fused == 2 ? (unsigned)((src.sm.nblocks + 7) / 8 * 8) : 0u;
-    const dim3 grid(npro + 3 * xcd_grid(4, Z * B).x);
+    const dim3 grid(3 * xcd_grid(4, Z * B).x);
     DQZ_PHASE(0, switch (src.fused) {
       case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
       case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
@@ -337,9 +336,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     } else {
       fsrc.fused = 2;
       fsrc.sm = *sm;
-      // the draw's hand-off word and error word live with the learner's
-      fsrc.sm.sync = Handoff{L->sync + (16 * B + 1) * Handoff::kStride, L->sync + (16 * B + 2) * Handoff::kStride,
-                             L->sync + 16 * B * Handoff::kStride, sm->nblocks, C1_BLOCKS * Z * B, L->spin_max};
     }
     if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, true)) return rc;
   } else {
@@ -704,12 +700,13 @@ int dqz_gather_stacks(const dqz_store* S, const int32_t* slots, int n, int which
 struct dqz_logit_buffer {
   int64_t capacity;
   int nblocks, max_queries;
-  void* block;  // double bsum[nblocks] | MaxSum part[nblocks] | float lse | LogitRun
+  void* block;  // double csum[nblocks] | MaxSum part[nblocks] | int dirty[nblocks] | float lse | LogitRun | sync
+  double* csum;    // per-chunk sums of the sampling terms (sampling.hpp chunk_sum)
   MaxSum* part;
-  double* bsum;
+  int* dirty;      // chunks a writer changed, for chunk_sums_kernel
   float* lse;
   LogitRun* run;   // running log-sum-exp (sampling.hpp)
-  int* sync;       // softmax_sample_kernel's arrival / done / error words (SampleSync)
+  int* sync;       // softmax_sample_kernel's done word (SampleSync)
   bool run_known;  // host side: every write since the last scan went through the library
   int run_adds;    // running adds since the last scan
 };
@@ -720,11 +717,12 @@ constexpr int kLogitReseed = 4096;
 
 int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out) {
   if (!out || capacity < 1 || max_queries < 1) return fail(DQZ_ERR_INVALID, "bad logit buffer arguments");
+  if (capacity > ((int64_t)INT32_MAX + 1) * SM_CHUNK / 2) return fail(DQZ_ERR_INVALID, "capacity too large");
   dqz_logit_buffer* b = new dqz_logit_buffer();
   b->capacity = capacity;
   b->max_queries = max_queries;
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
-  const size_t head = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double));
+  const size_t head = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int));
   const size_t sync_off = (head + 64 + sizeof(LogitRun) + 255) / 256 * 256;
   const size_t bytes = sync_off + 3 * SampleSync::kStride * sizeof(int);
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
@@ -737,8 +735,9 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
     return fail(DQZ_ERR_HIP, "hipMemset of logit scratch failed");
   }
   char* p = (char*)b->block;
-  b->bsum = (double*)p;
+  b->csum = (double*)p;
   b->part = (MaxSum*)(p + (size_t)b->nblocks * sizeof(double));
+  b->dirty = (int*)(p + (size_t)b->nblocks * (sizeof(double) + sizeof(MaxSum)));
   b->lse = (float*)(p + head);
   b->run = (LogitRun*)(p + head + 64);
   b->sync = (int*)(p + sync_off);
@@ -755,7 +754,16 @@ int dqz_logit_buffer_destroy(dqz_logit_buffer* b) {
   return DQZ_OK;
 }
 
-// Full two-pass log-sum-exp over the buffer (re-seeds the running state).
+// csum of the flagged chunks (dirty != null) or of all of them.
+static int chunk_sums(dqz_logit_buffer* b, const float* logits, bool dirty_only, hipStream_t st) {
+  hipLaunchKernelGGL(chunk_sums_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
+                     b->csum, dirty_only ? b->dirty : nullptr);
+  DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+// Full two-pass log-sum-exp over the buffer (re-seeds the running state),
+// then every chunk sum about the new shift.
 static int logits_lse(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
                       float* lse_out, hipStream_t st) {
   hipLaunchKernelGGL(lse_partial_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part,
@@ -764,6 +772,7 @@ static int logits_lse(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int
   hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part, b->nblocks, lse_out ? lse_out : b->lse,
                      logits, write_pos, size, b->run);
   DQZ_HIP(hipGetLastError());
+  if (int rc = chunk_sums(b, logits, false, st)) return rc;
   b->run_known = true;
   b->run_adds = 0;
   return DQZ_OK;
@@ -781,7 +790,7 @@ int dqz_logits_add(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_
     if (int rc = logits_lse(b, logits, clear_pos, write_pos, size, lse_out, st)) return rc;
   } else {
     hipLaunchKernelGGL(logits_add_running_kernel, dim3(1), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
-                       clear_pos, write_pos, size, lse_out ? lse_out : b->lse);
+                       b->csum, clear_pos, write_pos, size, lse_out ? lse_out : b->lse);
     DQZ_HIP(hipGetLastError());
     ++b->run_adds;
   }
@@ -794,16 +803,29 @@ int dqz_logits_write(dqz_logit_buffer* b, float* logits, const int64_t* position
   if (!b || !logits || (n > 0 && (!positions || !values))) return fail(DQZ_ERR_INVALID, "null argument");
   if (n < 0) return fail(DQZ_ERR_INVALID, "n must be >= 0");
   if (n == 0) return DQZ_OK;
-  hipLaunchKernelGGL(logits_write_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, logits, b->run, positions, values,
-                     n);
+  hipStream_t st = (hipStream_t)stream;
+  if (!b->run_known) {  // no running state to keep: write, and the next use re-seeds
+    hipLaunchKernelGGL(logits_scatter_kernel, dim3(1), dim3(64), 0, st, logits, positions, values, n);
+    DQZ_HIP(hipGetLastError());
+    return DQZ_OK;
+  }
+  hipLaunchKernelGGL(logits_write_kernel, dim3(1), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run, b->dirty,
+                     positions, values, n);
   DQZ_HIP(hipGetLastError());
-  return DQZ_OK;
+  return chunk_sums(b, logits, true, st);
 }
 
 int dqz_logits_put(dqz_logit_buffer* b, float* logits, int64_t position, float value, void* stream) {
   if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
   if (position < 0 || position >= b->capacity) return fail(DQZ_ERR_INVALID, "position out of range");
-  hipLaunchKernelGGL(logits_put1_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, logits, b->run, position, value);
+  hipStream_t st = (hipStream_t)stream;
+  if (!b->run_known) {
+    hipLaunchKernelGGL(logits_scatter1_kernel, dim3(1), dim3(64), 0, st, logits, position, value);
+    DQZ_HIP(hipGetLastError());
+    return DQZ_OK;
+  }
+  hipLaunchKernelGGL(logits_put1_kernel, dim3(1), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run, b->csum,
+                     position, value);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -826,14 +848,17 @@ int dqz_logits_run_get(dqz_logit_buffer* b, double* S, float* c, int* valid, int
   return DQZ_OK;
 }
 
-int dqz_logits_run_set(dqz_logit_buffer* b, double S, float c, int valid, int known, int adds, void* stream) {
-  if (!b) return fail(DQZ_ERR_INVALID, "null argument");
+int dqz_logits_run_set(dqz_logit_buffer* b, const float* logits, double S, float c, int valid, int known, int adds,
+                       void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
   if (adds < 0) return fail(DQZ_ERR_INVALID, "adds must be >= 0");
-  hipLaunchKernelGGL(logits_run_set_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, b->run,
-                     LogitRun{S, c, valid ? 1 : 0});
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(logits_run_set_kernel, dim3(1), dim3(64), 0, st, b->run, LogitRun{S, c, valid ? 1 : 0});
   DQZ_HIP(hipGetLastError());
-  b->run_known = known != 0;
+  b->run_known = known != 0 && valid != 0;
   b->run_adds = adds;
+  // the chunk sums are a function of (logits, c): the restored state's
+  if (b->run_known) return chunk_sums(b, logits, false, st);
   return DQZ_OK;
 }
 
@@ -843,8 +868,8 @@ int dqz_logits_invalidate(dqz_logit_buffer* b) {
   return DQZ_OK;
 }
 
-// The samplers use the running state's lse: seed it with a scan first when
-// the host cannot vouch for it.
+// The samplers use the running state and its chunk sums: seed both with a
+// scan first when the host cannot vouch for them.
 static int ensure_run(dqz_logit_buffer* b, const float* logits, hipStream_t st) {
   if (b->run_known) return DQZ_OK;
   return logits_lse(b, const_cast<float*>(logits), -1, -1, 0, nullptr, st);
@@ -854,12 +879,11 @@ static int logits_sample_impl(dqz_logit_buffer* b, const float* logits, uint64_t
                               const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, hipStream_t st) {
   if (!b || !logits || (!uniforms && !counter_dev) || (!out_slots && !out_idx))
     return fail(DQZ_ERR_INVALID, "null argument");
-  if (n < 1 || n > 65535 - b->nblocks) return fail(DQZ_ERR_INVALID, "n out of range");
+  if (n < 1 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
   if (out_slots && b->capacity > INT32_MAX) return fail(DQZ_ERR_INVALID, "int32 slots need capacity < 2^31");
   if (int rc = ensure_run(b, logits, st)) return rc;
-  hipLaunchKernelGGL(softmax_sample_kernel, dim3(b->nblocks + n), dim3(SM_THREADS), 0, st, logits, b->capacity,
-                     b->run, b->bsum, b->nblocks, SampleSync{b->sync}, seed, counter_dev, uniforms, n, out_slots,
-                     out_idx);
+  hipLaunchKernelGGL(softmax_sample_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run, b->csum,
+                     b->nblocks, SampleSync{b->sync}, seed, counter_dev, uniforms, n, out_slots, out_idx);
   DQZ_HIP(hipGetLastError());
   return DQZ_OK;
 }
@@ -879,10 +903,22 @@ int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, flo
   if (!b || !logits || !p_out) return fail(DQZ_ERR_INVALID, "null argument");
   hipStream_t st = (hipStream_t)stream;
   if (int rc = ensure_run(b, logits, st)) return rc;
-  hipLaunchKernelGGL(prob_block_sum_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
-                     b->lse, b->bsum, p_out);
+  hipLaunchKernelGGL(logit_terms_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
+                     b->csum, b->nblocks, p_out, (float*)nullptr, lse_out, (float*)nullptr);
   DQZ_HIP(hipGetLastError());
-  if (lse_out) DQZ_HIP(hipMemcpyAsync(lse_out, b->lse, sizeof(float), hipMemcpyDeviceToDevice, st));
+  return DQZ_OK;
+}
+
+int dqz_logits_terms(dqz_logit_buffer* b, const float* logits, float* t_out, double* csum_out, float* c_out,
+                     void* stream) {
+  if (!b || !logits || !t_out) return fail(DQZ_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = ensure_run(b, logits, st)) return rc;
+  hipLaunchKernelGGL(logit_terms_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->run,
+                     b->csum, b->nblocks, (float*)nullptr, t_out, (float*)nullptr, c_out);
+  DQZ_HIP(hipGetLastError());
+  if (csum_out)
+    DQZ_HIP(hipMemcpyAsync(csum_out, b->csum, sizeof(double) * b->nblocks, hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }
 
@@ -895,8 +931,8 @@ int dqz_learner_step_logits(dqz_learner* L, const dqz_params* P, const dqz_store
   if (buf->capacity > INT32_MAX) return fail(DQZ_ERR_INVALID, "int32 slots need capacity < 2^31");
   hipStream_t st = (hipStream_t)stream;
   if (int rc = ensure_run(buf, logits, st)) return rc;
-  SoftmaxDraw sm{logits,      buf->capacity, buf->run, buf->bsum, buf->nblocks, Handoff{}, seed,
-                 uniforms ? nullptr : counter_dev, uniforms, slots_out};
+  SoftmaxDraw sm{logits, buf->capacity, buf->run, buf->csum, buf->nblocks,
+                 seed,   uniforms ? nullptr : counter_dev,    uniforms,  slots_out};
   return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0, nullptr, &sm);
 }
 
@@ -1389,9 +1425,13 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.dlogits = H->dl;
   // keep the buffer's running log-sum-exp current (the host keeps vouching
   // for it: every write went through the library)
-  ad.run = logit_buf && logit_buf->run_known ? logit_buf->run : nullptr;
+  const bool keep = logit_buf && logit_buf->run_known;
+  ad.run = keep ? logit_buf->run : nullptr;
+  ad.dirty = keep ? logit_buf->dirty : nullptr;
+  ad.n_logits = keep ? logit_buf->capacity : 0;
   hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
   DQZ_HIP(hipGetLastError());
+  if (keep) return chunk_sums(logit_buf, logits, true, st);
   return DQZ_OK;
 }
 

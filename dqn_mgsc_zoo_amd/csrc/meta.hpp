@@ -219,6 +219,8 @@ struct MetaAdamArgs {
   float* loss;
   float* dlogits;   // [M]
   LogitRun* run;    // the logit buffer's running log-sum-exp, or null
+  int* dirty;       // its chunk flags (chunk_sums_kernel runs after), with run
+  int64_t n_logits; // its capacity
 };
 
 // softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
@@ -254,17 +256,26 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
     if (r.valid) {
       dS += run_term(nx, r.c) - run_term(a.x[i], r.c);
       if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
+      a.dirty[a.pos[i] / SM_CHUNK] = 1;
     }
   }
   // the buffer's running log-sum-exp follows the M writes (what
-  // dqz_logits_write does for them), so the next add / sample needs no scan
+  // dqz_logits_write does for them) and their chunks are flagged, so the next
+  // add / sample needs no scan; a tripped guard re-seeds here (rare)
   if (a.run && r.valid) {
+    __shared__ int s_reseed;
     dS = block_sum_f64(dS, dbuf);  // fixed order: deterministic
     if (threadIdx.x == 0) {
       const double before = r.S;
       r.S += dS;
-      if (s_far || !run_ok(before, r.S, -INFINITY, r.c)) r.valid = 0;
+      s_reseed = s_far || !run_ok(before, r.S, -INFINITY, r.c);
       *a.run = r;
+    }
+    __syncthreads();
+    if (s_reseed) {
+      block_rescan(a.logits, a.n_logits, a.run);
+      const int nb = (int)((a.n_logits + SM_CHUNK - 1) / SM_CHUNK);
+      for (int k = threadIdx.x; k < nb; k += META_THREADS) a.dirty[k] = 1;
     }
   }
   if (threadIdx.x == 0) {

@@ -1,17 +1,13 @@
 // sampling.hpp — device replay samplers.
 //
 //  * learned-logit buffers (replay_circular.py:148-248, 500-565): f32 logits
-//    in HBM (-inf = empty slot).  log-sum-exp is a two-pass online (max, sum)
-//    reduction; softmax sampling forms p = exp(x - lse) in f32 exactly as the
-//    reference's probabilities_from_logits, then the float64 CDF that
-//    numpy's choice builds (sequential cumsum, normalise by the last entry,
-//    searchsorted right).  The device sums p in blocks; that equals numpy's
-//    sequential fp64 cumsum bit for bit whenever no partial sum rounds
-//    (every nonzero p a multiple of ulp(total): logits spanning < ~20 nats
-//    at 1M slots).  Otherwise both orders round a few tiny p by at most half
-//    an ulp of the running sum each, and a draw can differ only if u lies
-//    within those few ulps of a CDF boundary (~1e-16 of the total against
-//    boundary gaps of ~1e-6 at 1M slots).
+//    in HBM (-inf = empty slot).  The log-sum-exp (the default logit of an
+//    add) is a running float64 sum about a fixed shift c, seeded by a
+//    two-pass (max, sum) scan.  A draw is numpy's choice (float64 CDF,
+//    normalised by its last entry, searchsorted right) over the terms
+//    expf(x - c): softmax(logits) up to f32 rounding of the exponent, as the
+//    reference's probabilities_from_logits is.  Per-chunk sums of those terms
+//    are kept at write time, so a draw reads one chunk, not the buffer.
 //  * prioritized replay (replay.py:379-559): the fp64 implicit sum tree in
 //    HBM, same node layout as the host SumTree; set recomputes every touched
 //    ancestor as left + right, so device and host sums are bit-identical.
@@ -127,13 +123,19 @@ __device__ __forceinline__ MaxSum combine_parts(const MaxSum* __restrict__ part,
 // S from the scan) whenever the host-side owner cannot vouch for it (logits
 // handed out for writing, e.g. to the meta-update; set_state), every
 // kLogitReseed running adds (bounds the drift), and on the device when a
-// removal would cancel most of S or an item lands far above c (valid = 0:
-// the next add rescans inside its own block).
+// removal would cancel most of S or an item lands far above c (the writer
+// re-seeds in its own block before it returns, so a sampler always finds a
+// valid state and chunk sums about its c).
 struct LogitRun {
   double S;
   float c;
   int valid;
 };
+
+// The f32 log-sum-exp of a running state: c + log(S) in float64, rounded once.
+__device__ __forceinline__ float run_lse(const LogitRun& r) {
+  return r.S > 0.0 ? (float)((double)r.c + log(r.S)) : -INFINITY;
+}
 
 // The reference's default logit (replay_circular.py:171-176): the float32
 // logsumexp minus np.log(size) in float64, stored back as float32.
@@ -167,187 +169,6 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
   }
 }
 
-// Guard of a running update: S must stay well conditioned (no removal that
-// cancels most of it) and terms within exp's range about c.
-__device__ __forceinline__ bool run_ok(double s_before, double s_after, float x, float c) {
-  return s_after >= 1e-6 * s_before && s_after > 0.0 && (x == -INFINITY || (double)x - (double)c < 80.0);
-}
-
-// add / reservoir replace with the running state (one block).  If `run` is
-// not valid (a guard tripped), the block rescans the buffer itself first.
-__global__ __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* __restrict__ x, int64_t n,
-                                                                        LogitRun* run, int64_t clear_pos,
-                                                                        int64_t write_pos, int64_t size,
-                                                                        float* lse_out) {
-  __shared__ int s_valid;
-  __shared__ double dbuf[SM_THREADS / 64];
-  __shared__ float fbuf[SM_THREADS / 64];
-  if (threadIdx.x == 0) {
-    LogitRun r = *run;
-    if (r.valid && clear_pos >= 0) {
-      const double before = r.S;
-      r.S -= run_term(x[clear_pos], r.c);
-      if (!run_ok(before, r.S, -INFINITY, r.c) && r.S != 0.0) r.valid = 0;
-    }
-    if (clear_pos >= 0) x[clear_pos] = -INFINITY;
-    s_valid = r.valid;
-    *run = r;
-  }
-  __syncthreads();
-  if (!s_valid) {  // rescan: c = max, S = sum exp(x - c) in float64
-    float m = -INFINITY;
-    for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, x[j]);
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
-    __syncthreads();
-    m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
-    const float c = m == -INFINITY ? 0.f : m;
-    double sum = 0.0;
-    for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(x[j], c);
-    sum = block_sum_f64(sum, dbuf);
-    if (threadIdx.x == 0) *run = LogitRun{sum, c, 1};
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    LogitRun r = *run;
-    const float lse = r.S > 0.0 ? (float)((double)r.c + log(r.S)) : -INFINITY;
-    if (lse_out) *lse_out = lse;
-    if (write_pos >= 0) {
-      const float item = logmeanexp_item(lse, size);
-      const double before = r.S;
-      r.S += run_term(item, r.c) - run_term(x[write_pos], r.c);
-      x[write_pos] = item;
-      if (!run_ok(before, r.S, item, r.c)) r.valid = 0;
-    }
-    *run = r;
-  }
-}
-
-// One write x[pos] = v passed by value (popleft's -inf), keeping the running state.
-__global__ void logits_put1_kernel(float* __restrict__ x, LogitRun* run, int64_t pos, float v) {
-  if (threadIdx.x != 0) return;
-  LogitRun r = *run;
-  if (r.valid) {
-    const double before = r.S;
-    r.S += run_term(v, r.c) - run_term(x[pos], r.c);
-    if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
-  }
-  x[pos] = v;
-  *run = r;
-}
-
-// Explicit writes x[pos[i]] = val[i] in order (a repeated slot keeps its last
-// value, as numpy fancy assignment does), keeping the running state.
-__global__ void logits_write_kernel(float* __restrict__ x, LogitRun* run, const int64_t* __restrict__ pos,
-                                    const float* __restrict__ val, int n) {
-  if (threadIdx.x != 0) return;
-  LogitRun r = *run;
-  for (int i = 0; i < n; ++i) {
-    const int64_t j = pos[i];
-    const float v = val[i];
-    if (r.valid) {
-      const double before = r.S;
-      r.S += run_term(v, r.c) - run_term(x[j], r.c);
-      if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
-    }
-    x[j] = v;
-  }
-  *run = r;
-}
-
-// Uniform doubles in [0, 1) from Philox (53-bit mantissa), counter advanced on device.
-__global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, double* out) {
-  const uint64_t ctr = *counter;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x50F7u),
-                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-    out[i] = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) *counter = ctr + 1;
-}
-
-// p of one logit as every sampling kernel forms it (f32, like the reference's
-// probabilities_from_logits), widened to float64 like numpy's choice.
-__device__ __forceinline__ float prob_f32(float x, float L) { return expf(x - L); }
-
-// The f32 log-sum-exp of a running state: c + log(S) in float64, rounded once.
-__device__ __forceinline__ float run_lse(const LogitRun& r) {
-  return r.S > 0.0 ? (float)((double)r.c + log(r.S)) : -INFINITY;
-}
-
-// lse of the buffer as the samplers use it: the running state's when it is
-// valid (the host re-seeds it with a scan whenever it cannot vouch for it), or
-// — when a device-side guard invalidated it since (a removal that cancelled
-// most of S) — a full scan by this block: max, then float64 sum of exp(x - max)
-// in one fixed order, so every block of a launch gets the same bits.  Rare.
-__device__ __forceinline__ float sample_lse(const float* __restrict__ x, int64_t n, const LogitRun* run) {
-  __shared__ float s_L;
-  __shared__ float fbuf[SM_THREADS / 64];
-  __shared__ double dbuf[SM_THREADS / 64];
-  const LogitRun r = *run;
-  if (r.valid) return run_lse(r);
-  float m = -INFINITY;
-  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, x[j]);
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
-  const float c = m == -INFINITY ? 0.f : m;
-  double sum = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(x[j], c);
-  sum = block_sum_f64(sum, dbuf);
-  if (threadIdx.x == 0) s_L = run_lse(LogitRun{sum, c, 1});
-  __syncthreads();
-  return s_L;
-}
-
-// float64 sum of the f32 p of chunk b (SM_CHUNK logits, lane t holding the
-// float4s t, t + 256, ...), in one fixed order; optionally stores every p.
-__device__ __forceinline__ double chunk_prob_sum(const float* __restrict__ x, int64_t n, int b, float L,
-                                                 float* __restrict__ p_out, double* dbuf) {
-  const int64_t base = (int64_t)b * SM_CHUNK;
-  double acc = 0.0;
-#pragma unroll
-  for (int q = 0; q < SM_CHUNK / SM_THREADS / 4; ++q) {
-    const int64_t j = base + 4 * (threadIdx.x + SM_THREADS * q);
-    float4 f = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    if (j + 3 < n && (reinterpret_cast<uintptr_t>(x + j) & 15) == 0) {
-      f = *reinterpret_cast<const float4*>(x + j);
-    } else {
-      if (j < n) f.x = x[j];
-      if (j + 1 < n) f.y = x[j + 1];
-      if (j + 2 < n) f.z = x[j + 2];
-      if (j + 3 < n) f.w = x[j + 3];
-    }
-    const float p0 = prob_f32(f.x, L), p1 = prob_f32(f.y, L), p2 = prob_f32(f.z, L), p3 = prob_f32(f.w, L);
-    acc += (double)p0;
-    acc += (double)p1;
-    acc += (double)p2;
-    acc += (double)p3;
-    if (p_out) {
-      if (j < n) p_out[j] = p0;
-      if (j + 1 < n) p_out[j + 1] = p1;
-      if (j + 2 < n) p_out[j + 2] = p2;
-      if (j + 3 < n) p_out[j + 3] = p3;
-    }
-  }
-  return block_sum_f64(acc, dbuf);
-}
-
-// Per-block float64 sums of p with the running lse (diagnostic
-// dqz_logits_probs: p_out gets the f32 p of every slot, block 0 the lse).
-__global__ __launch_bounds__(SM_THREADS) void prob_block_sum_kernel(const float* __restrict__ x, int64_t n,
-                                                                    const LogitRun* run, float* __restrict__ lse_out,
-                                                                    double* __restrict__ bsum,
-                                                                    float* __restrict__ p_out) {
-  __shared__ double dbuf[SM_THREADS / 64];
-  const float L = sample_lse(x, n, run);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *lse_out = L;
-  const double acc = chunk_prob_sum(x, n, blockIdx.x, L, p_out, dbuf);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = acc;
-}
-
 // Scan of one double per thread over the block in a fixed order
 // (deterministic run to run): a Hillis-Steele scan inside each wave by
 // shuffles, then each wave adds the totals of the waves before it, summed in
@@ -379,57 +200,30 @@ __device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, 
   return excl;
 }
 
-// One query u: find the chunk whose normalised cumulative sum first exceeds
-// u, then inside the chunk the lane (16 logits each) and the logit.  Both
-// levels are parallel: each lane sums a contiguous run of block sums / holds
-// 16 logits (four float4 loads), a block-wide scan gives the exclusive
-// prefixes, and the first crossing is the minimum index any lane finds.
-// Returns the first index with cdf > u (searchsorted side='right'); cdf =
-// cumsum(float64 p) / total.
+// ---------------------------------------------------------------------------
+// Chunk sums of the sampling terms, kept at write time.
+//
+// A draw's distribution is softmax(logits) formed as terms t_i = expf(x_i - c)
+// (f32, widened to float64; 0 for an empty slot) about the running state's
+// shift c, and the float64 CDF over them.  The buffer keeps one float64 sum
+// per chunk of SM_CHUNK logits: csum[k] = chunk_sum(k) — lane t sums its 16
+// consecutive terms in index order, then block_scan_excl_f64's fixed-order
+// total — a pure function of (logits, c).  Every write recomputes the chunks
+// it touched (the add / put kernels in their own block; the explicit writes
+// and the meta-update through dirty flags and chunk_sums_kernel), and a
+// re-seed (new c) recomputes all of them.  A draw is then a two-level search
+// (csum prefix -> chunk, chunk terms -> slot) whose second level re-forms
+// exactly the terms csum[k] was summed from: no pass over the buffer per draw,
+// where the reference forms the softmax of every slot for every sample
+// (replay_circular.py:205-217, 540-545).
 constexpr int SM_PER_LANE = SM_CHUNK / SM_THREADS;  // 16
 
-// bsum is read with agent-scope (L2-bypassing) loads: in the fused sampler
-// its producers are other workgroups of the same launch.
-__device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, float L,
-                                                       const double* bsum, int nblocks, double u) {
-  __shared__ double s_wave[SM_THREADS / 64];
-  __shared__ double s_before;
-  __shared__ int s_blk;
-  __shared__ unsigned long long s_idx;
-  const int t = threadIdx.x;
-  // level 1: lane t owns block sums [t seg, (t + 1) seg)
-  const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
-  const int b0 = min(t * seg, nblocks), b1 = min(b0 + seg, nblocks);
-  double mine = 0.0;
-  double mb[8];  // this lane's block sums (seg <= 8 up to 8M logits), else re-read
-  for (int b = b0; b < b1; ++b) {
-    const double v = load_fresh(bsum + b);
-    if (b - b0 < 8) mb[b - b0] = v;
-    mine += v;
-  }
-  if (t == 0) {
-    s_blk = nblocks - 1;
-    s_idx = ~0ull;
-  }
-  double tot;
-  const double excl = block_scan_excl_f64(mine, s_wave, &tot);
-  {
-    double run = excl;
-    for (int b = b0; b < b1; ++b) {
-      const double v = b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
-      if ((run + v) / tot > u) {
-        atomicMin(&s_blk, b);
-        break;
-      }
-      run += v;
-    }
-  }
-  // level 2 loads do not depend on the crossing lane's prefix: issue them
-  // as soon as the chunk is known
-  __syncthreads();
-  const int blk = s_blk;
-  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
-  float xv[SM_PER_LANE];
+__device__ __forceinline__ double chunk_term(float x, float c) { return x == -INFINITY ? 0.0 : (double)expf(x - c); }
+
+// Lane t's 16 consecutive logits of chunk k (-inf past n): four float4 loads.
+__device__ __forceinline__ void load_chunk_lane(const float* __restrict__ x, int64_t n, int k,
+                                                float (&xv)[SM_PER_LANE]) {
+  const int64_t base = (int64_t)k * SM_CHUNK + threadIdx.x * SM_PER_LANE;
   if (base + SM_PER_LANE <= n && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
 #pragma unroll
     for (int q = 0; q < SM_PER_LANE / 4; ++q) {
@@ -443,33 +237,320 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < SM_PER_LANE; ++i) xv[i] = base + i < n ? x[base + i] : -INFINITY;
   }
-  if (blk >= b0 && blk < b1) {  // the owner of the crossing block publishes the mass before it
-    double run = excl;
-    for (int b = b0; b < blk; ++b) run += b - b0 < 8 ? mb[b - b0] : load_fresh(bsum + b);
-    s_before = run;
+}
+
+// The canonical sum of chunk k's terms (all 256 threads; every thread gets it).
+__device__ __forceinline__ double chunk_sum(const float* __restrict__ x, int64_t n, int k, float c, double* s_wave) {
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, k, xv);
+  double lane = 0.0;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], c);
+  double tot;
+  (void)block_scan_excl_f64(lane, s_wave, &tot);
+  return tot;
+}
+
+// One block per chunk: csum[k] = chunk_sum(k) about the running state's c;
+// with `dirty`, only the chunks flagged by a writer (flags cleared).
+__global__ __launch_bounds__(SM_THREADS) void chunk_sums_kernel(const float* __restrict__ x, int64_t n,
+                                                                const LogitRun* run, double* __restrict__ csum,
+                                                                int* __restrict__ dirty) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  const int k = blockIdx.x;
+  if (dirty && dirty[k] == 0) return;
+  const double s = chunk_sum(x, n, k, run->c, s_wave);
+  if (threadIdx.x == 0) {
+    csum[k] = s;
+    if (dirty) dirty[k] = 0;
   }
-  // level 2: the chunk's 256 lanes x 16 logits
+}
+
+// Re-seed of the running state by one block (a guard tripped inside a
+// single-block writer; rare): c = max, S = float64 sum of exp(x - c).
+// Returns c to every thread.
+__device__ __forceinline__ float block_rescan(const float* __restrict__ x, int64_t n, LogitRun* run) {
+  __shared__ float fbuf[SM_THREADS / 64];
+  __shared__ double dbuf[SM_THREADS / 64];
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, x[j]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
+  const float c = m == -INFINITY ? 0.f : m;
+  double sum = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(x[j], c);
+  sum = block_sum_f64(sum, dbuf);
+  if (threadIdx.x == 0) *run = LogitRun{sum, c, 1};
+  __syncthreads();
+  return c;
+}
+
+// Every chunk in turn, by one block (after block_rescan).
+__device__ __forceinline__ void block_all_chunk_sums(const float* __restrict__ x, int64_t n, float c,
+                                                     double* __restrict__ csum) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  const int nb = (int)((n + SM_CHUNK - 1) / SM_CHUNK);
+  for (int k = 0; k < nb; ++k) {
+    const double s = chunk_sum(x, n, k, c, s_wave);
+    if (threadIdx.x == 0) csum[k] = s;
+  }
+}
+
+// Guard of a running update: S must stay well conditioned (no removal that
+// cancels most of it) and terms within exp's range about c (the f32 sampling
+// terms included: expf(80) is finite).
+__device__ __forceinline__ bool run_ok(double s_before, double s_after, float x, float c) {
+  return s_after >= 1e-6 * s_before && s_after > 0.0 && (x == -INFINITY || (double)x - (double)c < 80.0);
+}
+
+// add / reservoir replace with the running state (one block), then the chunk
+// sums of the (at most two) chunks it wrote.  A tripped guard re-seeds the
+// state and every chunk sum in this block (rare).
+__global__ __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* __restrict__ x, int64_t n,
+                                                                        LogitRun* run, double* __restrict__ csum,
+                                                                        int64_t clear_pos, int64_t write_pos,
+                                                                        int64_t size, float* lse_out) {
+  __shared__ int s_valid;
+  __shared__ float s_c;
+  __shared__ double s_wave[SM_THREADS / 64];
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    if (r.valid && clear_pos >= 0) {
+      const double before = r.S;
+      r.S -= run_term(x[clear_pos], r.c);
+      if (!run_ok(before, r.S, -INFINITY, r.c) && r.S != 0.0) r.valid = 0;
+    }
+    if (clear_pos >= 0) x[clear_pos] = -INFINITY;
+    s_valid = r.valid;
+    *run = r;
+  }
+  __syncthreads();
+  bool all = false;
+  if (!s_valid) {
+    block_rescan(x, n, run);
+    all = true;
+  }
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    const float lse = run_lse(r);
+    if (lse_out) *lse_out = lse;
+    if (write_pos >= 0) {
+      const float item = logmeanexp_item(lse, size);
+      const double before = r.S;
+      r.S += run_term(item, r.c) - run_term(x[write_pos], r.c);
+      x[write_pos] = item;
+      if (!run_ok(before, r.S, item, r.c)) r.valid = 0;
+    }
+    *run = r;
+    s_valid = r.valid;
+    s_c = r.c;
+  }
+  __syncthreads();
+  if (!s_valid) {
+    s_c = 0.f;  // every thread has read s_valid; block_rescan's barrier orders this store
+    const float c = block_rescan(x, n, run);
+    block_all_chunk_sums(x, n, c, csum);
+    return;
+  }
+  const float c = s_c;
+  if (all) {
+    block_all_chunk_sums(x, n, c, csum);
+    return;
+  }
+  const int kw = write_pos >= 0 ? (int)(write_pos / SM_CHUNK) : -1;
+  const int kc = clear_pos >= 0 ? (int)(clear_pos / SM_CHUNK) : -1;
+  if (kc >= 0 && kc != kw) {
+    const double s = chunk_sum(x, n, kc, c, s_wave);
+    if (threadIdx.x == 0) csum[kc] = s;
+  }
+  if (kw >= 0) {
+    const double s = chunk_sum(x, n, kw, c, s_wave);
+    if (threadIdx.x == 0) csum[kw] = s;
+  }
+}
+
+// One write x[pos] = v passed by value (popleft's -inf), keeping the running
+// state and the chunk sum (one block).
+__global__ __launch_bounds__(SM_THREADS) void logits_put1_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
+                                                                 double* __restrict__ csum, int64_t pos, float v) {
+  __shared__ int s_valid;
+  __shared__ float s_c;
+  __shared__ double s_wave[SM_THREADS / 64];
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    if (r.valid) {
+      const double before = r.S;
+      r.S += run_term(v, r.c) - run_term(x[pos], r.c);
+      if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
+    }
+    x[pos] = v;
+    *run = r;
+    s_valid = r.valid;
+    s_c = r.c;
+  }
+  __syncthreads();
+  if (!s_valid) {
+    const float c = block_rescan(x, n, run);
+    block_all_chunk_sums(x, n, c, csum);
+    return;
+  }
+  const int k = (int)(pos / SM_CHUNK);
+  const double s = chunk_sum(x, n, k, s_c, s_wave);
+  if (threadIdx.x == 0) csum[k] = s;
+}
+
+// Explicit writes x[pos[i]] = val[i] in order (a repeated slot keeps its last
+// value, as numpy fancy assignment does), keeping the running state; the
+// written chunks are flagged for chunk_sums_kernel (all of them after a
+// re-seed).
+__global__ __launch_bounds__(SM_THREADS) void logits_write_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
+                                                                  int* __restrict__ dirty,
+                                                                  const int64_t* __restrict__ pos,
+                                                                  const float* __restrict__ val, int m) {
+  __shared__ int s_valid;
+  if (threadIdx.x == 0) {
+    LogitRun r = *run;
+    for (int i = 0; i < m; ++i) {
+      const int64_t j = pos[i];
+      const float v = val[i];
+      if (r.valid) {
+        const double before = r.S;
+        r.S += run_term(v, r.c) - run_term(x[j], r.c);
+        if (!run_ok(before, r.S, v, r.c)) r.valid = 0;
+      }
+      x[j] = v;
+      dirty[j / SM_CHUNK] = 1;
+    }
+    *run = r;
+    s_valid = r.valid;
+  }
+  __syncthreads();
+  if (!s_valid) {
+    block_rescan(x, n, run);
+    const int nb = (int)((n + SM_CHUNK - 1) / SM_CHUNK);
+    for (int k = threadIdx.x; k < nb; k += SM_THREADS) dirty[k] = 1;
+  }
+}
+
+// Plain writes while the host cannot vouch for the running state (the next
+// use re-seeds it and every chunk sum).
+__global__ void logits_scatter_kernel(float* __restrict__ x, const int64_t* __restrict__ pos,
+                                      const float* __restrict__ val, int m) {
+  if (threadIdx.x == 0)
+    for (int i = 0; i < m; ++i) x[pos[i]] = val[i];  // in order: a repeated slot keeps its last value
+}
+
+__global__ void logits_scatter1_kernel(float* __restrict__ x, int64_t pos, float v) {
+  if (threadIdx.x == 0) x[pos] = v;
+}
+
+// Uniform double in [0, 1) of draw q at Philox step ctr (53-bit mantissa):
+// the dqz_uniform_philox stream.
+__device__ __forceinline__ double philox_uniform(uint64_t seed, uint64_t ctr, int q) {
+  const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)q, 0x50F7u),
+                             make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+  return ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+}
+
+// Uniform doubles in [0, 1) from Philox, counter advanced on device.
+__global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, double* out) {
+  const uint64_t ctr = *counter;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = philox_uniform(seed, ctr, i);
+  __syncthreads();
+  if (threadIdx.x == 0) *counter = ctr + 1;
+}
+
+// Level 1 of a draw over the chunk sums: lane t sums csum[t seg, (t + 1) seg)
+// in order; the block scan gives its exclusive prefix and the total (the
+// draw's normaliser; every diagnostic forms it the same way).
+struct CsumLane {
+  int b0, b1;
+  double mb[8];  // this lane's chunk sums (seg <= 8 up to 8M logits), else re-read
+  double excl, tot;
+};
+
+__device__ __forceinline__ CsumLane csum_scan(const double* __restrict__ csum, int nblocks, double* s_wave) {
+  CsumLane l;
+  const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
+  l.b0 = min((int)threadIdx.x * seg, nblocks);
+  l.b1 = min(l.b0 + seg, nblocks);
+  double mine = 0.0;
+  for (int b = l.b0; b < l.b1; ++b) {
+    const double v = csum[b];
+    if (b - l.b0 < 8) l.mb[b - l.b0] = v;
+    mine += v;
+  }
+  l.excl = block_scan_excl_f64(mine, s_wave, &l.tot);
+  return l;
+}
+
+__device__ __forceinline__ double csum_at(const CsumLane& l, const double* __restrict__ csum, int b) {
+  return b - l.b0 < 8 ? l.mb[b - l.b0] : csum[b];
+}
+
+// One query u: the first slot whose normalised cumulative term sum exceeds u
+// (searchsorted side='right' on cumsum(t) / total, as numpy's choice does on
+// its p).  Level 1 finds the chunk from the csum prefix (the minimum chunk
+// any lane sees the crossing in), level 2 the lane (16 terms each) and the
+// slot from the chunk's re-formed terms, whose scan total is csum[chunk].
+__device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, const LogitRun* run,
+                                                       const double* __restrict__ csum, int nblocks, double u) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  __shared__ double s_before;
+  __shared__ int s_blk;
+  __shared__ unsigned long long s_idx;
+  __shared__ int64_t s_out;
+  const int t = threadIdx.x;
+  const float c = run->c;
+  if (t == 0) {
+    s_blk = nblocks - 1;
+    s_idx = ~0ull;
+  }
+  const CsumLane l = csum_scan(csum, nblocks, s_wave);
+  const double tot = l.tot;
+  {
+    double acc = l.excl;
+    for (int b = l.b0; b < l.b1; ++b) {
+      const double v = csum_at(l, csum, b);
+      if ((acc + v) / tot > u) {
+        atomicMin(&s_blk, b);
+        break;
+      }
+      acc += v;
+    }
+  }
+  __syncthreads();
+  const int blk = s_blk;
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, blk, xv);  // independent of the prefix: issued first
+  if (blk >= l.b0 && blk < l.b1) {  // the owner of the crossing chunk publishes the mass before it
+    double acc = l.excl;
+    for (int b = l.b0; b < blk; ++b) acc += csum_at(l, csum, b);
+    s_before = acc;
+  }
   double p[SM_PER_LANE];
   double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) {
-    p[i] = xv[i] == -INFINITY ? 0.0 : (double)prob_f32(xv[i], L);
+    p[i] = chunk_term(xv[i], c);
     lane += p[i];
   }
   double tot2;
   const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);  // its barriers publish s_before
-  double run = s_before + lexcl;
-  if (run / tot <= u && (run + lane) / tot > u) {
+  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
+  double acc = s_before + lexcl;
+  if (acc / tot <= u && (acc + lane) / tot > u) {
     for (int i = 0; i < SM_PER_LANE; ++i) {
-      run += p[i];
-      if (run / tot > u) {
+      acc += p[i];
+      if (acc / tot > u) {
         atomicMin(&s_idx, (unsigned long long)(base + i));
         break;
       }
     }
   }
   __syncthreads();
-  __shared__ int64_t s_out;
   if (t == 0) {
     int64_t idx = s_idx == ~0ull ? -1 : (int64_t)s_idx;
     if (idx < 0) {  // rounding at the chunk edge: last live slot of the chunk
@@ -486,112 +567,87 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
   return s_out;
 }
 
+// Diagnostics (dqz_logits_probs / dqz_logits_terms), one block per chunk:
+// p = t / total as f32 (the draw's distribution), the terms t themselves, the
+// running lse and c.
+__global__ __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __restrict__ x, int64_t n,
+                                                                 const LogitRun* run, const double* __restrict__ csum,
+                                                                 int nblocks, float* __restrict__ p_out,
+                                                                 float* __restrict__ t_out, float* lse_out,
+                                                                 float* c_out) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  const LogitRun r = *run;
+  const CsumLane l = csum_scan(csum, nblocks, s_wave);
+  const int k = blockIdx.x;
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, k, xv);
+  const int64_t base = (int64_t)k * SM_CHUNK + threadIdx.x * SM_PER_LANE;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) {
+    if (base + i < n) {
+      const double ti = chunk_term(xv[i], r.c);
+      if (p_out) p_out[base + i] = (float)(ti / l.tot);
+      if (t_out) t_out[base + i] = (float)ti;
+    }
+  }
+  if (k == 0 && threadIdx.x == 0) {
+    if (lse_out) *lse_out = run_lse(r);
+    if (c_out) *c_out = r.c;
+  }
+}
+
 // The learned-logit draw fused into the learner's forward launch
-// (dqz_learner_step_logits): fwd_conv_kernel gets `nblocks` producer blocks
-// in front (chunk_prob_sum, as softmax_sample_kernel's producers) and every
-// conv1 block of sample b waits for their arrivals, draws uniform b of step
-// *counter (the dqz_uniform_philox stream) and runs the CDF search itself
-// before its frame gather.  The head advances *counter once every conv1
-// block has read it.
+// (dqz_learner_step_logits): every conv1 block of sample b draws uniform b
+// of step *counter (the dqz_uniform_philox stream) or takes the caller's,
+// and runs the two-level search itself before its frame gather.  The head
+// advances *counter once every conv1 block has read it.
 struct SoftmaxDraw {
-  const float* x;        // logits [n]
+  const float* x;         // logits [n]
   int64_t n;
   const LogitRun* run;
-  double* bsum;          // [nblocks] chunk sums (written by the producers)
+  const double* csum;     // [nblocks] chunk sums
   int nblocks;
-  Handoff sync;          // one word: need = nblocks, consumers = the conv1 blocks
   uint64_t seed;
-  uint64_t* counter;     // Philox step counter (null when `uniforms` is set)
+  uint64_t* counter;      // Philox step counter (null when `uniforms` is set)
   const double* uniforms;  // the caller's uniforms [B] (a host Generator's draws), or null
-  int32_t* slots_out;    // [B]: block (rb 0, z 0) of sample b publishes its slot
+  int32_t* slots_out;     // [B]: block (rb 0, z 0) of sample b publishes its slot
 };
 
-__device__ __forceinline__ void softmax_draw_produce(const SoftmaxDraw& d, int blk) {
-  __shared__ double dbuf[SM_THREADS / 64];
-  const float L = sample_lse(d.x, d.n, d.run);
-  const double acc = chunk_prob_sum(d.x, d.n, blk, L, nullptr, dbuf);
-  if (threadIdx.x == 0) __hip_atomic_store(d.bsum + blk, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  d.sync.arrive(0);
-}
-
 __device__ __forceinline__ int32_t softmax_draw_slot(const SoftmaxDraw& d, int b) {
-  double u;
-  if (d.uniforms) {
-    u = d.uniforms[b];
-  } else {
-    const uint64_t ctr = *d.counter;
-    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)b, 0x50F7u),
-                               make_uint2((unsigned)d.seed, (unsigned)(d.seed >> 32)));
-    u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
-  }
-  const float L = sample_lse(d.x, d.n, d.run);
-  d.sync.wait(0);
-  return (int32_t)softmax_choice_body(d.x, d.n, L, d.bsum, d.nblocks, u);
+  const double u = d.uniforms ? d.uniforms[b] : philox_uniform(d.seed, *d.counter, b);
+  return (int32_t)softmax_choice_body(d.x, d.n, d.run, d.csum, d.nblocks, u);
 }
 
-// Learned-logit batch draw in one launch (replay_circular.py:205-217,
-// 540-545: Generator.choice(C, n, p=softmax(logits))).  Blocks [0, nb) are
-// producers: chunk b's float64 sum of p, stored agent-scope, then an arrival
-// on the launch's counter.  Blocks [nb, nb + n) are the n queries: draw q's
-// uniform (the caller's, or Philox (seed, *counter, q) — the stream
-// dqz_uniform_philox produces), wait for all nb arrivals, then the two-level
-// CDF search.  Workgroups are dispatched in index order and producers never
-// wait, so every wait ends; the spin is bounded anyway (the error word gets
-// 1).  The last query to finish resets the counters and advances *counter,
-// so graph replays start clean.
+// Learned-logit batch draw (replay_circular.py:205-217, 540-545:
+// Generator.choice(C, n, p=softmax(logits))), one block per query: the
+// caller's uniform or Philox (seed, *counter, q), then the two-level search.
+// The last query to finish resets the done word and advances *counter, so
+// graph replays start clean.
 struct SampleSync {
-  static constexpr int kStride = 64;  // cnt / done / err on their own 256-byte lines
+  static constexpr int kStride = 64;  // done / err words on their own 256-byte lines
   int* words;
 };
 
 __global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
-    const float* __restrict__ x, int64_t n, const LogitRun* run, double* bsum, int nblocks, SampleSync sync,
-    uint64_t seed, uint64_t* counter, const double* __restrict__ uniforms, int nq, int32_t* __restrict__ out_slots,
-    int64_t* __restrict__ out_idx) {
-  __shared__ double dbuf[SM_THREADS / 64];
-  int* cnt = sync.words;
+    const float* __restrict__ x, int64_t n, const LogitRun* run, const double* __restrict__ csum, int nblocks,
+    SampleSync sync, uint64_t seed, uint64_t* counter, const double* __restrict__ uniforms, int nq,
+    int32_t* __restrict__ out_slots, int64_t* __restrict__ out_idx) {
   int* done = sync.words + SampleSync::kStride;
-  int* err = sync.words + 2 * SampleSync::kStride;
-  const float L = sample_lse(x, n, run);
-  const int b = blockIdx.x;
-  if (b < nblocks) {
-    const double acc = chunk_prob_sum(x, n, b, L, nullptr, dbuf);
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(bsum + b, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  const int q = b - nblocks;
-  double u;
+  const int q = blockIdx.x;
   uint64_t ctr = 0;
+  double u;
   if (uniforms) {
     u = uniforms[q];
   } else {
     ctr = *counter;
-    const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)q, 0x50F7u),
-                               make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-    u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+    u = philox_uniform(seed, ctr, q);
   }
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nblocks) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  const int64_t idx = softmax_choice_body(x, n, L, bsum, nblocks, u);
+  const int64_t idx = softmax_choice_body(x, n, run, csum, nblocks, u);
   if (threadIdx.x == 0) {
     if (out_slots) out_slots[q] = (int32_t)idx;
     if (out_idx) out_idx[q] = idx;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nq - 1) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!uniforms) *counter = ctr + 1;
     }

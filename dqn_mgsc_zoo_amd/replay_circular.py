@@ -117,7 +117,8 @@ class _DeviceLogits:
 
   def set_run_state(self, st):
     n = self._native
-    n.check(n.lib().dqz_logits_run_set(self._h, float(st['S']), float(st['c']),
+    n.check(n.lib().dqz_logits_run_set(self._h, n.ptr(self.logits),
+                                       float(st['S']), float(st['c']),
                                        int(st['valid']), int(st['known']),
                                        int(st['adds']), n.stream_handle()))
 
@@ -139,8 +140,22 @@ class _DeviceLogits:
                                 device=self.device)
     return self.logits[pos].cpu().numpy()
 
+  def terms(self):
+    """(t, csum, c): the f32 terms expf(x - c) a draw's CDF is built from,
+    the float64 chunk sums and the shift (diagnostic; device tensors)."""
+    t = self._torch.empty_like(self.logits)
+    nb = (self.logits.numel() + 4095) // 4096
+    csum = self._torch.empty((nb,), dtype=self._torch.float64, device=self.device)
+    c = self._torch.empty((1,), dtype=self._torch.float32, device=self.device)
+    nat = self._native
+    nat.check(nat.lib().dqz_logits_terms(self._h, nat.ptr(self.logits), nat.ptr(t),
+                                         nat.ptr(csum), nat.ptr(c),
+                                         nat.stream_handle()))
+    return t, csum, c
+
   def probs(self):
-    """(p, lse) as dqz_logits_sample forms them (diagnostic; device tensors)."""
+    """(p, lse): the sampling probabilities (f32) and the running
+    log-sum-exp (diagnostic; device tensors)."""
     p = self._torch.empty_like(self.logits)
     lse = self._torch.empty((1,), dtype=self._torch.float32, device=self.device)
     nat = self._native

@@ -151,8 +151,8 @@ int dqz_learner_step_per(dqz_learner* learner, const dqz_params* params, const d
  * dqz_logits_sample_slots(buf, logits, seed, counter_dev, NULL, B,
  * slots_out, ...) — Philox uniform b of step *counter_dev (or uniforms[b]
  * when `uniforms`, device f64 [B], is given: the replay Generator's own
- * draws), the CDF search of dqz_logits_sample — computed by the forward's
- * conv1 workgroups behind in-launch producer blocks (no sampler launch);
+ * draws), the CDF search of dqz_logits_sample — computed by each of the
+ * forward's conv1 workgroups before its frame gather (no sampler launch);
  * slots_out (device int32 [B]) receives the slots and *counter_dev advances
  * by one (Philox mode).  buf / logits: the replay's learned-logit buffer. */
 typedef struct dqz_logit_buffer dqz_logit_buffer;
@@ -277,7 +277,9 @@ int dqz_gather_stacks(const dqz_store* store, const int32_t* slots, int n, int w
 /* ---- learned-logit replay sampling (dqn_mgsc_batched replays) ----------
  * logits: device f32 [capacity], -inf marks an empty slot
  * (CircularLogitBuffer / MGSCReservoirDistribution, replay_circular.py:148-248,
- * 500-565).  A dqz_logit_buffer owns only the reduction scratch. */
+ * 500-565).  A dqz_logit_buffer owns the running log-sum-exp state and one
+ * float64 sum of the sampling terms per chunk of 4096 slots, both kept
+ * current by every write through the library (capacity <= 2^42). */
 int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer** out);
 int dqz_logit_buffer_destroy(dqz_logit_buffer* buf);
 
@@ -300,19 +302,22 @@ int dqz_logits_add(dqz_logit_buffer* buf, float* logits, int64_t clear_pos, int6
 int dqz_logits_write(dqz_logit_buffer* buf, float* logits, const int64_t* positions, const float* values, int n,
                      void* stream);
 
-/* One write logits[position] = value (by value: popleft's -inf), keeping the running sum. */
+/* One write logits[position] = value (by value: popleft's -inf), keeping the
+ * running sum and the chunk sum. */
 int dqz_logits_put(dqz_logit_buffer* buf, float* logits, int64_t position, float value, void* stream);
 
 /* Running log-sum-exp state of a logit buffer, for checkpoints
  * (parts.py:517-561): S = float64 sum of exp(x - c) over the buffer, the
  * shift c, the device-side valid flag, and the host bookkeeping (known: every
  * write since the last scan went through the library; adds: running adds
- * since that scan).  get synchronises `stream`; set restores all five, so a
- * restored buffer continues with the saver's bits (no re-scan on either
- * side). */
+ * since that scan).  get synchronises `stream`; set restores all five and
+ * recomputes the chunk sums from `logits` about c (they are a function of
+ * the two), so a restored buffer continues with the saver's bits (no re-scan
+ * on either side). */
 int dqz_logits_run_get(dqz_logit_buffer* buf, double* S, float* c, int* valid, int* known, int* adds,
                        void* stream);
-int dqz_logits_run_set(dqz_logit_buffer* buf, double S, float c, int valid, int known, int adds, void* stream);
+int dqz_logits_run_set(dqz_logit_buffer* buf, const float* logits, double S, float c, int valid, int known,
+                       int adds, void* stream);
 
 /* The logits were written outside the library (e.g. the meta-update's Adam
  * step, a state restore): the next dqz_logits_add re-scans the buffer. */
@@ -320,9 +325,11 @@ int dqz_logits_invalidate(dqz_logit_buffer* buf);
 
 /* Softmax sampling with replacement (CircularLogitBuffer.sample,
  * replay_circular.py:205-217 = Generator.choice(capacity, n, p=softmax)):
- * p = exp(x - logsumexp(x)) in f32, cdf = cumsum(float64 p) / total,
- * out_idx[i] = first slot with cdf > uniforms[i].  uniforms: device f64 [n]
- * in [0,1) (host Generator draws for parity, or dqz_uniform_philox). */
+ * terms t = expf(x - c) about the running shift c (softmax up to f32
+ * rounding of the exponent), cdf = cumsum(float64 t) / total, out_idx[i] =
+ * first slot with cdf > uniforms[i].  Reads the chunk sums and one chunk of
+ * 4096 logits per query.  uniforms: device f64 [n] in [0,1) (host Generator
+ * draws for parity, or dqz_uniform_philox). */
 int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
                       int64_t* out_idx, void* stream);
 
@@ -337,13 +344,20 @@ int dqz_logits_sample(dqz_logit_buffer* buf, const float* logits, const double* 
 int dqz_logits_sample_slots(dqz_logit_buffer* buf, const float* logits, uint64_t seed, uint64_t* counter_dev,
                             const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, void* stream);
 
-/* Diagnostic: the f32 p = exp(x - lse) of every slot exactly as
- * dqz_logits_sample forms it (p_out: device f32 [capacity]) and lse
- * (device f32, may be NULL) — probabilities_from_logits,
- * replay_circular.py:69-76.  Lets a checker separate the index search (which
- * is bit-exact against numpy given the same p) from the last-ulp differences
- * of f32 exp / log between numpy and the device. */
+/* Diagnostic: the sampling probability of every slot, p = t / total as f32
+ * (p_out: device f32 [capacity]; probabilities_from_logits,
+ * replay_circular.py:69-76) and the running log-sum-exp (lse_out: device
+ * f32, may be NULL). */
 int dqz_logits_probs(dqz_logit_buffer* buf, const float* logits, float* p_out, float* lse_out, void* stream);
+
+/* Diagnostic: the exact terms a draw's CDF is built from, t = expf(x - c)
+ * (t_out: device f32 [capacity]), the chunk sums (csum_out: device f64
+ * [ceil(capacity / 4096)], may be NULL) and c (c_out: device f32, may be
+ * NULL).  Lets a checker separate the index search (bit-exact against numpy's
+ * sequential-cumsum choice given the same t) from the last-ulp differences of
+ * f32 exp between numpy and the device. */
+int dqz_logits_terms(dqz_logit_buffer* buf, const float* logits, float* t_out, double* csum_out, float* c_out,
+                     void* stream);
 
 /* n uniform doubles in [0,1) from Philox4x32-10 (counter advanced on device). */
 int dqz_uniform_philox(uint64_t seed, uint64_t* counter_dev, int n, double* out, void* stream);

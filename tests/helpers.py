@@ -65,3 +65,29 @@ def kink_free_slots(params, host, capacity, batch, rng, margin=1e-6, tries=64):
     if learner_ref.relu_margin(params, s) >= margin:
       return slots
   raise AssertionError('no kink-free batch in %d draws' % tries)
+
+
+def canonical_chunk_sums(t):
+  """Restatement of the device's chunk sums (sampling.hpp chunk_sum): per
+  chunk of 4096 terms, lane l sums terms [16 l, 16 l + 16) in order, a
+  Hillis-Steele scan inside each 64-lane wave, then the last wave's total
+  plus the sum of the first three in order."""
+  t = np.asarray(t, np.float32).astype(np.float64)
+  nb = -(-len(t) // 4096)
+  padded = np.zeros(nb * 4096)
+  padded[:len(t)] = t
+  terms = padded.reshape(nb, 256, 16)
+  lane = terms[:, :, 0].copy()
+  for i in range(1, 16):
+    lane = lane + terms[:, :, i]
+  incl = lane.reshape(nb, 4, 64)
+  pos = np.arange(64)
+  o = 1
+  while o < 64:
+    up = np.zeros_like(incl)
+    up[..., o:] = incl[..., :-o]
+    incl = np.where(pos >= o, incl + up, incl)
+    o *= 2
+  w = incl[..., 63]
+  first3 = (w[:, 0] + w[:, 1]) + w[:, 2]
+  return w[:, 3] + first3

@@ -172,8 +172,8 @@ def test_config3_mgsc_reservoir_1m_sample_step_and_meta(device, store):
       break
   else:
     raise AssertionError('no kink-free batch')
-  p_dev = dev.probs()[0].cpu().numpy()
-  cdf = np.cumsum(p_dev.astype(np.float64))
+  t_dev = dev.terms()[0].cpu().numpy()  # the terms expf(x - c) the draw's CDF is built from
+  cdf = np.cumsum(t_dev.astype(np.float64))
   cdf /= cdf[-1]
   np.testing.assert_array_equal(idx, np.searchsorted(cdf, u, side='right'))
   assert (idx != replay_ref.softmax_choice(logits, u)).sum() <= 1
@@ -221,6 +221,10 @@ def test_config3_mgsc_reservoir_1m_sample_step_and_meta(device, store):
   a64 = after.astype(np.float64)
   want_lse = a64.max() + np.log(np.exp(a64 - a64.max()).sum())
   assert abs(run['c'] + np.log(run['S']) - want_lse) < 1e-9
+  # ... and the chunk sums of the chunks it wrote (dirty flags + chunk pass)
+  t_dev, csum, _ = dev.terms()
+  np.testing.assert_array_equal(csum.cpu().numpy(),
+                                helpers.canonical_chunk_sums(t_dev.cpu().numpy()))
 
 
 def test_config4_per_1m_sample_step_write_back(device, store):
