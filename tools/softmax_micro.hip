@@ -33,6 +33,78 @@ __global__ __launch_bounds__(256) void k_stream(const float* __restrict__ x, int
   if (s == 12345.f) out[blockIdx.x] = s;
 }
 
+
+// softmax_choice_body with s_memrealtime stamps after each phase (tick = 10 ns)
+__global__ __launch_bounds__(256) void k_query_timed(const float* __restrict__ x, int64_t n, const LogitRun* run,
+                                                     const double* __restrict__ csum, int nblocks, const double* uu,
+                                                     int64_t* out, uint64_t* stamps) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  __shared__ double s_before;
+  __shared__ int s_blk;
+  __shared__ unsigned long long s_idx;
+  uint64_t ts[8];
+  ts[0] = __builtin_amdgcn_s_memrealtime();
+  const double u = uu[blockIdx.x];
+  const int t = threadIdx.x;
+  const float c = run->c;
+  if (t == 0) {
+    s_blk = nblocks - 1;
+    s_idx = ~0ull;
+  }
+  const CsumLane l = csum_scan(csum, nblocks, s_wave);
+  ts[1] = __builtin_amdgcn_s_memrealtime();
+  const double tot = l.tot;
+  {
+    double acc = l.excl;
+    for (int b = l.b0; b < l.b1; ++b) {
+      const double v = csum_at(l, csum, b);
+      if ((acc + v) / tot > u) {
+        atomicMin(&s_blk, b);
+        break;
+      }
+      acc += v;
+    }
+  }
+  __syncthreads();
+  ts[2] = __builtin_amdgcn_s_memrealtime();
+  const int blk = s_blk;
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, blk, xv);
+  if (blk >= l.b0 && blk < l.b1) {
+    double acc = l.excl;
+    for (int b = l.b0; b < blk; ++b) acc += csum_at(l, csum, b);
+    s_before = acc;
+  }
+  double p[SM_PER_LANE];
+  double lane = 0.0;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) {
+    p[i] = chunk_term(xv[i], c);
+    lane += p[i];
+  }
+  ts[3] = __builtin_amdgcn_s_memrealtime();
+  double tot2;
+  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);
+  ts[4] = __builtin_amdgcn_s_memrealtime();
+  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
+  double acc = s_before + lexcl;
+  if (acc / tot <= u && (acc + lane) / tot > u) {
+    for (int i = 0; i < SM_PER_LANE; ++i) {
+      acc += p[i];
+      if (acc / tot > u) {
+        atomicMin(&s_idx, (unsigned long long)(base + i));
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  ts[5] = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) {
+    out[blockIdx.x] = (int64_t)s_idx;
+    for (int i = 0; i < 6; ++i) stamps[blockIdx.x * 8 + i] = ts[i];
+  }
+}
+
 template <class F>
 float time_graph(hipStream_t st, F launch, int n = 200) {
   hipGraph_t g;
@@ -127,6 +199,21 @@ int main() {
            pos = (pos + 4099) % n;
            hipLaunchKernelGGL(logits_put1_kernel, dim3(1), dim3(SM_THREADS), 0, st, x, n, run, bsum, pos, 0.5f);
          }));
+  uint64_t* stamps;
+  hipMalloc(&stamps, nq * 8 * 8);
+  std::vector<uint64_t> hs(nq * 8);
+  std::vector<double> acc(5, 0.0);
+  const int reps = 50;
+  for (int r = 0; r < reps; ++r) {
+    hipLaunchKernelGGL(k_query_timed, dim3(nq), dim3(SM_THREADS), 0, st, x, n, run, bsum, nb, u, out, stamps);
+    hipStreamSynchronize(st);
+    hipMemcpy(hs.data(), stamps, nq * 64, hipMemcpyDeviceToHost);
+    for (int q = 0; q < nq; ++q)
+      for (int i = 0; i < 5; ++i) acc[i] += (double)(hs[q * 8 + i + 1] - hs[q * 8 + i]) * 0.01;
+  }
+  printf(", \"query_phases_us\": {\"csum_load_scan\": %.3f, \"level1_pick\": %.3f, \"chunk_load_terms\": %.3f, "
+         "\"level2_scan\": %.3f, \"pick\": %.3f}",
+         acc[0] / (reps * nq), acc[1] / (reps * nq), acc[2] / (reps * nq), acc[3] / (reps * nq), acc[4] / (reps * nq));
   printf("}\n");
   return 0;
 }
