@@ -464,10 +464,14 @@ __global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, d
 
 // Level 1 of a draw over the chunk sums: lane t sums csum[t seg, (t + 1) seg)
 // in order; the block scan gives its exclusive prefix and the total (the
-// draw's normaliser; every diagnostic forms it the same way).
+// draw's normaliser; every diagnostic forms it the same way).  A lane's first
+// CS_SEG sums stay in registers (every index below is a compile-time
+// constant: no scratch), the rest (beyond 8M logits) are re-read.
+constexpr int CS_SEG = 8;
+
 struct CsumLane {
   int b0, b1;
-  double mb[8];  // this lane's chunk sums (seg <= 8 up to 8M logits), else re-read
+  double mb[CS_SEG];
   double excl, tot;
 };
 
@@ -476,18 +480,45 @@ __device__ __forceinline__ CsumLane csum_scan(const double* __restrict__ csum, i
   const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
   l.b0 = min((int)threadIdx.x * seg, nblocks);
   l.b1 = min(l.b0 + seg, nblocks);
+#pragma unroll
+  for (int j = 0; j < CS_SEG; ++j) l.mb[j] = l.b0 + j < l.b1 ? csum[l.b0 + j] : 0.0;
   double mine = 0.0;
-  for (int b = l.b0; b < l.b1; ++b) {
-    const double v = csum[b];
-    if (b - l.b0 < 8) l.mb[b - l.b0] = v;
-    mine += v;
-  }
+#pragma unroll
+  for (int j = 0; j < CS_SEG; ++j)
+    if (l.b0 + j < l.b1) mine += l.mb[j];
+  for (int b = l.b0 + CS_SEG; b < l.b1; ++b) mine += csum[b];
   l.excl = block_scan_excl_f64(mine, s_wave, &l.tot);
   return l;
 }
 
-__device__ __forceinline__ double csum_at(const CsumLane& l, const double* __restrict__ csum, int b) {
-  return b - l.b0 < 8 ? l.mb[b - l.b0] : csum[b];
+// First chunk of this lane whose normalised cumulative sum exceeds u, or -1.
+__device__ __forceinline__ int csum_crossing(const CsumLane& l, const double* __restrict__ csum, double u) {
+  double acc = l.excl;
+  int hit = -1;
+#pragma unroll
+  for (int j = 0; j < CS_SEG; ++j) {
+    if (hit < 0 && l.b0 + j < l.b1) {
+      const double v = l.mb[j];
+      if ((acc + v) / l.tot > u) hit = l.b0 + j;
+      acc += v;
+    }
+  }
+  for (int b = l.b0 + CS_SEG; hit < 0 && b < l.b1; ++b) {
+    const double v = csum[b];
+    if ((acc + v) / l.tot > u) hit = b;
+    acc += v;
+  }
+  return hit;
+}
+
+// Mass before chunk blk (blk in this lane's range), in the scan's order.
+__device__ __forceinline__ double csum_before(const CsumLane& l, const double* __restrict__ csum, int blk) {
+  double acc = l.excl;
+#pragma unroll
+  for (int j = 0; j < CS_SEG; ++j)
+    if (l.b0 + j < blk) acc += l.mb[j];
+  for (int b = l.b0 + CS_SEG; b < blk; ++b) acc += csum[b];
+  return acc;
 }
 
 // One query u: the first slot whose normalised cumulative term sum exceeds u
@@ -510,26 +541,14 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
   }
   const CsumLane l = csum_scan(csum, nblocks, s_wave);
   const double tot = l.tot;
-  {
-    double acc = l.excl;
-    for (int b = l.b0; b < l.b1; ++b) {
-      const double v = csum_at(l, csum, b);
-      if ((acc + v) / tot > u) {
-        atomicMin(&s_blk, b);
-        break;
-      }
-      acc += v;
-    }
-  }
+  const int hit = csum_crossing(l, csum, u);
+  if (hit >= 0) atomicMin(&s_blk, hit);
   __syncthreads();
   const int blk = s_blk;
   float xv[SM_PER_LANE];
   load_chunk_lane(x, n, blk, xv);  // independent of the prefix: issued first
-  if (blk >= l.b0 && blk < l.b1) {  // the owner of the crossing chunk publishes the mass before it
-    double acc = l.excl;
-    for (int b = l.b0; b < blk; ++b) acc += csum_at(l, csum, b);
-    s_before = acc;
-  }
+  // the owner of the crossing chunk publishes the mass before it
+  if (blk >= l.b0 && blk < l.b1) s_before = csum_before(l, csum, blk);
   double p[SM_PER_LANE];
   double lane = 0.0;
 #pragma unroll
@@ -542,13 +561,15 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
   const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
   double acc = s_before + lexcl;
   if (acc / tot <= u && (acc + lane) / tot > u) {
-    for (int i = 0; i < SM_PER_LANE; ++i) {
-      acc += p[i];
-      if (acc / tot > u) {
-        atomicMin(&s_idx, (unsigned long long)(base + i));
-        break;
+    int hit2 = -1;
+#pragma unroll
+    for (int i = 0; i < SM_PER_LANE; ++i) {  // constant indices: p stays in registers
+      if (hit2 < 0) {
+        acc += p[i];
+        if (acc / tot > u) hit2 = i;
       }
     }
+    if (hit2 >= 0) atomicMin(&s_idx, (unsigned long long)(base + hit2));
   }
   __syncthreads();
   if (t == 0) {
