@@ -435,7 +435,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 16 * B8;
+  const int G3 = ((B + C3DW_G - 1) / C3DW_G + 7) / 8 * 8, G2 = ((B + C2DW_G - 1) / C2DW_G + 7) / 8 * 8;
+  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * G3 + 8 * B8 + 8 * G2;
   DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
@@ -452,8 +453,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.p2 = L->p2;
   u.p3 = L->p3;
   u.S1 = B * C1_BLOCKS;
-  u.S2 = kDwXcd ? min(8, B) : B;  // XCD-group sums in slabs 0..7
-  u.S3 = kDwXcd ? min(8, B) : B;
+  // one slab per dW job group (XCD-group sums in slabs 0..7 with per-sample jobs)
+  u.S2 = kDwXcd && C2DW_G == 1 ? min(8, B) : (B + C2DW_G - 1) / C2DW_G;
+  u.S3 = kDwXcd && C3DW_G == 1 ? min(8, B) : (B + C3DW_G - 1) / C3DW_G;
   u.h1 = L->h1;
   u.dz1 = L->dz1;
   u.gq = L->gq;
