@@ -502,7 +502,7 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
     sb += __shfl_xor(sb, 32, 64);
     if (kq == 0) part[C3KK * C3CO] = sb;
   }
-  if (a.dwcnt && C3DW_G == 1) {
+  if (kDwXcd && C3DW_G == 1 && a.dwcnt) {
     int off[9];
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) off[tp] = ((tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) * 4;
@@ -770,7 +770,7 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
       if (kq == 0) part[C2KK * C2CO + 16 * ct] = v;
     }
   }
-  if (a.dwcnt && C2DW_G == 1) {
+  if (kDwXcd && C2DW_G == 1 && a.dwcnt) {
     int off[4];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -934,6 +934,7 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // leading workgroups: wave 0 of the first runs per_write_back_wave beside the
 // whole backward (the TD errors are final since the head), the other seven
 // exit at once (the sample ranges keep their XCD alignment).
+template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
   constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
@@ -946,7 +947,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const int B8 = (c3.B + 7) / 8 * 8;
   constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
   int i = blockIdx.x;
-  if (wb.tree) {
+  if constexpr (WB) {
     if (i < 8) {
       if (i == 0 && threadIdx.x < 64) per_write_back_wave(wb, reinterpret_cast<char*>(smem));
       return;

@@ -303,8 +303,11 @@ struct Fc1FwdArgs {
 };
 
 // The MFMA body of one fc1 block: its (z, split s, column tile nt, row group
-// mg) and the four waves' [2][256] K-quarter tiles in s_red[w * 512 ..]
-// (row 16 mt + 4 kq + rr, column n at [mt * 256 + (4 kq + rr) * 16 + n]).
+// mg) and the four waves' [2][16 x 16] K-quarter tiles in s_red[w * FC1_RW ..]
+// (row 16 mt + r, column n at [mt * FC1_RT + red_idx(r, n)]: 16 floats of
+// padding after every 4 rows, so the lanes kq = 0 / 1 of one ds_write_b32
+// group land 16 banks apart).
+constexpr int FC1_RT = red_rows(16), FC1_RW = 2 * FC1_RT;  // 320, 640 floats
 __device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int& z, int& s, int& nt, int& mg) {
   // Block -> tile map: the two 16-column tiles that share W1's 128-byte lines
   // (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
@@ -349,18 +352,18 @@ __device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, 
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * 512 + mt * 256 + (4 * kq + rr) * 16 + n] = acc[mt][rr];
+    for (int rr = 0; rr < 4; ++rr) s_red[w * FC1_RW + mt * FC1_RT + red_idx(4 * kq + rr, n)] = acc[mt][rr];
   __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
-  __shared__ float s_red[4 * 2 * 256];
+  __shared__ float s_red[4 * FC1_RW];
   int z, s, nt, mg;
   fc1_fwd_tile(a, s_red, z, s, nt, mg);
   DQZ_STAMP(3, 2);
   const int t = threadIdx.x;
-  if (a.sum) {
+  if (kFc1Reduce && a.sum) {
     // 128 threads x 4 columns: row t / 4, columns 16 nt + 4 (t % 4) .. + 3.
     // Partials go out write-through (16-B sc1 stores) and are read back with
     // sc1 loads by the tile's last block (the guide's hand-off row: one lane
@@ -377,8 +380,8 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = mt * 256 + r16 * 16 + c4 + e;
-        v[e] = (s_red[k] + s_red[512 + k]) + (s_red[1024 + k] + s_red[1536 + k]);
+        const int k = mt * FC1_RT + red_idx(r16, c4 + e);
+        v[e] = (s_red[k] + s_red[FC1_RW + k]) + (s_red[2 * FC1_RW + k] + s_red[3 * FC1_RW + k]);
       }
       if (32 * mg + row < a.B) {
         const int64_t off = ((((int64_t)z * FC1_S + s) * a.B + 32 * mg + row) * HID + colo) * 4;
@@ -416,8 +419,8 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = 32 * mg + 16 * h + (t >> 4);
-    const float* sr = s_red + h * 256 + t;
-    const float v = (sr[0] + sr[512]) + (sr[1024] + sr[1536]);
+    const float* sr = s_red + h * FC1_RT + red_idx(t >> 4, t & 15);
+    const float v = (sr[0] + sr[FC1_RW]) + (sr[2 * FC1_RW] + sr[3 * FC1_RW]);
     if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
   }
   DQZ_STAMP(3, 3);

@@ -66,21 +66,6 @@ struct dqz_learner {
   void* block;
 };
 
-// fc1 split-K partials summed inside fc1_fwd_kernel by each tile's last split
-// block (the head then loads one pre-activation row per sample) instead of by
-// the head (DQZ_FC1_REDUCE=0).
-#ifndef DQZ_FC1_REDUCE
-#define DQZ_FC1_REDUCE 0
-#endif
-constexpr bool kFc1Reduce = DQZ_FC1_REDUCE != 0;
-
-// conv2 / conv3 dW partials pre-reduced per XCD group inside the backward
-// launch (bwd.hpp dw_xcd_reduce), so update_kernel reads min(8, B) slabs.
-#ifndef DQZ_DW_XCD
-#define DQZ_DW_XCD 0
-#endif
-constexpr bool kDwXcd = DQZ_DW_XCD != 0;
-
 static int g_attr_done = 0;
 
 static int init_kernel_attrs() {
@@ -437,7 +422,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   }
   const int G3 = ((B + C3DW_G - 1) / C3DW_G + 7) / 8 * 8, G2 = ((B + C2DW_G - 1) / C2DW_G + 7) / 8 * 8;
   const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * G3 + 8 * B8 + 8 * G2;
-  DQZ_PHASE(6, hipLaunchKernelGGL(bwd_bc_kernel, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
+  DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
+            else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
