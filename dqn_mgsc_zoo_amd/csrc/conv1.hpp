@@ -22,9 +22,11 @@ struct Conv1Src {
   int fused;              // 1: slots come from the fused uniform sampler `draw`;
                           // 2: from the fused learned-logit draw `sm`;
                           // 3: from the fused prioritized draw `per`
-  UniformDraw draw;
-  SoftmaxDraw sm;
-  PerSampleArgs per;
+  union {                 // one draw per launch: the kernel argument stays small
+    UniformDraw draw;
+    SoftmaxDraw sm;
+    PerSampleArgs per;
+  };
   // Batch record: block (rb 0, z 0) of sample b also copies action / reward /
   // discount of its slot into rec[b] = {a as int bits, r, d, 0}, so the head
   // reads one record per sample instead of the slot -> record chain.

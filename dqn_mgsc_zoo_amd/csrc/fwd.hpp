@@ -37,8 +37,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // lanes kq = 0 / 1 (one ds_write_b32 lane group) 16 banks apart instead of on
 // the same banks; a 32-lane read group covers rows 2j, 2j + 1 of one 4-row
 // block, so the position-major reads stay conflict-free.
-__device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + 16 * (row >> 2) + col; }
-constexpr int red_rows(int rows) { return rows * 16 + 16 * ((rows + 3) / 4); }
+#ifndef DQZ_RED_PAD
+#define DQZ_RED_PAD 1
+#endif
+__device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + (DQZ_RED_PAD ? 16 * (row >> 2) : 0) + col; }
+constexpr int red_rows(int rows) { return rows * 16 + (DQZ_RED_PAD ? 16 * ((rows + 3) / 4) : 0); }
 
 struct LayerFwdArgs {
   const float* in;  // [Z][B][...] layer input (NHWC)
