@@ -73,7 +73,10 @@ __device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double e
 //   the cotangent at td is clip(w td / B, +-bound) because rlax.clip_gradient
 //   clips the incoming gradient; dq[b, a_b] = -that; dz1 = dq W2[:, a_b] relu'.
 // Cross-sample sums (fc2/fc1-bias grads, mean loss) happen in update_kernel.
-template <int AMAX, int SMAX>
+// ZMAX: network copies this instantiation handles (2: online + target, or
+// one copy; 3: double-Q's online(s_t) too), so no load is issued for a copy
+// the launch does not have.
+template <int AMAX, int SMAX, int ZMAX>
 __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   DQZ_STAMP(4, 0);
   __shared__ float s_red[8][3 * AMAX];
@@ -93,9 +96,9 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   const int slot = chain ? h.slots[b] : 0;  // uniform load, in flight with the partials
   float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
   if (!h.fwd_only && h.rec != nullptr && n == 0) rv = h.rec[b];
-  float pv[3][SMAX], b1v[3], w2v[3][AMAX];
+  float pv[ZMAX][SMAX], b1v[ZMAX], w2v[ZMAX][AMAX];
 #pragma unroll
-  for (int z = 0; z < 3; ++z) {
+  for (int z = 0; z < ZMAX; ++z) {
     const int zc = min(z, Z - 1);
     const float* part = h.fc1p + ((int64_t)zc * S * B + b) * HID + n;
 #pragma unroll
@@ -118,10 +121,19 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   const int kk = n >> lgT, jj = n & (T - 1);
   const bool qthread = kTr ? (kk < K && jj == 0) : (n < 3 * AMAX && n / AMAX < Z && n % AMAX < A);
   const int zq = kTr ? min(kk / A, 2) : n / AMAX, aq = kTr ? kk % A : n % AMAX;  // output of this q thread
-  float b2v = 0.f;  // fc2 bias of output (zq, aq)
-  if (kTr ? kk < K : n < 3 * AMAX) {
-    const int zc = min(zq, Z - 1), a = min(aq, A - 1);
-    b2v = h.nz.p[zc][h.b2_off + (h.shared_bias ? 0 : a)];
+  // fc2 bias of output (zq, aq): the bias of every copy is loaded (each
+  // through the copy's uniform parameter pointer) and the lane's one selected
+  // by value; indexing nz.p by the lane's copy would load the pointer per
+  // lane, and that load's wait would also wait for every load issued above
+  float b2v = 0.f;
+  {
+    const int a2 = h.shared_bias ? 0 : min(aq, A - 1);
+    float b2z[ZMAX];
+#pragma unroll
+    for (int z = 0; z < ZMAX; ++z) b2z[z] = h.nz.p[min(z, Z - 1)][h.b2_off + a2];
+    const int zc = min(zq, Z - 1);
+#pragma unroll
+    for (int z = 0; z < ZMAX; ++z) b2v = zc == z ? b2z[z] : b2v;
   }
   float wper = 1.f;
   if (h.per_probs && wave == 0) {  // the batch's IS weights (the fused PER draw)
@@ -150,9 +162,11 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     if (h.meta_p) pm = h.meta_p[b];
   }
   DQZ_STAMP(4, 1);
-  float hz[3] = {0.f, 0.f, 0.f};
+  float hz[ZMAX];
 #pragma unroll
-  for (int z = 0; z < 3; ++z) {
+  for (int z = 0; z < ZMAX; ++z) hz[z] = 0.f;
+#pragma unroll
+  for (int z = 0; z < ZMAX; ++z) {
     if (z < Z) {
       float acc = b1v[z];
 #pragma unroll
@@ -263,7 +277,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   }
   // deferred outputs: fc1 activations (fc2 dW in the update kernel), q values
 #pragma unroll
-  for (int z = 0; z < 3; ++z)
+  for (int z = 0; z < ZMAX; ++z)
     if (z < Z) h.h1[((int64_t)z * B + b) * HID + n] = hz[z];
   if (qthread) h.q[((int64_t)zq * B + b) * A + aq] = qv;
   // the fused sampler's step counter: every conv1 block of this step has read it
@@ -272,23 +286,31 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   DQZ_STAMP(4, 3);
 }
 
-template <int AMAX, int SMAX>
+template <int AMAX, int SMAX, int ZMAX>
 __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
-  head_body<AMAX, SMAX>(h, blockIdx.x);
+  head_body<AMAX, SMAX, ZMAX>(h, blockIdx.x);
 }
 
 // Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.
+template <int SMAX, int ZMAX>
+inline void launch_head_z(const HeadArgs& h, int grid, hipStream_t st) {
+  if (h.A <= 8)
+    hipLaunchKernelGGL((head_kernel<8, SMAX, ZMAX>), dim3(grid), dim3(HID), 0, st, h);
+  else
+    hipLaunchKernelGGL((head_kernel<MAXA, SMAX, ZMAX>), dim3(grid), dim3(HID), 0, st, h);
+}
+
 inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
-  if (h.S > 7) return hipErrorInvalidValue;
-  if (h.S == 1) {  // fc1 sums reduced in fc1_fwd_kernel: one row per sample
-    if (h.A <= 8)
-      hipLaunchKernelGGL((head_kernel<8, 1>), dim3(grid), dim3(HID), 0, st, h);
+  if (h.S > 7 || h.Z < 1 || h.Z > 3) return hipErrorInvalidValue;
+  if (kFc1Reduce && h.S == 1) {  // fc1 sums reduced in fc1_fwd_kernel: one row per sample
+    if (h.Z <= 2)
+      launch_head_z<1, 2>(h, grid, st);
     else
-      hipLaunchKernelGGL((head_kernel<MAXA, 1>), dim3(grid), dim3(HID), 0, st, h);
-  } else if (h.A <= 8) {
-    hipLaunchKernelGGL((head_kernel<8, 7>), dim3(grid), dim3(HID), 0, st, h);
+      launch_head_z<1, 3>(h, grid, st);
+  } else if (h.Z <= 2) {
+    launch_head_z<7, 2>(h, grid, st);
   } else {
-    hipLaunchKernelGGL((head_kernel<MAXA, 7>), dim3(grid), dim3(HID), 0, st, h);
+    launch_head_z<7, 3>(h, grid, st);
   }
   return hipGetLastError();
 }
