@@ -462,93 +462,110 @@ __global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, d
   if (threadIdx.x == 0) *counter = ctr + 1;
 }
 
-// Level 1 of a draw over the chunk sums: lane t sums csum[t seg, (t + 1) seg)
-// in order; the block scan gives its exclusive prefix and the total (the
-// draw's normaliser; every diagnostic forms it the same way).  A lane's first
-// CS_SEG sums stay in registers (every index below is a compile-time
-// constant: no scratch), the rest (beyond 8M logits) are re-read.
+// Level 1 of a draw over the chunk sums, by one wave: lane l sums
+// csum[l seg, (l + 1) seg) in order (seg = ceil(nblocks / 64): 4 at 1M
+// logits), an inclusive Hillis-Steele scan over the 64 lanes by shuffles
+// gives each lane's exclusive prefix and the total (the draw's normaliser;
+// the diagnostics form it the same way).  No LDS and no barrier.  A lane's
+// first CS_SEG sums stay in registers (constant indices: no scratch), the
+// rest (beyond 2M logits) are re-read.
 constexpr int CS_SEG = 8;
 
-struct CsumLane {
-  int b0, b1;
-  double mb[CS_SEG];
-  double excl, tot;
+struct CsumLevel1 {
+  int blk;        // the chunk the query's u falls in
+  double before;  // the normalised-cumsum mass before it
+  double tot;     // total of all chunk sums
 };
 
-__device__ __forceinline__ CsumLane csum_scan(const double* __restrict__ csum, int nblocks, double* s_wave) {
-  CsumLane l;
-  const int seg = (nblocks + SM_THREADS - 1) / SM_THREADS;
-  l.b0 = min((int)threadIdx.x * seg, nblocks);
-  l.b1 = min(l.b0 + seg, nblocks);
+// Wave-uniform result on every lane of the calling wave (a whole wave).
+__device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csum, int nblocks, double u) {
+  const int l = threadIdx.x & 63;
+  const int seg = (nblocks + 63) / 64;
+  const int b0 = min(l * seg, nblocks), b1 = min(b0 + seg, nblocks);
+  double mb[CS_SEG];
 #pragma unroll
-  for (int j = 0; j < CS_SEG; ++j) l.mb[j] = l.b0 + j < l.b1 ? csum[l.b0 + j] : 0.0;
+  for (int j = 0; j < CS_SEG; ++j) mb[j] = b0 + j < b1 ? csum[b0 + j] : 0.0;
   double mine = 0.0;
 #pragma unroll
   for (int j = 0; j < CS_SEG; ++j)
-    if (l.b0 + j < l.b1) mine += l.mb[j];
-  for (int b = l.b0 + CS_SEG; b < l.b1; ++b) mine += csum[b];
-  l.excl = block_scan_excl_f64(mine, s_wave, &l.tot);
-  return l;
-}
-
-// First chunk of this lane whose normalised cumulative sum exceeds u, or -1.
-__device__ __forceinline__ int csum_crossing(const CsumLane& l, const double* __restrict__ csum, double u) {
-  double acc = l.excl;
+    if (b0 + j < b1) mine += mb[j];
+  for (int b = b0 + CS_SEG; b < b1; ++b) mine += csum[b];
+  double incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double up = __shfl_up(incl, o, 64);
+    if (l >= o) incl += up;
+  }
+  const double tot = __shfl(incl, 63, 64);
+  double excl = __shfl_up(incl, 1, 64);
+  excl = l == 0 ? 0.0 : excl;
+  // this lane's first crossing chunk and the mass before it
+  double acc = excl, before = 0.0, before_last = excl;
   int hit = -1;
 #pragma unroll
   for (int j = 0; j < CS_SEG; ++j) {
-    if (hit < 0 && l.b0 + j < l.b1) {
-      const double v = l.mb[j];
-      if ((acc + v) / l.tot > u) hit = l.b0 + j;
+    if (b0 + j < b1) {
+      const double v = mb[j];
+      if (b0 + j == nblocks - 1) before_last = acc;
+      if (hit < 0 && (acc + v) / tot > u) {
+        hit = b0 + j;
+        before = acc;
+      }
       acc += v;
     }
   }
-  for (int b = l.b0 + CS_SEG; hit < 0 && b < l.b1; ++b) {
+  for (int b = b0 + CS_SEG; b < b1; ++b) {
     const double v = csum[b];
-    if ((acc + v) / l.tot > u) hit = b;
+    if (b == nblocks - 1) before_last = acc;
+    if (hit < 0 && (acc + v) / tot > u) {
+      hit = b;
+      before = acc;
+    }
     acc += v;
   }
-  return hit;
-}
-
-// Mass before chunk blk (blk in this lane's range), in the scan's order.
-__device__ __forceinline__ double csum_before(const CsumLane& l, const double* __restrict__ csum, int blk) {
-  double acc = l.excl;
-#pragma unroll
-  for (int j = 0; j < CS_SEG; ++j)
-    if (l.b0 + j < blk) acc += l.mb[j];
-  for (int b = l.b0 + CS_SEG; b < blk; ++b) acc += csum[b];
-  return acc;
+  const unsigned long long m = __ballot(hit >= 0);
+  CsumLevel1 r;
+  r.tot = tot;
+  if (m) {  // the lowest crossing lane holds the earliest chunk
+    const int src = __ffsll((long long)m) - 1;
+    r.blk = __shfl(hit, src, 64);
+    r.before = __shfl(before, src, 64);
+  } else {  // rounding at the top: the last chunk (as numpy's searchsorted clamps)
+    const int src = (nblocks - 1) / seg;
+    r.blk = nblocks - 1;
+    r.before = __shfl(before_last, src, 64);
+  }
+  return r;
 }
 
 // One query u: the first slot whose normalised cumulative term sum exceeds u
 // (searchsorted side='right' on cumsum(t) / total, as numpy's choice does on
-// its p).  Level 1 finds the chunk from the csum prefix (the minimum chunk
-// any lane sees the crossing in), level 2 the lane (16 terms each) and the
-// slot from the chunk's re-formed terms, whose scan total is csum[chunk].
+// its p).  Level 1 (wave 0, csum_level1) finds the chunk, level 2 (all 256
+// lanes) the lane (16 terms each) and the slot from the chunk's re-formed
+// terms, whose scan total is csum[chunk].  At most one lane sees the
+// crossing, so it stores the slot directly.
 __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, const LogitRun* run,
                                                        const double* __restrict__ csum, int nblocks, double u) {
   __shared__ double s_wave[SM_THREADS / 64];
-  __shared__ double s_before;
+  __shared__ double s_before, s_tot;
   __shared__ int s_blk;
-  __shared__ unsigned long long s_idx;
-  __shared__ int64_t s_out;
+  __shared__ int64_t s_idx;
   const int t = threadIdx.x;
   const float c = run->c;
-  if (t == 0) {
-    s_blk = nblocks - 1;
-    s_idx = ~0ull;
+  if (t < 64) {
+    const CsumLevel1 r = csum_level1(csum, nblocks, u);
+    if (t == 0) {
+      s_blk = r.blk;
+      s_before = r.before;
+      s_tot = r.tot;
+      s_idx = -1;
+    }
   }
-  const CsumLane l = csum_scan(csum, nblocks, s_wave);
-  const double tot = l.tot;
-  const int hit = csum_crossing(l, csum, u);
-  if (hit >= 0) atomicMin(&s_blk, hit);
   __syncthreads();
   const int blk = s_blk;
+  const double tot = s_tot, before = s_before;
   float xv[SM_PER_LANE];
-  load_chunk_lane(x, n, blk, xv);  // independent of the prefix: issued first
-  // the owner of the crossing chunk publishes the mass before it
-  if (blk >= l.b0 && blk < l.b1) s_before = csum_before(l, csum, blk);
+  load_chunk_lane(x, n, blk, xv);
   double p[SM_PER_LANE];
   double lane = 0.0;
 #pragma unroll
@@ -557,9 +574,9 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
     lane += p[i];
   }
   double tot2;
-  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);  // its barriers publish s_before
+  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);
   const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
-  double acc = s_before + lexcl;
+  double acc = before + lexcl;
   if (acc / tot <= u && (acc + lane) / tot > u) {
     int hit2 = -1;
 #pragma unroll
@@ -569,23 +586,24 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
         if (acc / tot > u) hit2 = i;
       }
     }
-    if (hit2 >= 0) atomicMin(&s_idx, (unsigned long long)(base + hit2));
+    if (hit2 >= 0) s_idx = base + hit2;
   }
   __syncthreads();
-  if (t == 0) {
-    int64_t idx = s_idx == ~0ull ? -1 : (int64_t)s_idx;
-    if (idx < 0) {  // rounding at the chunk edge: last live slot of the chunk
+  int64_t idx = s_idx;
+  if (idx < 0) {  // rounding at the chunk edge: the last live slot of the chunk (block-uniform)
+    if (t == 0) {
       const int64_t end = min(n, (int64_t)(blk + 1) * SM_CHUNK);
       for (int64_t j = end - 1; j >= (int64_t)blk * SM_CHUNK; --j)
         if (x[j] != -INFINITY) {
           idx = j;
           break;
         }
+      s_idx = idx;
     }
-    s_out = idx;
+    __syncthreads();
+    idx = s_idx;
   }
-  __syncthreads();
-  return s_out;
+  return idx;
 }
 
 // Diagnostics (dqz_logits_probs / dqz_logits_terms), one block per chunk:
@@ -596,9 +614,14 @@ __global__ __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __
                                                                  int nblocks, float* __restrict__ p_out,
                                                                  float* __restrict__ t_out, float* lse_out,
                                                                  float* c_out) {
-  __shared__ double s_wave[SM_THREADS / 64];
+  __shared__ double s_tot;
   const LogitRun r = *run;
-  const CsumLane l = csum_scan(csum, nblocks, s_wave);
+  if (threadIdx.x < 64) {
+    const CsumLevel1 l1 = csum_level1(csum, nblocks, 2.0);  // u = 2: only the total is used
+    if (threadIdx.x == 0) s_tot = l1.tot;
+  }
+  __syncthreads();
+  const double tot = s_tot;
   const int k = blockIdx.x;
   float xv[SM_PER_LANE];
   load_chunk_lane(x, n, k, xv);
@@ -607,7 +630,7 @@ __global__ __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __
   for (int i = 0; i < SM_PER_LANE; ++i) {
     if (base + i < n) {
       const double ti = chunk_term(xv[i], r.c);
-      if (p_out) p_out[base + i] = (float)(ti / l.tot);
+      if (p_out) p_out[base + i] = (float)(ti / tot);
       if (t_out) t_out[base + i] = (float)ti;
     }
   }

@@ -34,81 +34,6 @@ __global__ __launch_bounds__(256) void k_stream(const float* __restrict__ x, int
 }
 
 
-// softmax_choice_body with s_memrealtime stamps after each phase (tick = 10 ns)
-template <int V>  // 0: as the product; 1: level-1 crossing by multiply instead of divide
-__global__ __launch_bounds__(256) void k_query_timed(const float* __restrict__ x, int64_t n, const LogitRun* run,
-                                                     const double* __restrict__ csum, int nblocks, const double* uu,
-                                                     int64_t* out, uint64_t* stamps) {
-  __shared__ double s_wave[SM_THREADS / 64];
-  __shared__ double s_before;
-  __shared__ int s_blk;
-  __shared__ unsigned long long s_idx;
-  uint64_t ts[8];
-  ts[0] = __builtin_amdgcn_s_memrealtime();
-  const double u = uu[blockIdx.x];
-  const int t = threadIdx.x;
-  const float c = run->c;
-  if (t == 0) {
-    s_blk = nblocks - 1;
-    s_idx = ~0ull;
-  }
-  const CsumLane l = csum_scan(csum, nblocks, s_wave);
-  ts[1] = __builtin_amdgcn_s_memrealtime();
-  const double tot = l.tot;
-  int hit;
-  if constexpr (V == 0) {
-    hit = csum_crossing(l, csum, u);
-  } else {
-    const double rt = 1.0 / tot;
-    double acc = l.excl;
-    hit = -1;
-#pragma unroll
-    for (int j = 0; j < CS_SEG; ++j) {
-      if (hit < 0 && l.b0 + j < l.b1) {
-        acc += l.mb[j];
-        if (acc * rt > u) hit = l.b0 + j;
-      }
-    }
-  }
-  if (hit >= 0) atomicMin(&s_blk, hit);
-  __syncthreads();
-  ts[2] = __builtin_amdgcn_s_memrealtime();
-  const int blk = s_blk;
-  float xv[SM_PER_LANE];
-  load_chunk_lane(x, n, blk, xv);
-  if (blk >= l.b0 && blk < l.b1) s_before = csum_before(l, csum, blk);
-  double p[SM_PER_LANE];
-  double lane = 0.0;
-#pragma unroll
-  for (int i = 0; i < SM_PER_LANE; ++i) {
-    p[i] = chunk_term(xv[i], c);
-    lane += p[i];
-  }
-  ts[3] = __builtin_amdgcn_s_memrealtime();
-  double tot2;
-  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);
-  ts[4] = __builtin_amdgcn_s_memrealtime();
-  const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
-  double acc = s_before + lexcl;
-  if (acc / tot <= u && (acc + lane) / tot > u) {
-    int hit2 = -1;
-#pragma unroll
-    for (int i = 0; i < SM_PER_LANE; ++i) {
-      if (hit2 < 0) {
-        acc += p[i];
-        if (acc / tot > u) hit2 = i;
-      }
-    }
-    if (hit2 >= 0) atomicMin(&s_idx, (unsigned long long)(base + hit2));
-  }
-  __syncthreads();
-  ts[5] = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) {
-    out[blockIdx.x] = (int64_t)s_idx;
-    for (int i = 0; i < 6; ++i) stamps[blockIdx.x * 8 + i] = ts[i];
-  }
-}
-
 template <class F>
 float time_graph(hipStream_t st, F launch, int n = 200) {
   hipGraph_t g;
@@ -203,26 +128,6 @@ int main() {
            pos = (pos + 4099) % n;
            hipLaunchKernelGGL(logits_put1_kernel, dim3(1), dim3(SM_THREADS), 0, st, x, n, run, bsum, pos, 0.5f);
          }));
-  uint64_t* stamps;
-  hipMalloc(&stamps, nq * 8 * 8);
-  std::vector<uint64_t> hs(nq * 8);
-  for (int v = 0; v < 2; ++v) {
-    std::vector<double> acc(5, 0.0);
-    const int reps = 50;
-    for (int r = 0; r < reps; ++r) {
-      if (v == 0)
-        hipLaunchKernelGGL(k_query_timed<0>, dim3(nq), dim3(SM_THREADS), 0, st, x, n, run, bsum, nb, u, out, stamps);
-      else
-        hipLaunchKernelGGL(k_query_timed<1>, dim3(nq), dim3(SM_THREADS), 0, st, x, n, run, bsum, nb, u, out, stamps);
-      hipStreamSynchronize(st);
-      hipMemcpy(hs.data(), stamps, nq * 64, hipMemcpyDeviceToHost);
-      for (int q = 0; q < nq; ++q)
-        for (int i = 0; i < 5; ++i) acc[i] += (double)(hs[q * 8 + i + 1] - hs[q * 8 + i]) * 0.01;
-    }
-    printf(", \"query_phases_us_v%d\": {\"csum_load_scan\": %.3f, \"level1_pick\": %.3f, \"chunk_load_terms\": %.3f, "
-           "\"level2_scan\": %.3f, \"pick\": %.3f}", v,
-           acc[0] / (reps * nq), acc[1] / (reps * nq), acc[2] / (reps * nq), acc[3] / (reps * nq), acc[4] / (reps * nq));
-  }
   printf("}\n");
   return 0;
 }
