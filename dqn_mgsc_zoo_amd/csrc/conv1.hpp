@@ -127,6 +127,7 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
     // slot -> 4 frame ids -> 504 16-byte pieces (2 per thread), all loads in
     // flight before the first LDS store.
     int slot;
+    double per_prob = 0.0;  // F == 3: the draw's probability (thread 0)
     if constexpr (F == 1) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
       slot = uniform_slot(*src.draw.counter, b, src.draw);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.draw.slots_out[b] = slot;
@@ -134,7 +135,9 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
       slot = softmax_draw_slot(src.sm, b);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.sm.slots_out[b] = slot;
     } else if constexpr (F == 3) {  // fused prioritized draw (the tree top staged in s_in first)
-      slot = per_draw_slot(src.per, b, reinterpret_cast<double*>(s_in), rb == 0 && z == 0);
+      const PerDrawOut d = per_draw_slot(src.per, b, reinterpret_cast<double*>(s_in), rb == 0 && z == 0);
+      slot = d.slot;
+      per_prob = d.prob;
     } else {
       slot = src.slots[b];
     }
@@ -156,6 +159,9 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
       const uint4* g = reinterpret_cast<const uint4*>(src.frames + (int64_t)max(f, 0) * FB + row0 * FW);
       v[q] = g[j];
     }
+    // the fused PER draw's IS weight, while the frame loads are in flight
+    if constexpr (F == 3)
+      if (threadIdx.x == 0 && rb == 0 && z == 0) per_publish_weight(src.per, b, per_prob);
     if (sk >= 0) DQZ_STAMP(sk, 1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {

@@ -17,11 +17,11 @@ struct HeadArgs {
   const float* reward;
   const float* discount;
   const float* weights;  // PER importance weights or null
-  // fused PER draw (or null): the B sampling probabilities conv1 published;
-  // w_b = (up / p_b)^beta, normalised by the batch maximum if per_normalize
-  // (importance_sampling_weights, replay.py:344-376), also written to per_w_out
-  const double* per_probs;
-  double per_up, per_beta;
+  // fused PER draw (or null): the B unnormalised importance weights
+  // w_b = (up / p_b)^beta conv1 published; normalised here by the batch
+  // maximum if per_normalize (importance_sampling_weights,
+  // replay.py:344-376), also written to per_w_out
+  const double* per_wb;
   int per_normalize;
   float* per_w_out;
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
@@ -136,13 +136,13 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     for (int z = 0; z < ZMAX; ++z) b2v = zc == z ? b2z[z] : b2v;
   }
   float wper = 1.f;
-  if (h.per_probs && wave == 0) {  // the batch's IS weights (the fused PER draw)
+  if (h.per_wb && wave == 0) {  // the batch's IS weights (the fused PER draw)
     double m = 0.0;
-    for (int j = lane; j < B; j += 64) m = fmax(m, pow(h.per_up / h.per_probs[j], h.per_beta));
+    for (int j = lane; j < B; j += 64) m = fmax(m, h.per_wb[j]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     if (lane == 0) {
-      const double wb = pow(h.per_up / h.per_probs[b], h.per_beta);
+      const double wb = h.per_wb[b];
       wper = (float)(h.per_normalize ? wb / m : wb);
       if (h.per_w_out) h.per_w_out[b] = wper;
     }
@@ -158,7 +158,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
       d = rv.z;
     }
     if (h.weights) w = h.weights[b];
-    if (h.per_probs) w = wper;
+    if (h.per_wb) w = wper;
     if (h.meta_p) pm = h.meta_p[b];
   }
   DQZ_STAMP(4, 1);

@@ -60,6 +60,7 @@ struct dqz_learner {
   int32_t* fc1cnt;  // its tile arrival counters
   int32_t* dwcnt;   // XCD-group dW reduce counters: conv3 [8][4], conv2 [8][8] (x Handoff::kStride)
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
+  double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
@@ -121,11 +122,12 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
                            n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
                            (int64_t)Z_MAX_FC1 * MAXB * HID, (int64_t)Z_MAX_FC1 * (MAXB / 32) * (HID / 16) * Handoff::kStride,
-                           (int64_t)(8 * 4 + 8 * 8) * Handoff::kStride};
+                           (int64_t)(8 * 4 + 8 * 8) * Handoff::kStride, 2 * (int64_t)B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p,
-                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt), reinterpret_cast<float**>(&L->dwcnt)};
+                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt), reinterpret_cast<float**>(&L->dwcnt),
+                    reinterpret_cast<float**>(&L->per_wb)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -318,6 +320,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     } else if (pd) {
       fsrc.fused = 3;
       fsrc.per = *pd;
+      fsrc.per.out_wb = L->per_wb;
     } else {
       fsrc.fused = 2;
       fsrc.sm = *sm;
@@ -343,9 +346,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   h.discount = S->discount;
   h.weights = L->cfg.algo == DQZ_ALGO_PER && !pd ? is_weights : nullptr;
   if (pd) {
-    h.per_probs = pd->out_probs;
-    h.per_up = 1.0 / (double)pd->size;
-    h.per_beta = pd->beta;
+    h.per_wb = L->per_wb;
     h.per_normalize = pd->normalize;
     h.per_w_out = pd->out_weights;
   }
@@ -990,7 +991,7 @@ int dqz_per_sample(const double* tree, int64_t cap, int64_t live_base, int64_t s
   if (n < 1 || n > 1024) return fail(DQZ_ERR_INVALID, "n must be in [1, 1024]");
   if (!(beta >= 0.0 && beta <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= exponent <= 1.");
   if (!(usp >= 0.0 && usp <= 1.0)) return fail(DQZ_ERR_INVALID, "Require 0 <= uniform_sample_probability <= 1.");
-  PerSampleArgs a;
+  PerSampleArgs a{};
   a.tree = tree;
   a.cap = cap;
   a.levels = tree_levels(cap);
@@ -1031,7 +1032,7 @@ int dqz_learner_step_per_draw(dqz_learner* L, const dqz_params* P, const dqz_sto
   const int levels = tree_levels(d->cap);
   if (L->cfg.batch > 64 || levels > PWB_LEVELS)
     return fail(DQZ_ERR_INVALID, "the fused PER step takes batch <= 64 and cap <= 2^%d", PWB_LEVELS);
-  PerSampleArgs a;
+  PerSampleArgs a{};
   a.tree = d->tree;
   a.cap = d->cap;
   a.levels = levels;

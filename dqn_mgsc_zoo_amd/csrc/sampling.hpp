@@ -996,6 +996,7 @@ struct PerSampleArgs {
   int32_t* out_slots;
   float* out_weights;
   double* out_probs;
+  double* out_wb;  // fused draw only: the unnormalised IS weight (up / p)^beta of each draw
 };
 
 // Depths 0 .. PS_TOPD of the tree (2047 nodes, 16 KB) are staged in LDS once
@@ -1026,22 +1027,42 @@ struct PerPick {
   double prob;
 };
 
-__device__ __forceinline__ PerPick per_pick(const PerSampleArgs& a, int i, int l, const double* s_top, int dtop,
-                                            uint64_t ctr) {
-  const double root = s_top[1];
+// The draw's three random inputs: injected from the caller's RandomState, or
+// Philox (seed, ctr, i).  Separate from the descent so a caller can issue
+// their loads before it stages the tree top.
+struct PerDrawInput {
   double u_target, u_mix;
   int64_t uni;
+};
+
+// Injected inputs as loaded (u_target, u_mix, uni) or, in Philox mode, the
+// step counter in `uni` (per_draw_input turns it into the draw's inputs).
+__device__ __forceinline__ PerDrawInput per_draw_load(const PerSampleArgs& a, int i) {
+  if (a.inj_u) return PerDrawInput{a.inj_u[i], a.inj_u[a.n + i], a.inj_uniform[i]};
+  return PerDrawInput{0.0, 0.0, (int64_t)*a.counter};
+}
+
+__device__ __forceinline__ PerDrawInput per_draw_input(const PerSampleArgs& a, int i, uint64_t ctr) {
+  PerDrawInput d;
   if (a.inj_u) {
-    u_target = a.inj_u[i];
-    u_mix = a.inj_u[a.n + i];
-    uni = a.inj_uniform[i];
+    d.u_target = a.inj_u[i];
+    d.u_mix = a.inj_u[a.n + i];
+    d.uni = a.inj_uniform[i];
   } else {
     const uint4 r = philox4x32(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), (unsigned)i, 0x9E12u),
                                make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32)));
-    u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
-    u_mix = (double)(r.z >> 8) * 0x1.0p-24;
-    uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
+    d.u_target = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
+    d.u_mix = (double)(r.z >> 8) * 0x1.0p-24;
+    d.uni = (a.live_base + (int64_t)((double)(r.w) * 0x1.0p-32 * (double)a.size)) % a.capacity;
   }
+  return d;
+}
+
+__device__ __forceinline__ PerPick per_pick(const PerSampleArgs& a, int l, const double* s_top, int dtop,
+                                            const PerDrawInput& in) {
+  const double root = s_top[1];
+  const double u_target = in.u_target, u_mix = in.u_mix;
+  const int64_t uni = in.uni;
   const bool use_uniform = u_mix < a.usp;
   int64_t idx = uni;
   double leaf;
@@ -1114,7 +1135,7 @@ __global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
   const int h = threadIdx.x >> 5, l = threadIdx.x & 31;
   const double up = 1.0 / (double)a.size;
   for (int i = h; i < a.n; i += 32) {
-    const PerPick pk = per_pick(a, i, l, s_top, dtop, ctr);
+    const PerPick pk = per_pick(a, l, s_top, dtop, per_draw_input(a, i, ctr));
     const double w = per_weight(up, pk.prob, a.beta);
     if (l == 0) {
       if (a.out_indices) a.out_indices[i] = (int32_t)pk.idx;
@@ -1139,15 +1160,25 @@ __global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
 // probability of draw b (the head turns the B probabilities into normalised
 // IS weights, the backward's write-back uses the indices).  The Philox
 // counter is advanced by the head once every conv1 block has read it.
-__device__ __forceinline__ int32_t per_draw_slot(const PerSampleArgs& a, int b, double* lds, bool publish) {
+struct PerDrawOut {
+  int32_t slot;  // every thread
+  double prob;   // thread 0
+};
+
+__device__ __forceinline__ PerDrawOut per_draw_slot(const PerSampleArgs& a, int b, double* lds, bool publish) {
   __shared__ int32_t s_slot;
+  double prob = 0.0;
+  // the draw's inputs (the counter or the injected values: block-uniform
+  // loads) are issued before the tree top is staged and land under it
+  const PerDrawInput raw = per_draw_load(a, b);
   const int dtop = per_stage_top(a, lds);
   if (threadIdx.x < 32) {
-    const uint64_t ctr = a.inj_u ? 0 : *a.counter;
-    const PerPick pk = per_pick(a, b, threadIdx.x, lds, dtop, ctr);
+    const PerDrawInput in = a.inj_u ? raw : per_draw_input(a, b, (uint64_t)raw.uni);
+    const PerPick pk = per_pick(a, threadIdx.x, lds, dtop, in);
     if (threadIdx.x == 0) {
       const int32_t slot = a.index_to_slot ? a.index_to_slot[pk.idx] : (int32_t)pk.idx;
       s_slot = slot;
+      prob = pk.prob;
       if (publish) {
         a.out_indices[b] = (int32_t)pk.idx;
         a.out_slots[b] = slot;
@@ -1156,7 +1187,14 @@ __device__ __forceinline__ int32_t per_draw_slot(const PerSampleArgs& a, int b, 
     }
   }
   __syncthreads();  // s_slot published; every read of lds done before the frame gather reuses it
-  return s_slot;
+  return PerDrawOut{s_slot, prob};
+}
+
+// The publishing block's IS weight of draw b, (1/size / p)^beta unnormalised
+// (per_sample_kernel's per_weight, the same bits), for the head's batch
+// normalisation; called by thread 0 with the probability per_draw_slot left it.
+__device__ __forceinline__ void per_publish_weight(const PerSampleArgs& a, int b, double prob) {
+  if (a.out_wb) a.out_wb[b] = per_weight(1.0 / (double)a.size, prob, a.beta);
 }
 
 // PrioritizedTransitionReplay.add on device (replay.py:1068-1096 with

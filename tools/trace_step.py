@@ -1,6 +1,7 @@
 """Per-kernel timeline of one learner step from in-kernel s_memrealtime stamps.
 
-usage (GPU box): python tools/trace_step.py   (builds libdqz_trace.so first)
+usage (GPU box): [ALGO=dqn|double|per|mgsc] python tools/trace_step.py
+(builds libdqz_trace.so first)
 Prints, per kernel in launch order: first-block start relative to the previous
 kernel's last-block end (the boundary), kernel span, median block lifetime and
 the median of the named intervals between stamps (10 ns ticks -> us).
@@ -28,17 +29,22 @@ ORDER = [10, 0, 14, 1, 2, 3, 4, 15, 5, 6, 11, 7, 12, 8, 13, 9]
 K, NB, NS = 16, 4096, 4
 
 dev = torch.device('cuda:0')
-net = networks.dqn_atari_network(6)
-lrn = learner_lib.Learner(net, 32, algo='dqn', device=dev)
-lrn.set_params(net.init(0))
 cap = int(os.environ.get('CAP', '200000'))
-store = synthetic.fill_episodic(cap, 6, seed=0, device=dev)
-slots = torch.zeros((32,), dtype=torch.int32, device=dev)
-counter = torch.zeros((1,), dtype=torch.int64, device=dev)
+ALGO = os.environ.get('ALGO', 'dqn')  # dqn | double | per | mgsc: bench.py's workloads
+if ALGO == 'dqn':
+  net = networks.dqn_atari_network(6)
+  lrn = learner_lib.Learner(net, 32, algo='dqn', device=dev)
+  lrn.set_params(net.init(0))
+  store = synthetic.fill_episodic(cap, 6, seed=0, device=dev)
+  slots = torch.zeros((32,), dtype=torch.int32, device=dev)
+  counter = torch.zeros((1,), dtype=torch.int64, device=dev)
 
-
-def step():
-  lrn.step_uniform(store, 0, cap, cap, 1, counter, slots)
+  def step():
+    lrn.step_uniform(store, 0, cap, cap, 1, counter, slots)
+else:
+  import bench  # noqa: E402  (its workloads: the PER / learned-logit draws inside the step)
+  wl = bench.Workload(ALGO, cap, 0, dev)
+  step = wl.one_step
 
 
 lib = _native.lib()
