@@ -558,6 +558,40 @@ def test_chunk_sums_follow_every_write(device):
   _check_chunk_sums(dev)
 
 
+def test_chunk_sums_follow_fifo_writes(device):
+  """The same invariant through CircularLogitBuffer (MGSC FIFO): running adds,
+  popleft (-inf puts), explicit writes through __setitem__, wrap-around past
+  the capacity, a buffer emptied to nothing (S = 0 re-seeds) and refilled."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap = 2 * 4096 + 777
+  rng = np.random.default_rng(22)
+  buf = rc.CircularLogitBuffer(cap, np.random.default_rng(3))
+  dev = buf._dev  # pylint: disable=protected-access
+  for _ in range(cap):
+    buf.add()
+  _check_chunk_sums(dev)
+  for step in range(400):
+    op = rng.random()
+    if op < 0.4 and buf.size > 0:
+      buf.popleft(return_value=False)
+    elif op < 0.55 and buf.size > 0:
+      keys = rng.integers(0, buf.size, 5)
+      buf[keys] = rng.normal(0, 2, 5).astype(np.float32)
+    elif buf.size < cap:
+      buf.add()
+    if step % 100 == 99:
+      _check_chunk_sums(dev)
+  while buf.size > 0:  # empty: the last popleft leaves S = 0
+    buf.popleft(return_value=False)
+  _check_chunk_sums(dev)
+  for _ in range(100):
+    buf.add()
+  t = _check_chunk_sums(dev)
+  u = np.random.default_rng(6).random(32)
+  got = dev.sample_abs(u).cpu().numpy()
+  np.testing.assert_array_equal(got, _choice_from_p(t, u))
+
+
 def test_fused_logit_sampler_equals_philox_then_choice(device):
   """dqz_logits_sample_slots (one launch: Philox uniforms + block sums + CDF
   search behind an in-launch hand-off) draws exactly what
