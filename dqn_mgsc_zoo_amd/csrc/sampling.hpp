@@ -173,7 +173,9 @@ __global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __r
 // (deterministic run to run): a Hillis-Steele scan inside each wave by
 // shuffles, then each wave adds the totals of the waves before it, summed in
 // wave order.  Returns the exclusive prefix; *tot gets the block total with
-// exactly the bits the last lane's inclusive prefix has.  Two barriers.
+// exactly the bits the last lane's inclusive prefix has.  Two barriers; a
+// caller that does not reuse s_wave afterwards may drop the second (TAIL).
+template <bool TAIL = true>
 __device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, double* tot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double incl = v;
@@ -196,7 +198,7 @@ __device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, 
   excl = lane == 0 ? 0.0 : excl;
   excl = wave == 0 ? excl : (lane == 0 ? pre : excl + pre);
   *tot = last_incl;
-  __syncthreads();
+  if constexpr (TAIL) __syncthreads();
   return excl;
 }
 
@@ -573,8 +575,8 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
     p[i] = chunk_term(xv[i], c);
     lane += p[i];
   }
-  double tot2;
-  const double lexcl = block_scan_excl_f64(lane, s_wave, &tot2);
+  double tot2;  // (s_wave is not used again in this call: no trailing barrier)
+  const double lexcl = block_scan_excl_f64<false>(lane, s_wave, &tot2);
   const int64_t base = (int64_t)blk * SM_CHUNK + t * SM_PER_LANE;
   double acc = before + lexcl;
   if (acc / tot <= u && (acc + lane) / tot > u) {
