@@ -8,17 +8,12 @@
 
 namespace dqz {
 
-// ---- fc1 backward: dX + dW + centered RMSProp in one pass over W1 ----------
-// grid = 196 blocks of 16 rows of W1 [3136][512].  A block
-//   * computes dy3[:, rows] = (dz1 @ W1[rows]^T) * relu'(y3) with the OLD W1
-//     rows (M = B samples, N = 16 rows, K = 512 split over the 4 waves), and
-//   * accumulates dW1[rows][:] = y3[:, rows]^T @ dz1 (M = 16 rows, N = 512
-//     columns, wave w owns columns [128 w, 128 w + 128), K = B), then
-//   * applies RMSProp to its rows (or writes the gradient in gradient-output
-//     mode).  No other block touches these rows, so reading the old weights
-//     for dX and updating them in the same kernel is race-free.
-// W1, mu and nu are each read once and written once: the fc1 step is
-// HBM-bound at 6 x 6.4 MB.
+// ---- fc1 backward ----------------------------------------------------------
+// dX in fc1_dx_kernel (196 blocks of 16 rows of W1 [3136][512], below);
+// dW1 = y3^T @ dz1 + centered RMSProp in bwd_bc_kernel's fc1 dW range
+// (fc1_dw_body, 784 blocks of 16 rows x 128 columns), which starts after
+// fc1_dx_kernel (the update overwrites the rows dX reads).  W1, mu and nu
+// are each read once and written once (HBM-bound at 6 x 6.4 MB).
 struct Fc1BwdArgs {
   const float* dz1;  // [B][512]
   const float* y3;   // [B][3136] online activations
@@ -57,30 +52,27 @@ __device__ __forceinline__ int w2p_src(int i) {
 }
 constexpr int W3P_N = 4 * 9 * 1024, W2P_N = 8 * 4 * 1024;  // 36864, 32768
 
-// LDS row stride of the dz1 chunk.  The dW path's ds_read_b32 of rows
-// 4 kk + kq (lanes n, kq) needs rows 16 (mod 32) banks apart: 528.  The dX
-// path's ds_read_b128 A fragments (lane n reads row 16 mt + n at column
-// 4 kq) are conflict-free in every 16-lane group only with a stride of 8
-// (mod 64) dwords: 520 (528 put two lanes on each bank quad: 4 extra LDS
-// cycles per read, the 1.67 conflict cycles per LDS instruction of round 2's
-// counters).
+// LDS row stride of the dz1 chunk: the dX A fragments' ds_read_b128 (lane n
+// reads row 16 mt + n at column 4 kq) are conflict-free in every 16-lane
+// group only with a stride of 8 (mod 64) dwords: 520 (528 put two lanes on
+// each bank quad: 4 extra LDS cycles per read, the 1.67 conflict cycles per
+// LDS instruction of round 2's counters).
 #ifndef DQZ_FC1DX_LD
 #define DQZ_FC1DX_LD 520
 #endif
-constexpr int FC1B_LD = 528;
 constexpr int FC1X_LD = DQZ_FC1DX_LD;
 
-// DX: dy3 = (dz1 @ W1^T) relu'(y3) (the critical path: conv3 backward waits on
-// it).  DW: dW1 + RMSProp, which only has to finish before the next step and
-// runs on the learner's side stream beside the conv backward kernels.  DW
-// must start after DX: it overwrites the W1 rows DX reads.
+// dy3 = (dz1 @ W1^T) relu'(y3), the head of the backward chain (conv3
+// backward waits on it).  Block blk owns W1 rows [16 blk, 16 blk + 16) for
+// all samples; wave w owns hidden units [128 w, 128 w + 128) (a quarter of
+// K).  dz1 is staged 32 samples at a time into LDS, the four K-quarter
+// partial tiles summed through LDS in a fixed order.
 constexpr int FC1X_RED = 256 + 4 * 16;  // one padded 16 x 16 dX partial tile
-constexpr int FC1B_SMEM = 32 * (FC1B_LD > FC1X_LD ? FC1B_LD : FC1X_LD) + 4 * 2 * FC1X_RED;  // floats: dz1 chunk (later the dW block) + dX partials
+constexpr int FC1X_SMEM = 32 * FC1X_LD + 4 * 2 * FC1X_RED;  // floats: dz1 chunk + dX partials
 
-template <bool DX, bool DW>
-__device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, int blk) {
-  DQZ_STAMP(DW ? 11 : 5, 0);
-  constexpr int LD = DW ? FC1B_LD : FC1X_LD;
+__device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, int blk) {
+  DQZ_STAMP(5, 0);
+  constexpr int LD = FC1X_LD;
   float* s_dz = smem;
   // dX partials [wave][mt][row 4 kq + r][n], 16 floats of padding after every
   // 4 rows: the writes of lanes kq = 0 / 1 (and 2 / 3), one ds_write_b32
@@ -92,136 +84,58 @@ __device__ __forceinline__ void fc1_bwd_body(const Fc1BwdArgs& a, float* smem, i
   const int n = lane & 15, kq = lane >> 4;
   const int k0 = 16 * blk;
   const float* W1 = a.th + a.w_off;
-  float4 wv[8];  // dX B operand: W1[k0 + n][128 w + 16 j + 4 kq + e]
-  if constexpr (DX) {
+  float4 wv[8];  // B operand: W1[k0 + n][128 w + 16 j + 4 kq + e]
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
-  }
-  const bool upd = DW && a.rms.gout == nullptr;
-  f32x4 gacc[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) gacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 8; ++j)
+    wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
   for (int c = 0; c < a.B; c += 32) {
     if (c > 0) __syncthreads();  // previous chunk's s_dz / s_red readers are done
     // stage dz1 rows [c, c + 32) (rows past B are zero)
-    {
-      float4 v[16];
+    float4 v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int f = t + 256 * i, row = f >> 7;
-        const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + 4 * (f & 127));
-        v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      float ym[2];
-      if constexpr (DX) {
+    for (int i = 0; i < 16; ++i) {
+      const int f = t + 256 * i, row = f >> 7;
+      const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + 4 * (f & 127));
+      v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float ym[2];  // relu'(y3) operands of the epilogue
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
-      }
-      float yv[8];  // dW A operand: y3[c + 4 kk + kq][k0 + n]
-      if constexpr (DW) {
+    for (int h = 0; h < 2; ++h)
+      ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int bb = c + 4 * kk + kq;
-          const float y = a.y3[(int64_t)min(bb, a.B - 1) * FLAT + k0 + n];
-          yv[kk] = bb < a.B ? y : 0.f;
-        }
-      }
+    for (int i = 0; i < 16; ++i) {
+      const int f = t + 256 * i;
+      *reinterpret_cast<float4*>(s_dz + (f >> 7) * LD + 4 * (f & 127)) = v[i];
+    }
+    __syncthreads();
+    // rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
+    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int f = t + 256 * i;
-        *reinterpret_cast<float4*>(s_dz + (f >> 7) * LD + 4 * (f & 127)) = v[i];
-      }
-      __syncthreads();
-      if constexpr (DX) {
-      // dX: rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
-      f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int mt = 0; mt < 2; ++mt) {
+      const float* d = s_dz + (16 * mt + n) * LD + 128 * w + 4 * kq;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const float* d = s_dz + (16 * mt + n) * LD + 128 * w + 4 * kq;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
-          xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
-          xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
-          xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
-          xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
-        }
-      }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[w][mt][red_at(4 * kq + r, n)] = xacc[mt][r];
-      }
-      if constexpr (DW) {
-      // dW over the chunk: A = y3[b][k0 + m], B = dz1[b][128 w + 16 q + n]
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const float* d = s_dz + (4 * kk + kq) * LD + 128 * w + n;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) gacc[q] = mfma4(yv[kk], d[16 * q], gacc[q]);
-      }
-      }
-      __syncthreads();
-      if constexpr (DX) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int sample = c + 16 * h + (t >> 4);
-        const int k = red_at(t >> 4, t & 15);
-        const float v2 = (s_red[0][h][k] + s_red[1][h][k]) + (s_red[2][h][k] + s_red[3][h][k]);
-        if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
-      }
+      for (int j = 0; j < 8; ++j) {
+        const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
+        xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
+        xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
+        xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
+        xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
       }
     }
-  }
-  if constexpr (!DW) {
-    DQZ_STAMP(5, 3);
-    return;
-  }
-  DQZ_STAMP(11, 2);
-  // dW block through LDS into the float4 layout of the RMSProp operands.
-  __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s_dz[(4 * kq + r) * LD + 128 * w + 16 * q + n] = gacc[q][r];
-  __syncthreads();
-  // RMSProp on this thread's 32 parameters of the 16 x 512 block, as float4
-  // f = t + 256 i: row f / 128, columns 4 (f % 128) .. +3; every operand load
-  // is issued before the first update.
-  const Rms& R = a.rms;
-  float4 gv[8], o_th[8], o_mu[8], o_nu[8];
+      for (int r = 0; r < 4; ++r) s_red[w][mt][red_at(4 * kq + r, n)] = xacc[mt][r];
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int f = t + 256 * i;
-    const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
-    gv[i] = *reinterpret_cast<const float4*>(s_dz + (f >> 7) * LD + 4 * (f & 127));
-    if (upd) {
-      o_th[i] = *reinterpret_cast<const float4*>(a.th + e);
-      o_mu[i] = *reinterpret_cast<const float4*>(a.mu + e);
-      o_nu[i] = *reinterpret_cast<const float4*>(a.nu + e);
+    for (int h = 0; h < 2; ++h) {
+      const int sample = c + 16 * h + (t >> 4);
+      const int k = red_at(t >> 4, t & 15);
+      const float v2 = (s_red[0][h][k] + s_red[1][h][k]) + (s_red[2][h][k] + s_red[3][h][k]);
+      if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
     }
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int f = t + 256 * i;
-    const int64_t e = a.w_off + (int64_t)(k0 + (f >> 7)) * HID + 4 * (f & 127);
-    const float4 g = gv[i];
-    if (!upd) {
-      *reinterpret_cast<float4*>(R.gout + e) = g;
-    } else {
-      float4 th4 = o_th[i], mu4 = o_mu[i], nu4 = o_nu[i];
-      R.step(g.x, th4.x, mu4.x, nu4.x);
-      R.step(g.y, th4.y, mu4.y, nu4.y);
-      R.step(g.z, th4.z, mu4.z, nu4.z);
-      R.step(g.w, th4.w, mu4.w, nu4.w);
-      *reinterpret_cast<float4*>(a.th + e) = th4;
-      *reinterpret_cast<float4*>(a.mu + e) = mu4;
-      *reinterpret_cast<float4*>(a.nu + e) = nu4;
-    }
-  }
-  DQZ_STAMP(11, 3);
+  DQZ_STAMP(5, 3);
 }
 
 // ---- conv3 backward: dX and per-sample dW partials -----------------------
@@ -900,7 +814,7 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
 // workgroups and the dW workgroups share the CUs (no cross-stream edges).
 
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[FC1B_SMEM];
+  __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
   // W3 / W2 dX copies: element i of the 69,632 is thread i of the grid (the
   // gathers are issued first and land under the block's own work)
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -909,7 +823,7 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
     if (g < W3P_N) v3 = a.w3[w3p_src(g)];
     if (g < W2P_N) v2 = a.w2[w2p_src(g)];
   }
-  fc1_bwd_body<true, false>(a, smem, blockIdx.x);
+  fc1_dx_body(a, smem, blockIdx.x);
   if (a.w3p) {
     if (g < W3P_N) a.w3p[g] = v3;
     if (g < W2P_N) a.w2p[g] = v2;
