@@ -311,11 +311,11 @@ struct Fc1FwdArgs {
 // padding after every 4 rows, so the lanes kq = 0 / 1 of one ds_write_b32
 // group land 16 banks apart).
 constexpr int FC1_RT = red_rows(16), FC1_RW = 2 * FC1_RT;  // 320, 640 floats
-__device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int& z, int& s, int& nt, int& mg) {
-  // Block -> tile map: the two 16-column tiles that share W1's 128-byte lines
-  // (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
+__device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int i, int& z, int& s, int& nt,
+                                             int& mg) {
+  // Block i -> tile map: the two 16-column tiles that share W1's 128-byte
+  // lines (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
   // dispatch places on the same XCD, so each line is fetched into one L2.
-  const int i = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const int slot = i >> 3, pair = (i & 7) + 8 * (slot >> 1);
   nt = 2 * (pair % 16) + (slot & 1);
   const int rest = pair / 16;
@@ -359,11 +359,23 @@ __device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, 
   __syncthreads();
 }
 
+// The block's 32 x 16 split partial (the four K-quarter tiles summed in order).
+__device__ __forceinline__ void fc1_fwd_store(const Fc1FwdArgs& a, const float* s_red, int z, int s, int nt, int mg) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 32 * mg + 16 * h + (t >> 4);
+    const float* sr = s_red + h * FC1_RT + red_idx(t >> 4, t & 15);
+    const float v = (sr[0] + sr[FC1_RW]) + (sr[2 * FC1_RW] + sr[3 * FC1_RW]);
+    if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_RW];
   int z, s, nt, mg;
-  fc1_fwd_tile(a, s_red, z, s, nt, mg);
+  fc1_fwd_tile(a, s_red, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), z, s, nt, mg);
   DQZ_STAMP(3, 2);
   const int t = threadIdx.x;
   if (kFc1Reduce && a.sum) {
@@ -418,15 +430,44 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
     DQZ_STAMP(3, 3);
     return;
   }
-  // 512 outputs (32 rows x 16 cols), 2 per thread
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = 32 * mg + 16 * h + (t >> 4);
-    const float* sr = s_red + h * FC1_RT + red_idx(t >> 4, t & 15);
-    const float v = (sr[0] + sr[FC1_RW]) + (sr[2 * FC1_RW] + sr[3 * FC1_RW]);
-    if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
-  }
+  fc1_fwd_store(a, s_red, z, s, nt, mg);
   DQZ_STAMP(3, 3);
+}
+
+// ---- MGSC meta tangent forward in one launch ------------------------------
+// V * y_{l-1} + vb of every layer over the meta batch's stored primal
+// activations (linear mode, the tangent v as weights; meta.hpp): the four
+// layers are independent of each other, so one launch holds them as block
+// ranges [conv1 4/sample] [conv2 4/sample] [conv3 4/sample] [fc1 tiles]
+// instead of four dependent launches.  Dynamic LDS = conv1's 57.6 KB.
+static_assert(4 * FC1_RW * sizeof(float) <= kConv1FwdSmem, "fc1's partial tiles fit the tangent launch's LDS");
+inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + (HID / 16) * FC1_S * MG; }
+__global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
+                                                          Fc1FwdArgs f1) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n = 4 * ((c1.B + 7) / 8 * 8);
+  int i = blockIdx.x;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, c1.B);
+    if (sj.valid) conv1_fwd_body<false, 0>(c1, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c2.B);
+    if (sj.valid) conv2_fwd_body<false, false>(c2, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
+    if (sj.valid) conv3_fwd_body<false>(c3, smem, sj);
+    return;
+  }
+  i -= n;
+  int z, s, nt, mg;
+  fc1_fwd_tile(f1, smem, i, z, s, nt, mg);
+  fc1_fwd_store(f1, smem, z, s, nt, mg);
 }
 
 }  // namespace dqz

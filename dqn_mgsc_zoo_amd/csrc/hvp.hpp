@@ -8,9 +8,16 @@
 //                    ydot_l = relu'(y_l) zdot_l;
 //   tangent backward ddot_l = relu'(y_l) (Wdot_{l+1}^T d_{l+1} + W_{l+1}^T ddot_{l+1});
 //   d/deps grad     dW_l = sum_p (ydot_{l-1} (x) d_l + y_{l-1} (x) ddot_l), db_l = sum_p ddot_l,
-// with d_l the unit-cotangent backward signals of q[a] (d_5 = e_a).  Every
-// kernel here is a plain one-thread-per-output loop: this runs once per meta
-// step on one sample (~40 M MAC), off the learner's hot loop.
+// with d_l the unit-cotangent backward signals of q[a] (d_5 = e_a).
+//
+// Eight launches, one per dependent stage (t1 t2 t3 t4 b3 b2 b1, then every
+// parameter-gradient block in one launch).  Each stage splits its reduction
+// over the threads of a workgroup and sums the splits through LDS in a fixed
+// order (deterministic, no partial-sum launches); the two passes over fc1's
+// 3136 x 512 weights (t4, b3) read whole rows with coalesced 8- / 16-byte
+// loads over hundreds of workgroups (they are the chain's HBM traffic:
+// 2 x 2 x 6.4 MB).  t4's K-chunk partials are summed by the gradient launch,
+// the only consumer of the fc1 tangent output.
 #pragma once
 #include "common.hpp"
 
@@ -30,211 +37,343 @@ struct HvpArgs {
   const float *y1, *y2, *y3, *h;  // [400*32], [81*64], [3136], [512]
   const float *d1, *d2, *d3, *d4; // same shapes (pre-activation grads of q[a])
   // tangent scratch
-  float *ty1, *ty2, *ty3, *th4, *td4, *td3, *td2, *td1;
+  float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1;
   float* hq;    // output, parameter layout
-  float* part;  // [HVP_SPLITS][C1M * C1CO] K-split partial sums of the current stage
+  float* part;  // [HVP_T4_CHUNKS][512] fc1 tangent K-chunk partials
+  // grad q . w: the meta_second_kernel partials, summed once (t1's last block)
+  const float* s1_part;
+  int s1_nparts;
+  float* s1;  // [1]
 };
 
-// Every stage below splits its reduction (K) over blockIdx.y and writes
-// part[split][i]; hvp_fin_kernel then sums the splits in order (deterministic),
-// adds the tangent bias and applies the fixed ReLU mask.  One thread per
-// (output, split): thousands of waves instead of one long loop per output.
-constexpr int HVP_SPLITS = 16;
+constexpr int HVP_T4_KC = 16, HVP_T4_CHUNKS = FLAT / HVP_T4_KC;  // 196 chunks of 16 rows
 
 __device__ __forceinline__ float hvp_x(const HvpArgs& a, int ih, int iw, int ci) {
   const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
   return f < 0 ? 0.f : u8n(a.frames[(int64_t)f * FB + ih * FW + iw]);
 }
 
-// out[i] = mask[i] > 0 ? bias[i % nb] + sum_s part[s][i] : 0   (mask / bias optional)
-__global__ void hvp_fin_kernel(const float* __restrict__ part, int S, int N, const float* __restrict__ mask,
-                               const float* __restrict__ bias, int nb, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  float z = bias ? bias[i % nb] : 0.f;
-  for (int s = 0; s < S; ++s) z += part[(int64_t)s * N + i];
-  out[i] = (mask == nullptr || mask[i] > 0.f) ? z : 0.f;
+// Sum of the block's 256 values v (thread order), deterministic, result in
+// every thread.  s: 4 floats of LDS.
+__device__ __forceinline__ float block_sum256(float v, float* s) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  return r;
 }
 
-// 1. conv1 tangent partial over kernel row kh = split: conv(x, Wdot1)
-__global__ void hvp_t1_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
-  if (i >= C1M * C1CO) return;
-  const int p = i / C1CO, co = i % C1CO, oh = p / C1O, ow = p % C1O;
+// 1. conv1 tangent: ty1[p][co] = relu'(y1) (bdot1[co] + sum_k x_p[k] Wdot1[k][co]).
+// Block p (400), thread (kh = t / 32, co = t % 32) sums kw, ci; the 8 kh
+// partials are summed in order.  Block 400 sums the s1 partials.
+__global__ __launch_bounds__(256) void hvp_t1_kernel(HvpArgs a) {
+  __shared__ float s_x[C1KK];
+  __shared__ float s_r[C1K][C1CO];
+  __shared__ float s_w[4];
+  const int t = threadIdx.x;
+  if (blockIdx.x == C1M) {
+    float v = 0.f;
+    for (int j = t; j < a.s1_nparts; j += 256) v += a.s1_part[j];
+    v = block_sum256(v, s_w);
+    if (t == 0) a.s1[0] = v;
+    return;
+  }
+  const int p = blockIdx.x, oh = p / C1O, ow = p % C1O;
+  {
+    const int kh = t >> 5, kw = (t >> 2) & 7, ci = t & 3;
+    s_x[t] = hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci);
+  }
+  __syncthreads();
+  const int kh = t >> 5, co = t & 31;
   const float* W = a.tw + a.off[0];
   float z = 0.f;
-  for (int kw = 0; kw < C1K; ++kw)
 #pragma unroll
-    for (int ci = 0; ci < FC; ++ci)
-      z += hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci) * W[((kh * C1K + kw) * FC + ci) * C1CO + co];
-  a.part[(int64_t)kh * (C1M * C1CO) + i] = z;
+  for (int j = 0; j < C1K * FC; ++j) {
+    const int k = kh * C1K * FC + j;  // (kh, kw = j / 4, ci = j % 4)
+    z += s_x[k] * W[k * C1CO + co];
+  }
+  s_r[kh][co] = z;
+  __syncthreads();
+  if (t < C1CO) {
+    float s = a.tw[a.off[1] + t];
+#pragma unroll
+    for (int k = 0; k < C1K; ++k) s += s_r[k][t];
+    a.ty1[p * C1CO + t] = a.y1[p * C1CO + t] > 0.f ? s : 0.f;
+  }
 }
 
-// 2./3. conv2 / conv3 tangent partial over kernel row kh: conv(y, Wdot) + conv(ydot, W)
-template <int IH, int CI, int K, int S, int CO, int OH>
-__device__ __forceinline__ float hvp_conv_t(const float* y, const float* yd, const float* W, const float* Wd,
-                                            int p, int co, int kh) {
-  const int oh = p / OH, ow = p % OH;
+// 2. conv2 tangent: ty2 = relu'(y2) (bdot2 + conv(y1, Wdot2) + conv(ty1, W2)).
+// Block (p, 16-channel group g); thread (tap = t / 16 = kh * 4 + kw, co).
+__global__ __launch_bounds__(256) void hvp_t2_kernel(HvpArgs a) {
+  __shared__ float s_r[16][16];
+  const int t = threadIdx.x, p = blockIdx.x, g = blockIdx.y;
+  const int oh = p / C2O, ow = p % C2O, tap = t >> 4, kh = tap >> 2, kw = tap & 3;
+  const int co = 16 * g + (t & 15);
+  const int src = ((oh * C2S + kh) * C1O + ow * C2S + kw) * C1CO;
+  const float *W = a.th + a.off[2] + tap * C2CI * C2CO + co, *Wd = a.tw + a.off[2] + tap * C2CI * C2CO + co;
   float z = 0.f;
-  for (int kw = 0; kw < K; ++kw)
-    for (int ci = 0; ci < CI; ++ci) {
-      const int src = ((oh * S + kh) * IH + ow * S + kw) * CI + ci;
-      const int wi = ((kh * K + kw) * CI + ci) * CO + co;
-      z += y[src] * Wd[wi] + yd[src] * W[wi];
+#pragma unroll 8
+  for (int ci = 0; ci < C2CI; ++ci) z += a.y1[src + ci] * Wd[ci * C2CO] + a.ty1[src + ci] * W[ci * C2CO];
+  s_r[tap][t & 15] = z;
+  __syncthreads();
+  if (t < 16) {
+    const int c = 16 * g + t;
+    float s = a.tw[a.off[3] + c];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += s_r[k][t];
+    a.ty2[p * C2CO + c] = a.y2[p * C2CO + c] > 0.f ? s : 0.f;
+  }
+}
+
+// 3. conv3 tangent: ty3 = relu'(y3) (bdot3 + conv(y2, Wdot3) + conv(ty2, W3)).
+// Block (p, 16-channel group g); thread (input-channel quad s = t / 16, co)
+// over the 9 taps.
+__global__ __launch_bounds__(256) void hvp_t3_kernel(HvpArgs a) {
+  __shared__ float s_r[16][16];
+  const int t = threadIdx.x, p = blockIdx.x, g = blockIdx.y;
+  const int oh = p / C3O, ow = p % C3O, s = t >> 4;
+  const int co = 16 * g + (t & 15);
+  const float *W = a.th + a.off[4] + co, *Wd = a.tw + a.off[4] + co;
+  float z = 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int kh = tap / 3, kw = tap % 3;
+    const int src = ((oh + kh) * C2O + ow + kw) * C2CO + 4 * s;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int wi = (tap * C3CI + 4 * s + e) * C3CO;
+      z += a.y2[src + e] * Wd[wi] + a.ty2[src + e] * W[wi];
     }
-  return z;
+  }
+  s_r[s][t & 15] = z;
+  __syncthreads();
+  if (t < 16) {
+    const int c = 16 * g + t;
+    float v = a.tw[a.off[5] + c];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += s_r[k][t];
+    a.ty3[p * C3CO + c] = a.y3[p * C3CO + c] > 0.f ? v : 0.f;
+  }
 }
 
-__global__ void hvp_t2_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
-  if (i >= C2M * C2CO) return;
-  a.part[(int64_t)kh * (C2M * C2CO) + i] = hvp_conv_t<C1O, C1CO, C2K, C2S, C2CO, C2O>(
-      a.y1, a.ty1, a.th + a.off[2], a.tw + a.off[2], i / C2CO, i % C2CO, kh);
-}
-
-__global__ void hvp_t3_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
-  if (i >= FLAT) return;
-  a.part[(int64_t)kh * FLAT + i] = hvp_conv_t<C2O, C2CO, C3K, 1, C3CO, C3O>(
-      a.y2, a.ty2, a.th + a.off[4], a.tw + a.off[4], i / C3CO, i % C3CO, kh);
-}
-
-// 4. fc1 tangent partial over k in [196 s, 196 s + 196) (hdot), and the
-// fc2-level backward tangent ddot4 = relu'(h) Wdot2[:, a] (split 0)
-constexpr int HVP_FC_KS = FLAT / HVP_SPLITS;  // 196
-__global__ void hvp_t4_kernel(HvpArgs a) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
-  if (n >= HID) return;
+// 4. fc1 tangent K-chunk partials: part[c][n] = sum_{k in chunk c} y3[k]
+// Wdot1[k][n] + ty3[k] W1[k][n] (thread t: columns 2t, 2t + 1; whole-row
+// float2 loads), and the fc2-level backward tangent ddot4 = relu'(h)
+// Wdot2[:, a] (block 0).
+__global__ __launch_bounds__(256) void hvp_t4_kernel(HvpArgs a) {
+  const int t = threadIdx.x, c = blockIdx.x;
   const float *W = a.th + a.off[6], *Wd = a.tw + a.off[6];
-  float z = 0.f;
-  for (int k = s * HVP_FC_KS; k < (s + 1) * HVP_FC_KS; ++k)
-    z += a.y3[k] * Wd[(int64_t)k * HID + n] + a.ty3[k] * W[(int64_t)k * HID + n];
-  a.part[(int64_t)s * HID + n] = z;
-  if (s == 0) {
+  float2 z = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < HVP_T4_KC; ++j) {
+    const int k = c * HVP_T4_KC + j;
+    const float2 w = *reinterpret_cast<const float2*>(W + (int64_t)k * HID + 2 * t);
+    const float2 wd = *reinterpret_cast<const float2*>(Wd + (int64_t)k * HID + 2 * t);
+    const float y = a.y3[k], ty = a.ty3[k];
+    z.x += y * wd.x + ty * w.x;
+    z.y += y * wd.y + ty * w.y;
+  }
+  *reinterpret_cast<float2*>(a.part + (int64_t)c * HID + 2 * t) = z;
+  if (c == 0) {
     const int act = a.action[a.slot[0]];
-    a.td4[n] = a.h[n] > 0.f ? a.tw[a.off[8] + n * a.A + act] : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = t + 256 * h;
+      a.td4[n] = a.h[n] > 0.f ? a.tw[a.off[8] + n * a.A + act] : 0.f;
+    }
   }
 }
 
-// 5. ddot3 partial over n in [32 s, 32 s + 32): Wdot1 d4 + W1 ddot4
-__global__ void hvp_b3_kernel(HvpArgs a) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+// 5. ddot3[k] = relu'(y3[k]) sum_n (Wdot1[k][n] d4[n] + W1[k][n] ddot4[n]):
+// one wave per row k (lane l: columns 8 l .. 8 l + 7, 16-byte loads).
+__global__ __launch_bounds__(256) void hvp_b3_kernel(HvpArgs a) {
+  const int lane = threadIdx.x & 63, k = 4 * blockIdx.x + (threadIdx.x >> 6);
   if (k >= FLAT) return;
-  const float *W = a.th + a.off[6] + (int64_t)k * HID, *Wd = a.tw + a.off[6] + (int64_t)k * HID;
-  constexpr int NS = HID / HVP_SPLITS;  // 32
+  const float *W = a.th + a.off[6] + (int64_t)k * HID + 8 * lane, *Wd = a.tw + a.off[6] + (int64_t)k * HID + 8 * lane;
   float z = 0.f;
-  for (int n = s * NS; n < (s + 1) * NS; ++n) z += Wd[n] * a.d4[n] + W[n] * a.td4[n];
-  a.part[(int64_t)s * FLAT + k] = z;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float4 w = reinterpret_cast<const float4*>(W)[h], wd = reinterpret_cast<const float4*>(Wd)[h];
+    const float4 d = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
+    const float4 dd = reinterpret_cast<const float4*>(a.td4 + 8 * lane)[h];
+    z += ((wd.x * d.x + w.x * dd.x) + (wd.y * d.y + w.y * dd.y)) + ((wd.z * d.z + w.z * dd.z) + (wd.w * d.w + w.w * dd.w));
+  }
+  z = wave_sum(z);
+  if (lane == 0) a.td3[k] = a.y3[k] > 0.f ? z : 0.f;
 }
 
-// 6./7. transposed-conv tangent partials over kernel row kh = split
-template <int IH, int CI, int K, int S, int CO, int OH>
-__device__ __forceinline__ float hvp_convT_t(const float* d, const float* dd, const float* W, const float* Wd,
-                                             int ih, int iw, int ci, int kh) {
+// 6. ddot2[pix][ci] = relu'(y2) sum_{taps, co} (d3 Wdot3 + ddot3 W3) (the
+// transposed conv3, stride 1).  Block (pix, 16-channel group g); thread
+// (ci, output-channel quad cs = t % 16): 16-byte W loads along co.
+__global__ __launch_bounds__(256) void hvp_b2_kernel(HvpArgs a) {
+  __shared__ float s_r[16][17];
+  const int t = threadIdx.x, pix = blockIdx.x, g = blockIdx.y;
+  const int ih = pix / C2O, iw = pix % C2O, cs = t & 15, cl = t >> 4, ci = 16 * g + cl;
   float z = 0.f;
-  const int th = ih - kh;
-  if (th < 0 || th % S) return 0.f;
-  const int oh = th / S;
-  if (oh >= OH) return 0.f;
-  for (int kw = 0; kw < K; ++kw) {
-    const int tw = iw - kw;
-    if (tw < 0 || tw % S) continue;
-    const int ow = tw / S;
-    if (ow >= OH) continue;
-    for (int co = 0; co < CO; ++co) {
-      const int src = (oh * OH + ow) * CO + co;
-      const int wi = ((kh * K + kw) * CI + ci) * CO + co;
-      z += d[src] * Wd[wi] + dd[src] * W[wi];
+  for (int kh = 0; kh < C3K; ++kh) {
+    const int oh = ih - kh;
+    if (oh < 0 || oh >= C3O) continue;
+    for (int kw = 0; kw < C3K; ++kw) {
+      const int ow = iw - kw;
+      if (ow < 0 || ow >= C3O) continue;
+      const int src = (oh * C3O + ow) * C3CO + 4 * cs;
+      const int64_t wi = ((kh * C3K + kw) * C3CI + ci) * C3CO + 4 * cs;
+      const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
+      const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
+      const float4 d = *reinterpret_cast<const float4*>(a.d3 + src);
+      const float4 dd = *reinterpret_cast<const float4*>(a.td3 + src);
+      z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) + ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
     }
   }
-  return z;
+  s_r[cl][cs] = z;
+  __syncthreads();
+  if (t < 16) {
+    const int c = 16 * g + t;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += s_r[t][k];
+    a.td2[pix * C2CO + c] = a.y2[pix * C2CO + c] > 0.f ? v : 0.f;
+  }
 }
 
-__global__ void hvp_b2_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
-  if (i >= C2M * C2CO) return;
-  const int pix = i / C2CO, ci = i % C2CO;
-  a.part[(int64_t)kh * (C2M * C2CO) + i] = hvp_convT_t<C2O, C3CI, C3K, 1, C3CO, C3O>(
-      a.d3, a.td3, a.th + a.off[4], a.tw + a.off[4], pix / C2O, pix % C2O, ci, kh);
+// 7. ddot1[pix][ci] = relu'(y1) sum_{taps, co} (d2 Wdot2 + ddot2 W2) (the
+// transposed conv2, stride 2: at most 2 x 2 live taps).  Block pix; thread
+// (ci = t / 8, output-channel octet cs = t % 8).
+__global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
+  __shared__ float s_r[C2CI][9];
+  const int t = threadIdx.x, pix = blockIdx.x;
+  const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
+  float z = 0.f;
+  for (int kh = (ih & 1); kh < C2K; kh += C2S) {
+    const int oh = (ih - kh) / C2S;
+    if (ih < kh || oh >= C2O) continue;
+    for (int kw = (iw & 1); kw < C2K; kw += C2S) {
+      const int ow = (iw - kw) / C2S;
+      if (iw < kw || ow >= C2O) continue;
+      const int src = (oh * C2O + ow) * C2CO + 8 * cs;
+      const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
+        const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
+        const float4 d = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
+        const float4 dd = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
+        z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) +
+             ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
+      }
+    }
+  }
+  s_r[ci][cs] = z;
+  __syncthreads();
+  if (t < C2CI) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += s_r[t][k];
+    a.td1[pix * C1CO + t] = a.y1[pix * C1CO + t] > 0.f ? v : 0.f;
+  }
 }
 
-__global__ void hvp_b1_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, kh = blockIdx.y;
-  if (i >= C1M * C1CO) return;
-  const int pix = i / C1CO, ci = i % C1CO;
-  a.part[(int64_t)kh * (C1M * C1CO) + i] = hvp_convT_t<C1O, C2CI, C2K, C2S, C2CO, C2O>(
-      a.d2, a.td2, a.th + a.off[2], a.tw + a.off[2], pix / C1O, pix % C1O, ci, kh);
-}
+// 8. Every parameter-gradient block of H_q w in one launch, grid in ranges:
+//   [257] conv1 rows k (row 256 = bias): sum_p x_p[k] ddot1[p][co] over 8
+//         position splits (thread (split, co));
+//   [513] conv2 rows, [577] conv3 rows (last row = bias):
+//         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
+//         splits (thread (split, co));
+//   [2]   fc2 / fc1 bias / fc2 bias: hdot = relu'(h) (bdot1 + sum of t4's
+//         chunk partials), the fc2 column a = hdot;
+//   [...] fc1: ydot3 (x) d4 + y3 (x) ddot4, 4 elements per thread.
+constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = 2;
+constexpr int HVP_G_FC = FLAT * HID / 4 / 256;  // 1568
+constexpr int HVP_G_BLOCKS = HVP_G_C1 + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC;
 
-// 8. d/deps of conv1's weight gradient, partial over positions [25 s, 25 s + 25);
-// row 256 = the bias (sum over positions of ddot1)
-constexpr int HVP_C1_PS = C1M / HVP_SPLITS;  // 25
-__global__ void hvp_g_conv1_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
-  constexpr int N = (C1KK + 1) * C1CO;
-  if (i >= N) return;
-  const int k = i / C1CO, co = i % C1CO;
+template <int IH, int CI, int K, int S, int CO, int OH>
+__device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
+                                               const float* dd, int k, float* dst_w, float* dst_b, float (*s_r)[64]) {
+  const int t = threadIdx.x, co = t & 63, sp = t >> 6;  // 4 position splits
+  constexpr int P = OH * OH, PS = (P + 3) / 4;
+  const int p0 = sp * PS, p1 = min(P, p0 + PS);
   float g = 0.f;
-  if (k == C1KK) {
-    for (int p = s * HVP_C1_PS; p < (s + 1) * HVP_C1_PS; ++p) g += a.td1[p * C1CO + co];
+  if (k == K * K * CI) {
+    for (int p = p0; p < p1; ++p) g += dd[p * CO + co];
   } else {
-    const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
-    for (int p = s * HVP_C1_PS; p < (s + 1) * HVP_C1_PS; ++p)
-      g += hvp_x(a, C1S * (p / C1O) + kh, C1S * (p % C1O) + kw, ci) * a.td1[p * C1CO + co];
-  }
-  a.part[(int64_t)s * N + i] = g;
-}
-
-template <int IH, int CI, int K, int S, int CO, int OH>
-__device__ __forceinline__ float hvp_dw(const float* y, const float* yd, const float* d, const float* dd, int k,
-                                        int co) {
-  const int kh = k / (K * CI), kw = (k / CI) % K, ci = k % CI;
-  float g = 0.f;
-  for (int p = 0; p < OH * OH; ++p) {
-    const int src = (((p / OH) * S + kh) * IH + (p % OH) * S + kw) * CI + ci;
-    g += yd[src] * d[p * CO + co] + y[src] * dd[p * CO + co];
-  }
-  return g;
-}
-
-__global__ void hvp_g_conv23_kernel(HvpArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  constexpr int N2 = (C2KK + 1) * C2CO, N3 = (C3KK + 1) * C3CO;
-  if (i < N2) {
-    const int k = i / C2CO, co = i % C2CO;
-    if (k == C2KK) {
-      float g = 0.f;
-      for (int p = 0; p < C2M; ++p) g += a.td2[p * C2CO + co];
-      a.hq[a.off[3] + co] = g;
-    } else {
-      a.hq[a.off[2] + k * C2CO + co] = hvp_dw<C1O, C1CO, C2K, C2S, C2CO, C2O>(a.y1, a.ty1, a.d2, a.td2, k, co);
-    }
-  } else if (i < N2 + N3) {
-    const int j = i - N2, k = j / C3CO, co = j % C3CO;
-    if (k == C3KK) {
-      float g = 0.f;
-      for (int p = 0; p < C3M; ++p) g += a.td3[p * C3CO + co];
-      a.hq[a.off[5] + co] = g;
-    } else {
-      a.hq[a.off[4] + k * C3CO + co] = hvp_dw<C2O, C2CO, C3K, 1, C3CO, C3O>(a.y2, a.ty2, a.d3, a.td3, k, co);
+    const int kh = k / (K * CI), kw = (k / CI) % K, ci = k % CI;
+    for (int p = p0; p < p1; ++p) {
+      const int src = (((p / OH) * S + kh) * IH + (p % OH) * S + kw) * CI + ci;
+      g += yd[src] * d[p * CO + co] + y[src] * dd[p * CO + co];
     }
   }
+  s_r[sp][co] = g;
+  __syncthreads();
+  if (t < CO) {
+    const float v = (s_r[0][t] + s_r[1][t]) + (s_r[2][t] + s_r[3][t]);
+    if (k == K * K * CI)
+      dst_b[t] = v;
+    else
+      dst_w[k * CO + t] = v;
+  }
 }
 
-__global__ void hvp_g_fc_kernel(HvpArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n1 = (int64_t)FLAT * HID;
-  if (i < n1) {
-    const int k = (int)(i / HID), n = (int)(i % HID);
-    a.hq[a.off[6] + i] = a.ty3[k] * a.d4[n] + a.y3[k] * a.td4[n];
-  } else if (i < n1 + HID) {
-    const int n = (int)(i - n1);
+__global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
+  __shared__ float s_r[8][64];
+  const int t = threadIdx.x;
+  int i = blockIdx.x;
+  if (i < HVP_G_C1) {  // conv1: thread (split = t / 32 of 50 positions, co)
+    const int k = i, co = t & 31, sp = t >> 5;
+    float g = 0.f;
+    if (k == C1KK) {
+      for (int p = 50 * sp; p < 50 * sp + 50; ++p) g += a.td1[p * C1CO + co];
+    } else {
+      const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
+      const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
+      const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
+      for (int p = 50 * sp; p < 50 * sp + 50; ++p) {
+        const float x = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
+        g += x * a.td1[p * C1CO + co];
+      }
+    }
+    s_r[sp][co] = g;
+    __syncthreads();
+    if (t < C1CO) {
+      float v = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v += s_r[s][t];
+      a.hq[a.off[0] + (int64_t)k * C1CO + t] = v;  // row 256 is the bias (off[1] = off[0] + 8192)
+    }
+    return;
+  }
+  i -= HVP_G_C1;
+  if (i < HVP_G_C2) {
+    hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i, a.hq + a.off[2], a.hq + a.off[3],
+                                                   s_r);
+    return;
+  }
+  i -= HVP_G_C2;
+  if (i < HVP_G_C3) {
+    hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i, a.hq + a.off[4], a.hq + a.off[5],
+                                                 s_r);
+    return;
+  }
+  i -= HVP_G_C3;
+  if (i < HVP_G_H) {  // hidden unit n: hdot, fc2 column, fc1 bias; fc2 bias = 0
+    const int n = 256 * i + t, act = a.action[a.slot[0]];
+    float z = a.tw[a.off[7] + n];
+    for (int c = 0; c < HVP_T4_CHUNKS; ++c) z += a.part[(int64_t)c * HID + n];
+    const float hd = a.h[n] > 0.f ? z : 0.f;
+    for (int col = 0; col < a.A; ++col) a.hq[a.off[8] + (int64_t)n * a.A + col] = col == act ? hd : 0.f;
     a.hq[a.off[7] + n] = a.td4[n];
-  } else if (i < n1 + HID + (int64_t)HID * a.A) {
-    const int j = (int)(i - n1 - HID), n = j / a.A, col = j % a.A;
-    a.hq[a.off[8] + j] = col == a.action[a.slot[0]] ? a.th4[n] : 0.f;
-  } else if (i < n1 + HID + (int64_t)HID * a.A + a.A) {
-    a.hq[a.off[9] + (i - n1 - HID - (int64_t)HID * a.A)] = 0.f;
+    if (i == 0 && t < a.A) a.hq[a.off[9] + t] = 0.f;
+    return;
+  }
+  i -= HVP_G_H;
+  {  // fc1 rows: 4 consecutive columns per thread
+    const int64_t e = ((int64_t)i * 256 + t) * 4;
+    const int k = (int)(e / HID), n = (int)(e % HID);
+    const float ty = a.ty3[k], y = a.y3[k];
+    const float4 d = *reinterpret_cast<const float4*>(a.d4 + n);
+    const float4 dd = *reinterpret_cast<const float4*>(a.td4 + n);
+    *reinterpret_cast<float4*>(a.hq + a.off[6] + e) =
+        make_float4(ty * d.x + y * dd.x, ty * d.y + y * dd.y, ty * d.z + y * dd.z, ty * d.w + y * dd.w);
   }
 }
 
@@ -285,27 +424,17 @@ __global__ __launch_bounds__(256) void meta_second_kernel(MetaSecondArgs a, cons
 }
 
 // v = v_dir + J (alpha s1 grad q - clip(td') H_q w), alpha = [|td'| < bound];
-// s1 = sum of the partials (every block re-sums them: deterministic).
+// s1 = grad q . w, summed once by hvp_t1_kernel's last block.
 __global__ __launch_bounds__(256) void meta_combine_kernel(MetaSecondArgs a, const float* __restrict__ vdir,
                                                            const float* __restrict__ J, const float* __restrict__ gq,
-                                                           const float* __restrict__ hq,
-                                                           const float* __restrict__ s1_part, int nparts,
+                                                           const float* __restrict__ hq, const float* __restrict__ s1,
                                                            float* __restrict__ v_out) {
-  __shared__ float sbuf[4];
-  __shared__ float s_s1;
-  float p = 0.f;
-  for (int j = threadIdx.x; j < nparts; j += blockDim.x) p += s1_part[j];
-  p = wave_sum(p);
-  if ((threadIdx.x & 63) == 0) sbuf[threadIdx.x >> 6] = p;
-  __syncthreads();
-  if (threadIdx.x == 0) s_s1 = (sbuf[0] + sbuf[1]) + (sbuf[2] + sbuf[3]);
-  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   const float td = a.td[0];
   const float alpha = fabsf(td) < a.bound ? 1.f : 0.f;
   const float clip = fminf(fmaxf(td, -a.bound), a.bound);
-  v_out[i] = vdir[i] + J[i] * (alpha * s_s1 * gq[i] - clip * hq[i]);
+  v_out[i] = vdir[i] + J[i] * (alpha * s1[0] * gq[i] - clip * hq[i]);
 }
 
 }  // namespace dqz

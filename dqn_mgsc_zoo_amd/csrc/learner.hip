@@ -74,7 +74,8 @@ static int init_kernel_attrs() {
   DQZ_HIP(hipFuncSetAttribute((const void*)conv1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kConv1FwdSmem));
   const void* fwd_kernels[] = {(const void*)fwd_conv_kernel<0>, (const void*)fwd_conv_kernel<1>,
-                               (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>};
+                               (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>,
+                               (const void*)tangent_fwd_kernel};
   for (const void* k : fwd_kernels)
     DQZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kConv1FwdSmem));
   g_attr_done = 1;
@@ -1102,7 +1103,7 @@ struct dqz_meta {
   int nparts;
   // second-order (reservoir) meta-gradient
   float *GQ, *HQ, *s1_part, *hpart;
-  float *ty1, *ty2, *ty3, *th4, *td4, *td3, *td2, *td1;
+  float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
   int nparts2;
   void* block;
 };
@@ -1147,13 +1148,13 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            (int64_t)H->lm->S_fc1 * C * HID,
                            M, KC, KC, M, 1, H->nparts2, KC, KC, multi * H->total,
                            so * H->total, so * H->total, so * H->nparts2,
-                           so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * HID, so * FLAT,
-                           so * C2M * C2CO, so * C1M * C1CO, so * HVP_SPLITS * C1M * C1CO};
+                           so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
+                           so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
-                    &H->ty1, &H->ty2, &H->ty3, &H->th4, &H->td4, &H->td3, &H->td2, &H->td1, &H->hpart};
+                    &H->ty1, &H->ty2, &H->ty3, &H->td4, &H->td3, &H->td2, &H->td1, &H->s1, &H->hpart};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
@@ -1198,9 +1199,8 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   const int C = H->C, K = H->K;
 
   // p = softmax(logits[pos]); slots padded to K C with slots[M - 1] (p = 0 there)
-  hipLaunchKernelGGL(meta_softmax_kernel, dim3(1), dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p);
-  hipLaunchKernelGGL(meta_pad_slots_kernel, dim3((unsigned)((K * C + 255) / 256)), dim3(256), 0, st, slots, M,
-                     K * C, H->slots_pad);
+  hipLaunchKernelGGL(meta_softmax_kernel, dim3(1 + (unsigned)((K * C + META_THREADS - 1) / META_THREADS)),
+                     dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p, slots, K * C, H->slots_pad);
   DQZ_HIP(hipGetLastError());
 
   // G = sum_i p_i g_i: batched backwards with p-weighted cotangents, one per
@@ -1209,7 +1209,9 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     if (int rc = step_impl(L, P, S, H->slots_pad + (int64_t)k * C, nullptr, stream, kNoProfile, H->G,
                            H->p + (int64_t)k * C, nullptr, 0, k > 0 ? 1 : 0))
       return rc;
-    DQZ_HIP(hipMemcpyAsync(H->td + (int64_t)k * C, L->td, sizeof(float) * C, hipMemcpyDeviceToDevice, st));
+    // (one chunk: the batch learner's td stays current until the next update,
+    // dqz_meta_outputs copies it from there)
+    if (K > 1) DQZ_HIP(hipMemcpyAsync(H->td + (int64_t)k * C, L->td, sizeof(float) * C, hipMemcpyDeviceToDevice, st));
   }
 
   MetaRmsArgs ra;
@@ -1276,43 +1278,28 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hv.ty1 = H->ty1;
     hv.ty2 = H->ty2;
     hv.ty3 = H->ty3;
-    hv.th4 = H->th4;
     hv.td4 = H->td4;
     hv.td3 = H->td3;
     hv.td2 = H->td2;
     hv.td1 = H->td1;
     hv.hq = H->HQ;
     hv.part = H->hpart;
-    auto g256 = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
-    auto gs = [](int64_t n, int splits) { return dim3((unsigned)((n + 255) / 256), (unsigned)splits); };
-    auto fin = [&](int S, int N, const float* mask, const float* bias, int nb, float* out) {
-      hipLaunchKernelGGL(hvp_fin_kernel, g256(N), dim3(256), 0, st, H->hpart, S, N, mask, bias, nb, out);
-    };
-    const float* tw = H->nu1;
-    hipLaunchKernelGGL(hvp_t1_kernel, gs(C1M * C1CO, C1K), dim3(256), 0, st, hv);
-    fin(C1K, C1M * C1CO, L1->y1, tw + L1->off[1], C1CO, H->ty1);
-    hipLaunchKernelGGL(hvp_t2_kernel, gs(C2M * C2CO, C2K), dim3(256), 0, st, hv);
-    fin(C2K, C2M * C2CO, L1->y2, tw + L1->off[3], C2CO, H->ty2);
-    hipLaunchKernelGGL(hvp_t3_kernel, gs(FLAT, C3K), dim3(256), 0, st, hv);
-    fin(C3K, FLAT, L1->y3, tw + L1->off[5], C3CO, H->ty3);
-    hipLaunchKernelGGL(hvp_t4_kernel, gs(HID, HVP_SPLITS), dim3(256), 0, st, hv);
-    fin(HVP_SPLITS, HID, L1->h1, tw + L1->off[7], HID, H->th4);
-    hipLaunchKernelGGL(hvp_b3_kernel, gs(FLAT, HVP_SPLITS), dim3(256), 0, st, hv);
-    fin(HVP_SPLITS, FLAT, L1->y3, nullptr, 1, H->td3);
-    hipLaunchKernelGGL(hvp_b2_kernel, gs(C2M * C2CO, C3K), dim3(256), 0, st, hv);
-    fin(C3K, C2M * C2CO, L1->y2, nullptr, 1, H->td2);
-    hipLaunchKernelGGL(hvp_b1_kernel, gs(C1M * C1CO, C2K), dim3(256), 0, st, hv);
-    fin(C2K, C1M * C1CO, L1->y1, nullptr, 1, H->td1);
-    // conv1 w rows 0..255 and its bias row are contiguous in the layout (off[1] = off[0] + 8192)
-    hipLaunchKernelGGL(hvp_g_conv1_kernel, gs((C1KK + 1) * C1CO, HVP_SPLITS), dim3(256), 0, st, hv);
-    fin(HVP_SPLITS, (C1KK + 1) * C1CO, nullptr, nullptr, 1, H->HQ + L1->off[0]);
-    hipLaunchKernelGGL(hvp_g_conv23_kernel, g256((C2KK + 1) * C2CO + (C3KK + 1) * C3CO), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_g_fc_kernel, g256((int64_t)FLAT * HID + HID + (int64_t)HID * A + A), dim3(256), 0, st,
-                       hv);
+    hv.s1_part = H->s1_part;
+    hv.s1_nparts = H->nparts2;
+    hv.s1 = H->s1;
+    // eight dependent stages (hvp.hpp): tangent forward, tangent backward,
+    // then every parameter block of H_q w
+    hipLaunchKernelGGL(hvp_t1_kernel, dim3(C1M + 1), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t2_kernel, dim3(C2M, C2CO / 16), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t3_kernel, dim3(C3M, C3CO / 16), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_t4_kernel, dim3(HVP_T4_CHUNKS), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b3_kernel, dim3(FLAT / 4), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b2_kernel, dim3(C2M, C2CO / 16), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_b1_kernel, dim3(C1M), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_g_kernel, dim3(HVP_G_BLOCKS), dim3(256), 0, st, hv);
     DQZ_HIP(hipGetLastError());
     // v = v_dir + J (alpha s1 grad q - clip(td') H w) -> thp (theta' is no longer needed)
-    hipLaunchKernelGGL(meta_combine_kernel, eg1, dim3(256), 0, st, sa, H->mu1, H->J, H->GQ, H->HQ, H->s1_part,
-                       H->nparts2, H->thp);
+    hipLaunchKernelGGL(meta_combine_kernel, eg1, dim3(256), 0, st, sa, H->mu1, H->J, H->GQ, H->HQ, H->s1, H->thp);
     DQZ_HIP(hipGetLastError());
     nloss = H->nparts2;
   }
@@ -1338,8 +1325,6 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     c1.Z = 1;
     c1.linear = 1;
     c1.out = H->zv1;
-    hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, C), dim3(256), kConv1FwdSmem, st, c1);
-    DQZ_HIP(hipGetLastError());
     LayerFwdArgs c2;
     c2.in = L->y1;
     c2.nz = nv;
@@ -1349,15 +1334,11 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     c2.Z = 1;
     c2.linear = 1;
     c2.out = H->zv2;
-    hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, C), dim3(256), 0, st, c2);
-    DQZ_HIP(hipGetLastError());
     LayerFwdArgs c3 = c2;
     c3.in = L->y2;
     c3.w_off = L->off[4];
     c3.b_off = L->off[5];
     c3.out = H->zv3;
-    hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, C), dim3(256), 0, st, c3);
-    DQZ_HIP(hipGetLastError());
     Fc1FwdArgs f1;
     f1.sum = nullptr;
     f1.cnt = nullptr;
@@ -1367,7 +1348,9 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     f1.B = C;
     f1.MG = (C + 31) / 32;
     f1.part = H->zvp;
-    hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, f1.MG), dim3(256), 0, st, f1);
+    // the four layers' tangent outputs are independent: one launch
+    hipLaunchKernelGGL(tangent_fwd_kernel, dim3((unsigned)tangent_fwd_blocks(C, f1.MG)), dim3(256), kConv1FwdSmem,
+                       st, c1, c2, c3, f1);
     DQZ_HIP(hipGetLastError());
 
     MetaDotArgs md;
@@ -1430,7 +1413,8 @@ int dqz_meta_outputs(dqz_meta* H, float* probs, float* dlogits, float* td, float
   const int M = H->cfg.meta_batch;
   if (probs) DQZ_HIP(hipMemcpyAsync(probs, H->p, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
   if (dlogits) DQZ_HIP(hipMemcpyAsync(dlogits, H->dl, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
-  if (td) DQZ_HIP(hipMemcpyAsync(td, H->td, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
+  if (td)
+    DQZ_HIP(hipMemcpyAsync(td, H->K > 1 ? H->td : H->lm->td, sizeof(float) * M, hipMemcpyDeviceToDevice, st));
   if (loss) DQZ_HIP(hipMemcpyAsync(loss, H->loss, sizeof(float), hipMemcpyDeviceToDevice, st));
   return DQZ_OK;
 }

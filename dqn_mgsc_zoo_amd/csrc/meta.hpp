@@ -45,12 +45,20 @@ __device__ __forceinline__ float block_max_f32(float v, float* sbuf) {
 }
 
 // p = exp(x - (c + log(sum exp(x - c)))), c = max x  (JNPprobabilities_from_logits,
-// replay_circular.py:79-86).  One block striding over the M meta-batch
-// entries; x gathered from logits[pos].
+// replay_circular.py:79-86).  Block 0 strides over the M meta-batch entries
+// (x gathered from logits[pos]); blocks 1.. pad the slots to the chunked meta
+// batch, slots_pad[i] = slots[min(i, M - 1)] (one launch for both).
 __global__ __launch_bounds__(META_THREADS) void meta_softmax_kernel(const float* __restrict__ logits,
                                                                     const int32_t* __restrict__ pos, int M,
                                                                     float* __restrict__ x_out,
-                                                                    float* __restrict__ p_out) {
+                                                                    float* __restrict__ p_out,
+                                                                    const int32_t* __restrict__ slots, int n_pad,
+                                                                    int32_t* __restrict__ slots_pad) {
+  if (blockIdx.x > 0) {
+    const int i = (blockIdx.x - 1) * META_THREADS + threadIdx.x;
+    if (i < n_pad) slots_pad[i] = slots[min(i, M - 1)];
+    return;
+  }
   __shared__ float sbuf[META_THREADS / 64];
   float mx = -INFINITY;
   for (int i = threadIdx.x; i < M; i += META_THREADS) {
@@ -63,12 +71,6 @@ __global__ __launch_bounds__(META_THREADS) void meta_softmax_kernel(const float*
   for (int i = threadIdx.x; i < M; i += META_THREADS) se += expf(x_out[i] - c);
   const float lse = c + logf(block_sum_f32(se, sbuf));
   for (int i = threadIdx.x; i < M; i += META_THREADS) p_out[i] = expf(x_out[i] - lse);
-}
-
-// slots padded to the chunked meta batch: dst[i] = src[min(i, M - 1)].
-__global__ void meta_pad_slots_kernel(const int32_t* __restrict__ src, int M, int n, int32_t* __restrict__ dst) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = src[min(i, M - 1)];
 }
 
 struct MetaRmsArgs {
