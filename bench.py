@@ -41,6 +41,7 @@ if ROOT not in sys.path:
 METRIC = ('learner grad-steps/sec at batch=32, 84×84×4 uint8, '
           '1/2/4/8 MI355X')
 BATCH = 32
+META_BATCH = 100  # the meta-update timed apart at M = 100
 NUM_ACTIONS = 6  # Pong minimal action set (gym_atari.py:52-54)
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32 = f32 vector peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -534,11 +535,48 @@ class Workload:
         # the draw runs inside the learner's forward launch
         lrn.step_logits(store, lb, slots, seed=seed, counter=counter)
       self.samplers = {'logits_sample_standalone': mgsc_sample}
+      # The meta-update the agent runs once per learn step
+      # (dqn_mgsc_batched/agent.py:253), M = 100, timed apart:
+      # first order (dqn_mgsc_batched) and second order (the reservoir
+      # variant), on a fixed meta batch and online transition.
+      from dqn_mgsc_zoo_amd import replay as replay_lib  # pylint: disable=g-import-not-at-top
+      rng = np.random.default_rng(300 + rank)
+      self.meta_online = replay_lib.Transition(
+          rng.integers(0, 256, (84, 84, 4), dtype=np.uint8), 2, 1.0, 0.99,
+          rng.integers(0, 256, (84, 84, 4), dtype=np.uint8))
+      self.meta_slots = torch.from_numpy(
+          rng.choice(capacity, META_BATCH, replace=False).astype(np.int32)).to(dev)
     else:
       raise ValueError(algo)
     self.one_step = one_step
     torch.cuda.synchronize(dev)
     self.fill_s = time.perf_counter() - t_fill
+
+  def time_meta(self, iters):
+    """MGSC only: average ms per M = 100 meta-update, first and second order
+    (HIP events around `iters` back-to-back calls after 3 untimed ones)."""
+    if self.algo != 'mgsc':
+      return {}
+    from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
+    out = {}
+    for order in (0, 1):
+      meta = learner_lib.MetaLearner(self.lrn, META_BATCH, learner_lib.adam(2.5e-4),
+                                     second_order=bool(order))
+      meta.set_online_transition(self.meta_online)
+      lb, ms = self.logit_buf, self.meta_slots
+      fn = lambda: meta.update(self.store, ms, lb.logits, ms, logit_buffer=lb)  # pylint: disable=cell-var-from-loop
+      for _ in range(3):
+        fn()
+      e0 = torch.cuda.Event(enable_timing=True)
+      e1 = torch.cuda.Event(enable_timing=True)
+      e0.record()
+      for _ in range(iters):
+        fn()
+      e1.record()
+      e1.synchronize()
+      out['M%d_%s_order' % (META_BATCH, 'second' if order else 'first')] = e0.elapsed_time(e1) / iters
+      del meta
+    return out
 
   def time_samplers(self, iters):
     """Average ms per launch of each sampler call, back to back on the
@@ -663,6 +701,7 @@ def run_gpu(args, g, rem):
   if 'conv1_fwd' in phases and 'conv2_fwd' not in phases:  # the one conv1..conv3 launch
     phases = {('conv_fwd' if k == 'conv1_fwd' else k): v for k, v in phases.items()}
   sampler_ms = wl.time_samplers(args.profile_iters)
+  meta_ms = wl.time_meta(max(20, args.profile_iters // 10))
   q_tm1, td, loss = lrn.fetch_outputs()
   torch.cuda.synchronize(dev)
   finite = bool(torch.isfinite(lrn.online).all().item())
@@ -768,6 +807,7 @@ def run_gpu(args, g, rem):
     # the reference's own per-call timings of this agent (V100 + JAX):
     # dqn_mgsc_batched/run_atari.py:308-315
     out['reference_per_call_ms'] = {'update': 12.24, 'replay_sample_batch': 57.1}
+    out['meta_update_us'] = {k: round(1e3 * v, 2) for k, v in meta_ms.items()}
   if world == 1 and args.cpu_seconds > 0:
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
   else:
