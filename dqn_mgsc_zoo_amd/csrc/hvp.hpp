@@ -316,22 +316,26 @@ __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y,
 
 __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
+  __shared__ float s_x[C1M];
   const int t = threadIdx.x;
   int i = blockIdx.x;
   if (i < HVP_G_C1) {  // conv1: thread (split = t / 32 of 50 positions, co)
+    // the row's 400 patch values x_p[k] staged once (a loop of scattered
+    // byte loads per thread was 11 of this launch's 20 us)
     const int k = i, co = t & 31, sp = t >> 5;
-    float g = 0.f;
-    if (k == C1KK) {
-      for (int p = 50 * sp; p < 50 * sp + 50; ++p) g += a.td1[p * C1CO + co];
-    } else {
+    if (k < C1KK) {
       const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
       const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
       const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
-      for (int p = 50 * sp; p < 50 * sp + 50; ++p) {
-        const float x = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
-        g += x * a.td1[p * C1CO + co];
-      }
+      for (int p = t; p < C1M; p += 256)
+        s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
+    } else {
+      for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
     }
+    __syncthreads();
+    float g = 0.f;
+#pragma unroll 10
+    for (int p = 50 * sp; p < 50 * sp + 50; ++p) g += s_x[p] * a.td1[p * C1CO + co];
     s_r[sp][co] = g;
     __syncthreads();
     if (t < C1CO) {
