@@ -806,7 +806,11 @@ def run_gpu(args, g, rem):
   if algo == 'mgsc':
     # the reference's own per-call timings of this agent (V100 + JAX):
     # dqn_mgsc_batched/run_atari.py:308-315
-    out['reference_per_call_ms'] = {'update': 12.24, 'replay_sample_batch': 57.1}
+    out['reference_per_call_ms'] = {'update': 12.24, 'replay_sample_batch': 57.1,
+                                    # 206.19 s / 49,924 calls, --meta_batch_size=5
+                                    # (run_mgscdqnbatched_normal_timing.sh:50)
+                                    'meta_update_M5': 4.13,
+                                    'replay_sample_meta_batch': 55.6}
     out['meta_update_us'] = {k: round(1e3 * v, 2) for k, v in meta_ms.items()}
   if world == 1 and args.cpu_seconds > 0:
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
