@@ -42,6 +42,7 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
                                          second_order=self._SECOND_ORDER)
     self._last_transitions = []
     self._slots_cache = None
+    self._upload = None  # pinned staging of the per-learn host draws
 
   def step(self, timestep):
     """agent.py:237-280."""
@@ -86,8 +87,9 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
     """agent.py:302-334: meta batch, meta_update, update_priorities."""
     import torch  # pylint: disable=g-import-not-at-top
     _, slots, positions = self._replay.meta_batch_slots(self._meta_batch_size)
-    pos = torch.as_tensor(positions.astype('int32'),
-                          device=self._learner.device)
+    pos = self._uploader()(torch.empty((len(positions),), dtype=torch.int32,
+                                       device=self._learner.device),
+                           np.asarray(positions, np.int32))
     self._meta.set_online_transition(online_transition)
     dl = self._replay.device_logits  # running log-sum-exp kept current
     self._meta.update(self._store(), slots, dl.logits, pos, logit_buffer=dl)
@@ -103,9 +105,18 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
       self._slots_cache = (torch.zeros((self._batch_size,), dtype=torch.int32, device=dev),
                            torch.zeros((self._batch_size,), dtype=torch.float64, device=dev))
     slots, u_dev = self._slots_cache
-    u_dev.copy_(torch.from_numpy(np.asarray(u, np.float64)))
+    self._uploader()(u_dev, np.asarray(u, np.float64))
     self._learner.step_logits(self._store(), self._replay.device_logits, slots,
                               uniforms=u_dev)
+
+  def _uploader(self):
+    """Host -> device copies without a host wait (store.Uploader): the meta
+    batch's positions and the learn step's uniforms would otherwise block
+    until the meta-update queued before them had finished."""
+    if self._upload is None:
+      from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
+      self._upload = store_lib.Uploader(8 * max(self._meta_batch_size, self._batch_size))
+    return self._upload
 
   @property
   def meta_learner(self) -> learner_lib.MetaLearner:

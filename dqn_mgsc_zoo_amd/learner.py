@@ -352,6 +352,7 @@ class MetaLearner:
     self.loss = torch.zeros((1,), dtype=torch.float32, device=dev)
     self.online_store = store_lib.FrameStore(1, 8, device=dev)
     self.online_store.fidx[0].copy_(torch.arange(8, dtype=torch.int32))
+    self._upload = None  # pinned staging of set_online_transition
     self.online_slot = torch.zeros((1,), dtype=torch.int32, device=dev)
     opt = learner.optimizer
     cfg = _native.DqzMetaConfig(
@@ -377,12 +378,13 @@ class MetaLearner:
     frames = np.concatenate([np.moveaxis(s_tm1, -1, 0),
                              np.moveaxis(s_t, -1, 0)]).reshape(8, -1)
     st = self.online_store
-    st.frames.copy_(torch.from_numpy(np.ascontiguousarray(frames)))
-    meta = torch.tensor([float(transition.r_t), float(transition.discount_t)],
-                        dtype=torch.float32)
-    st.action[0] = int(transition.a_tm1)
-    st.reward.copy_(meta[:1])
-    st.discount.copy_(meta[1:])
+    if self._upload is None:  # pinned staging: no host wait on queued work
+      from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
+      self._upload = store_lib.Uploader(frames.nbytes)
+    self._upload(st.frames, frames)
+    self._upload(st.action, np.array([int(transition.a_tm1)], np.int32))
+    self._upload(st.reward, np.array([float(transition.r_t)], np.float32))
+    self._upload(st.discount, np.array([float(transition.discount_t)], np.float32))
 
   def update(self, store, slots, logits, positions, stream=None,
              logit_buffer=None):

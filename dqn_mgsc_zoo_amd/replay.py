@@ -182,6 +182,7 @@ class _DeviceStorage:
     self.allocator = store_lib.FrameAllocator(self.store, mode,
                                               per_slot=frames_per_slot)
     self.device_name = device
+    self._slots_upload = None  # pinned staging of slots_tensor
 
   def put(self, slot, item, oldest_live_slot=None):
     s_tm1 = np.asarray(item.s_tm1, np.uint8)
@@ -198,8 +199,14 @@ class _DeviceStorage:
     self.allocator.forget(slot)
 
   def slots_tensor(self, slots):
-    return self._torch.as_tensor(np.asarray(slots, np.int32),
-                                 device=self.store.device)
+    """Device int32 copy of host slots, uploaded without a host wait
+    (store.Uploader; a fresh tensor per call, so callers may keep it)."""
+    a = np.asarray(slots, np.int32)
+    if self._slots_upload is None or self._slots_upload.nbytes < a.nbytes:
+      from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
+      self._slots_upload = store_lib.Uploader(max(a.nbytes, 4096))
+    return self._slots_upload(self._torch.empty(a.shape, dtype=self._torch.int32,
+                                                device=self.store.device), a)
 
   def stack(self, structure, slots):
     """Device Transition: uint8 stacks gathered on device, int32/f32 rest."""

@@ -27,6 +27,42 @@ STACK = _native.STACK
 _STAGE_SLOTS = 64
 
 
+class Uploader:
+  """Host -> device copies that do not wait for the device.
+
+  A pageable `tensor.copy_(host)` blocks the host until every launch queued
+  before it has finished (in the MGSC agent: the whole meta-update before
+  the learn step's 32 uniforms).  Here the host array is written into one of
+  a ring of pinned staging buffers and copied with non_blocking=True on the
+  current stream; a buffer is reused once the copy that read it has
+  completed (one event per buffer), so a call returns at once."""
+
+  def __init__(self, nbytes, slots=8):
+    self.nbytes = int(nbytes)
+    self._buf = torch.empty((slots, self.nbytes), dtype=torch.uint8, pin_memory=True)
+    self._np = self._buf.numpy()
+    self._ev = [None] * slots
+    self._k = 0
+
+  def __call__(self, dst, array):
+    """dst (contiguous device tensor) <- array (same itemsize, dst.numel() items)."""
+    a = np.ascontiguousarray(array)
+    n = a.nbytes
+    if (n > self.nbytes or not dst.is_contiguous() or a.dtype.itemsize != dst.element_size()
+        or dst.numel() * dst.element_size() != n):
+      raise ValueError('upload of %s %s into %s %s' % (a.dtype, a.shape, dst.dtype, tuple(dst.shape)))
+    k = self._k
+    self._k = (k + 1) % len(self._ev)
+    if self._ev[k] is not None:
+      self._ev[k].synchronize()
+    self._np[k, :n] = a.view(np.uint8).reshape(-1)
+    dst.view(-1).view(torch.uint8).copy_(self._buf[k, :n], non_blocking=True)
+    if self._ev[k] is None:
+      self._ev[k] = torch.cuda.Event()
+    self._ev[k].record()
+    return dst
+
+
 class FrameStore:
   """Device frame pool + transition table (see module docstring)."""
 
