@@ -352,7 +352,6 @@ class MetaLearner:
     self.loss = torch.zeros((1,), dtype=torch.float32, device=dev)
     self.online_store = store_lib.FrameStore(1, 8, device=dev)
     self.online_store.fidx[0].copy_(torch.arange(8, dtype=torch.int32))
-    self._upload = None  # pinned staging of set_online_transition
     self.online_slot = torch.zeros((1,), dtype=torch.int32, device=dev)
     opt = learner.optimizer
     cfg = _native.DqzMetaConfig(
@@ -372,19 +371,15 @@ class MetaLearner:
       self._h = None
 
   def set_online_transition(self, transition):
-    """Uploads the newest host transition (uint8 [84,84,4] stacks)."""
+    """Uploads the newest host transition (uint8 [84,84,4] stacks): its eight
+    channel frames (s_tm1 0..3, s_t 4..7) as pool rows 0..7 of the one-slot
+    store plus its {a, r, d} record, in one launch that reads pinned staging
+    in place (FrameStore.put / dqz_store_put): no host wait on queued work."""
     s_tm1 = np.asarray(transition.s_tm1, np.uint8)
     s_t = np.asarray(transition.s_t, np.uint8)
-    frames = np.concatenate([np.moveaxis(s_tm1, -1, 0),
-                             np.moveaxis(s_t, -1, 0)]).reshape(8, -1)
-    st = self.online_store
-    if self._upload is None:  # pinned staging: no host wait on queued work
-      from dqn_mgsc_zoo_amd import store as store_lib  # pylint: disable=g-import-not-at-top
-      self._upload = store_lib.Uploader(frames.nbytes)
-    self._upload(st.frames, frames)
-    self._upload(st.action, np.array([int(transition.a_tm1)], np.int32))
-    self._upload(st.reward, np.array([float(transition.r_t)], np.float32))
-    self._upload(st.discount, np.array([float(transition.discount_t)], np.float32))
+    frames = [(c, s_tm1[..., c]) for c in range(4)] + [(4 + c, s_t[..., c]) for c in range(4)]
+    self.online_store.put(0, range(8), int(transition.a_tm1), float(transition.r_t),
+                          float(transition.discount_t), frames)
 
   def update(self, store, slots, logits, positions, stream=None,
              logit_buffer=None):
