@@ -19,6 +19,7 @@ import torch
 
 from dqn_mgsc_zoo_amd import learner as learner_lib
 from dqn_mgsc_zoo_amd import networks as networks_lib
+from dqn_mgsc_zoo_amd import optim_state
 from dqn_mgsc_zoo_amd import parts
 
 
@@ -176,20 +177,20 @@ class DeviceDqnAgent(parts.Agent):
     lrn = self._learner
     self.check_learner_health()
     return {
-        'rng_key': {'seed': self._act_seed, 'count': self._act_count},
+        'rng_key': optim_state.pack_key(self._act_seed, self._act_count),
         'frame_t': self._frame_t,
-        'opt_state': (lrn.params_tree('mu'), lrn.params_tree('nu')),
+        'opt_state': optim_state.rmsprop_state(lrn.params_tree('mu'),
+                                               lrn.params_tree('nu')),
         'online_params': lrn.params_tree('online'),
         'target_params': lrn.params_tree('target'),
         'replay': self._replay.get_state(),
     }
 
   def set_state(self, state: Mapping[str, Any]) -> None:
-    self._act_seed = state['rng_key']['seed']
-    self._act_count = state['rng_key']['count']
+    self._act_seed, self._act_count = optim_state.unpack_key(state['rng_key'])
     self._frame_t = state['frame_t']
     self._learner.set_params(state['online_params'], state['target_params'])
-    self._learner.set_opt_state(*state['opt_state'])
+    self._learner.set_opt_state(*optim_state.rmsprop_moments(state['opt_state']))
     self._replay.set_state(state['replay'])
 
   def _store(self):

@@ -14,6 +14,7 @@ import torch
 
 from dqn_mgsc_zoo_amd import _native
 from dqn_mgsc_zoo_amd import networks as networks_lib
+from dqn_mgsc_zoo_amd import optim_state
 
 ALGOS = {'dqn': _native.ALGO_DQN, 'double': _native.ALGO_DOUBLE,
          'per': _native.ALGO_PER}
@@ -416,11 +417,14 @@ class MetaLearner:
     return self.probs, self.dlogits, self.td, self.loss
 
   def get_state(self):
-    """optax ScaleByAdamState(count, mu, nu) as host arrays."""
-    return {'count': int(self.adam_count.item()),
-            'mu': self.adam_mu.cpu().numpy(), 'nu': self.adam_nu.cpu().numpy()}
+    """optax.adam's state, (ScaleByAdamState(count, mu, nu), EmptyState()),
+    with host arrays (dqn_mgsc_batched/agent.py:80,390)."""
+    return optim_state.adam_state(int(self.adam_count.item()),
+                                  self.adam_mu.cpu().numpy(),
+                                  self.adam_nu.cpu().numpy())
 
   def set_state(self, state):
-    self.adam_count.fill_(int(state['count']))
-    self.adam_mu.copy_(torch.as_tensor(np.asarray(state['mu'], np.float32)))
-    self.adam_nu.copy_(torch.as_tensor(np.asarray(state['nu'], np.float32)))
+    count, mu, nu = optim_state.adam_moments(state)
+    self.adam_count.fill_(count)
+    self.adam_mu.copy_(torch.as_tensor(np.asarray(mu, np.float32)))
+    self.adam_nu.copy_(torch.as_tensor(np.asarray(nu, np.float32)))

@@ -234,7 +234,7 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
   logits0 = replay.logits.clone()
   _run(agent, 120, seed=3)
   meta = agent.meta_learner
-  assert meta.get_state()['count'] > 0
+  assert meta.get_state()[0].count > 0
   lg = replay.logits.cpu().numpy()
   assert np.isfinite(lg[lg != -np.inf]).all()
   assert not torch.equal(logits0, replay.logits)
@@ -258,7 +258,7 @@ def _check_meta_step_against_oracle(agent, replay, stop_gradient):
     return out
 
   replay.meta_batch_slots = spy
-  st = meta.get_state()
+  st = meta.get_state()[0]
   before = replay.logits.cpu().numpy()
   env = fake_env.FakeAtari(episode_len=9, seed=44)
   stacker = fake_env.FrameStacker()
@@ -278,7 +278,7 @@ def _check_meta_step_against_oracle(agent, replay, stop_gradient):
       *trees, mb, before[positions],
       dict(s_tm1=trans.s_tm1, a_tm1=2, r_t=trans.r_t,
            discount_t=trans.discount_t, s_t=trans.s_t),
-      st['mu'], st['nu'], st['count'], lr=LR, decay=DECAY, eps=EPS,
+      st.mu, st.nu, st.count, lr=LR, decay=DECAY, eps=EPS,
       grad_error_bound=BOUND, stop_gradient=stop_gradient)
   after = replay.logits.cpu().numpy()
   np.testing.assert_allclose(after[positions], ref['new_logits'], atol=1e-6)
@@ -313,7 +313,7 @@ def test_mgsc_reservoir_agent_run_loop(device):
   assert agent.meta_learner.second_order
   _run(agent, 260)
   assert replay.size == replay.capacity
-  assert agent.meta_learner.get_state()['count'] > 10
+  assert agent.meta_learner.get_state()[0].count > 10
   lg = replay.logits.cpu().numpy()
   assert np.isfinite(lg).all()
   assert torch.isfinite(agent.learner.online).all()

@@ -102,6 +102,16 @@ def test_checkpoint_save_restore_continues_bit_exactly(device, tmp_path, kind):
   from dqn_mgsc_zoo_amd import parts
   a1, r1 = _agent(kind, seed=4)
   _drive(a1, _timesteps(100, 5, 19))
+  # the reference's state shapes (dqn/agent.py:209-217): a uint32 key array,
+  # optax's (ScaleByRStdDevState(mu, nu), EmptyState()) over Haiku trees
+  st = a1.get_state()
+  assert st['rng_key'].dtype == np.uint32 and st['rng_key'].shape == (4,)
+  rms, empty = st['opt_state']
+  assert type(rms).__name__ == 'ScaleByRStdDevState' and empty._fields == ()
+  assert set(rms.mu) == set(st['online_params']) == set(rms.nu)
+  if kind.startswith('mgsc'):
+    adam = st['meta_opt_state'][0]
+    assert type(adam).__name__ == 'ScaleByAdamState' and adam.count > 0
   ck = parts.Checkpoint(str(tmp_path / 'run.chkpt'))
   ck.state.iteration = 3
   ck.state.train_agent = a1
@@ -128,10 +138,10 @@ def test_checkpoint_save_restore_continues_bit_exactly(device, tmp_path, kind):
     assert torch.equal(getattr(a1.learner, which), getattr(a2.learner, which)), which
   if kind.startswith('mgsc'):
     assert torch.equal(r1.logits, r2.logits)
-    m1, m2 = a1.meta_learner.get_state(), a2.meta_learner.get_state()
-    assert m1['count'] == m2['count'] and m1['count'] > 0
-    np.testing.assert_array_equal(m1['mu'], m2['mu'])
-    np.testing.assert_array_equal(m1['nu'], m2['nu'])
+    m1, m2 = a1.meta_learner.get_state()[0], a2.meta_learner.get_state()[0]
+    assert m1.count == m2.count and m1.count > 0
+    np.testing.assert_array_equal(m1.mu, m2.mu)
+    np.testing.assert_array_equal(m1.nu, m2.nu)
   if kind == 'per':
     assert a1.max_seen_priority == a2.max_seen_priority
 
@@ -199,7 +209,7 @@ def test_checkpoint_does_not_perturb_the_saver(device, tmp_path, kind):
     assert torch.equal(d1.logits, d2.logits)
     assert d1.run_state() == d2.run_state()
     assert d1.run_state()['known'] == 1  # nothing forced a re-scan
-    m1, m2 = a1.meta_learner.get_state(), a2.meta_learner.get_state()
-    np.testing.assert_array_equal(m1['mu'], m2['mu'])
+    m1, m2 = a1.meta_learner.get_state()[0], a2.meta_learner.get_state()[0]
+    np.testing.assert_array_equal(m1.mu, m2.mu)
   if kind == 'per':
     assert a1.max_seen_priority == a2.max_seen_priority

@@ -133,10 +133,10 @@ def test_meta_update_matches_oracle(device, meta_batch):
   np.testing.assert_allclose(new[pos], ref['new_logits'], atol=1e-6)
   untouched = np.setdiff1d(np.arange(cap_logits), pos)
   np.testing.assert_array_equal(new[untouched], logits[untouched])
-  state = meta.get_state()
-  assert state['count'] == 3
+  state = meta.get_state()[0]
+  assert state.count == 3
   # measured (round 2): 2.6e-10 against max |m| 2.8e-3
-  np.testing.assert_allclose(state['mu'], ref['adam_m'], atol=1e-5 * np.abs(ref['adam_m']).max())
+  np.testing.assert_allclose(state.mu, ref['adam_m'], atol=1e-5 * np.abs(ref['adam_m']).max())
 
 
 @pytest.mark.parametrize('bound,meta_batch', [(5.0, 8), (1.0 / 32, 8), (5.0, 260)])
