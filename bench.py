@@ -325,6 +325,10 @@ def parse_args(argv=None):
   ap.add_argument('--capacity', type=int, default=1_000_000)
   ap.add_argument('--graph', type=int, default=1, help='hipGraph-replay steps')
   ap.add_argument('--graph-steps', type=int, default=50)
+  ap.add_argument('--lead-eager', type=int, default=0,
+                  help='timed steps launched eagerly ahead of the graph '
+                       'replays (the first kernels start without waiting '
+                       'for a graph submission)')
   ap.add_argument('--target-period', type=int, default=2500)
   ap.add_argument('--stats-every', type=int, default=1000)
   ap.add_argument('--profile-iters', type=int, default=100)
@@ -350,7 +354,10 @@ def main(argv=None):
           file=sys.stderr)
     return 2
   try:
-    g, rem = plan_chunks(args.steps, args.graph_steps, bool(args.graph))
+    if not 0 <= args.lead_eager < args.steps:
+      raise ValueError('--lead-eager must be in [0, --steps)')
+    g, rem = plan_chunks(args.steps - args.lead_eager, args.graph_steps,
+                         bool(args.graph))
   except ValueError as e:
     print('bench.py: %s' % e, file=sys.stderr)
     return 2
@@ -371,11 +378,12 @@ def _barrier(reps):
   reps.barrier()
 
 
-def _timed(reps, runner, steps, g, rem, sync):
+def _timed(reps, runner, steps, g, rem, sync, lead=0):
   _barrier(reps)
   sync()
   t0 = time.perf_counter()
-  n = runner.run(steps, g, rem)
+  n = runner.run(lead, 1, 0) if lead else 0
+  n += runner.run(steps - lead, g, rem)
   sync()
   elapsed = time.perf_counter() - t0
   _barrier(reps)
@@ -418,7 +426,8 @@ def selftest_cpu(args, g, rem):
   # the timed gathers are collectives: every rank runs the same step counts
   runner.run(args.warmup, 1, 0)
   warm = counters['steps']
-  elapsed = _timed(reps, runner, args.steps, g, rem, lambda: None)
+  elapsed = _timed(reps, runner, args.steps, g, rem, lambda: None,
+                   lead=args.lead_eager)
   elapsed_max = reps.max_over_ranks(elapsed)
   per_rank = reps.gather_stats([counters['steps'] - warm, elapsed,
                                 counters['syncs'], counters['gathers']])
@@ -684,7 +693,7 @@ def run_gpu(args, g, rem):
   torch.cuda.synchronize(dev)
   clock['t0'] = time.perf_counter()
   elapsed = _timed(reps, runner, args.steps, g, rem,
-                   lambda: torch.cuda.synchronize(dev))
+                   lambda: torch.cuda.synchronize(dev), lead=args.lead_eager)
   steps = args.steps
   for w in pending:
     w.wait()
@@ -782,6 +791,7 @@ def run_gpu(args, g, rem):
                  'global_batch': BATCH * world, 'replay_capacity': args.capacity,
                  'parallelism': 'independent-seed replicas x%d' % world,
                  'hipgraph_chunks': [g, rem],
+                 'lead_eager_steps': args.lead_eager,
                  'warmup_steps_run': warm_steps},
       'roofline': roof,
       'step_roofline': {

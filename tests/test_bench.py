@@ -107,6 +107,20 @@ def test_gpus1_forms_a_process_group():
   assert out['rccl']['last_in_loop_gather']['steps_done'] == [10]
 
 
+def test_lead_eager_steps_keep_the_timed_count():
+  """--lead-eager L: L eager steps, then graphs over the other K - L."""
+  p = _run_bench(['--gpus', '1', '--steps', '20', '--warmup', '0',
+                  '--graph-steps', '6', '--lead-eager', '3', '--stats-every', '5',
+                  '--selftest-cpu'])
+  assert p.returncode == 0, p.stderr[-2000:]
+  out = json.loads([l for l in p.stdout.splitlines() if l.startswith('{')][0])
+  assert out['steps'] == 20 and out['per_rank_steps'] == [20]
+  assert out['chunks'] == [6, 5]  # 17 = 2 x 6 + 5
+  bad = _run_bench(['--gpus', '1', '--steps', '4', '--lead-eager', '4',
+                    '--selftest-cpu'], timeout=120)
+  assert bad.returncode != 0 and '--lead-eager' in bad.stderr
+
+
 def test_world_mismatch_fails():
   p = _run_bench(['--gpus', '2', '--steps', '4', '--warmup', '0',
                   '--selftest-cpu'], env={'WORLD_SIZE': '1'}, timeout=120)
