@@ -13,16 +13,9 @@ runs one seed per job; here the seeds report through one group).
 """
 
 import os
-import socket
 
 import numpy as np
 import torch
-
-
-def _free_port():
-  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-    s.bind(('127.0.0.1', 0))
-    return s.getsockname()[1]
 
 
 class Replicas:
@@ -39,11 +32,14 @@ class Replicas:
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
     if not dist.is_initialized():
       if self.world == 1 and 'MASTER_ADDR' not in os.environ:
-        # a lone rank still forms a group (loopback rendezvous)
-        os.environ['MASTER_ADDR'] = '127.0.0.1'
-        os.environ['MASTER_PORT'] = str(_free_port())
-      dist.init_process_group(backend or 'nccl', rank=self.rank,
-                              world_size=self.world)
+        # a lone rank still forms a group, over an in-process store: a
+        # loopback TCP rendezvous on a probed free port can lose the port
+        # to another process before it binds (EADDRINUSE, seen on the box)
+        dist.init_process_group(backend or 'nccl', store=dist.HashStore(),
+                                rank=0, world_size=1)
+      else:
+        dist.init_process_group(backend or 'nccl', rank=self.rank,
+                                world_size=self.world)
     self.dist = dist
     self.backend = dist.get_backend()
 
