@@ -99,6 +99,57 @@ def test_learner_step_matches_oracle(device, algo, nonzero):
   _compare_tree(lrn.params_tree('target'), target, 0.0, what='target')
 
 
+def _rel_norm_err(got, want):
+  worst = 0.0
+  for m in want:
+    for n in want[m]:
+      w = np.asarray(want[m][n], np.float64)
+      d = np.linalg.norm(np.asarray(got[m][n], np.float64) - w)
+      worst = max(worst, d / max(np.linalg.norm(w), 1e-30))
+  return worst
+
+
+@pytest.mark.parametrize('algo', ['dqn', 'double'])
+def test_learner_step_on_unfiltered_batches(device, algo):
+  """Plain rng.integers batches (no kink filter, helpers.kink_free_slots):
+  a ReLU pre-activation within f32 rounding of 0 may take the other branch
+  than in fp64, which moves single gradient entries (not the forward), so
+  q / td / loss keep their elementwise bars and the gradient (mu after one
+  step from zero state is (1 - decay) g) and the update are held to a
+  relative Frobenius-norm bar per leaf."""
+  batch = 32
+  for seed in (21, 22, 23, 24):
+    net, lrn, st, host, online, target, mu, nu = _setup(algo, batch, seed=seed)
+    slots = np.random.default_rng(seed).integers(
+        0, st.capacity, size=batch).astype(np.int32)
+    s_tm1 = helpers.stacks_from(host['frames'], host['fidx'], slots, 0)
+    s_t = helpers.stacks_from(host['frames'], host['fidx'], slots, 1)
+    ref = learner_ref.learner_step(
+        online, target, mu, nu, s_tm1, host['action'][slots],
+        host['reward'][slots], host['discount'][slots], s_t, algo=algo)
+    lrn.step(st, torch.from_numpy(slots).to(device))
+    q, td, loss = lrn.fetch_outputs()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(q.cpu().numpy(), ref['q_tm1'], atol=Q_ATOL)
+    np.testing.assert_allclose(td.cpu().numpy(), ref['td'], atol=Q_ATOL)
+    np.testing.assert_allclose(loss.cpu().numpy()[0], ref['loss'], rtol=1e-4,
+                               atol=1e-7)
+    g_err = _rel_norm_err(lrn.params_tree('mu'), ref['mu'])
+    after = lrn.params_tree('online')
+    delta_got = {m: {n: after[m][n] - online[m][n]
+                     for n in online[m]} for m in online}
+    delta_want = {m: {n: ref['params'][m][n] - online[m][n]
+                      for n in online[m]} for m in online}
+    u_err = _rel_norm_err(delta_got, delta_want)
+    print('seed %d margin %.2e: gradient rel err %.2e, update rel err %.2e' % (
+        seed, learner_ref.relu_margin(online, s_tm1), g_err, u_err))
+    # measured (round 3, seeds 21-24, margins 1.3e-7 .. 6.4e-7 — inside the
+    # 1e-6 band the filtered tests exclude): gradient <= 4.3e-7, update
+    # <= 3.6e-5
+    assert g_err <= 1e-5, g_err
+    assert u_err <= 1e-3, u_err
+
+
 def test_forward_q_values_direct_and_slots(device):
   batch = 16
   net, lrn, st, host, online, _, _, _ = _setup('dqn', batch, seed=21)
