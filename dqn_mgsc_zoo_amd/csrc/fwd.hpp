@@ -371,6 +371,71 @@ __device__ __forceinline__ void fc1_fwd_store(const Fc1FwdArgs& a, const float* 
   }
 }
 
+// fc1 forward on v_mfma_f32_32x32x2f32 (DQZ_FC1_32, default on since round
+// 3: fc1 5.8 -> 4.7 us, 15,870-15,960 -> 16,140-16,240 steps/s; 0 keeps the
+// 16x16x4 fc1_fwd_kernel, which the MGSC tangent launch still uses): a block owns
+// 32 columns (one 128-byte line of every W1 row it reads) x the 32 rows of
+// its row group x one K split; wave w owns k in [448 s + 112 w, +112).  Lane
+// l = 32 h + c: B column c, and for MFMA step (g, e), g < 14, e < 4, the k
+// pair {8 g + e, 8 g + 4 + e} (half h takes the second), so the A row loads
+// are float4.  Output rows (r & 3) + 8 (r >> 2) + 4 h of column c.
+#ifndef DQZ_FC1_32
+#define DQZ_FC1_32 1
+#endif
+constexpr bool kFc1M32 = DQZ_FC1_32 != 0;
+constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
+__device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
+  const int nt = i % (HID / 32);
+  const int rest = i / (HID / 32);
+  const int s = rest % FC1_S, zm = rest / FC1_S;
+  const int z = zm / a.MG, mg = zm % a.MG;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
+  const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
+  constexpr int G = FC1_KW / 8;                         // 14
+  float wr[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
+  const int row = min(32 * mg + c, a.B - 1);
+  const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
+  float4 av[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
+  f32x16 acc = {};
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
+  __syncthreads();
+  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
+  const int q = t >> 3, c4 = 4 * (t & 7);
+  if (32 * mg + q < a.B) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = q * 33 + c4 + e;
+      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+    }
+    *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
+        make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
+  DQZ_STAMP(3, 0);
+  __shared__ float s_red[4 * FC1_32RW];
+  fc1_fwd_block32(a, s_red, blockIdx.x);
+  DQZ_STAMP(3, 3);
+}
+
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_RW];

@@ -262,8 +262,12 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   f1.part = L->fc1p;
   f1.sum = kFc1Reduce ? L->fc1sum : nullptr;
   f1.cnt = L->fc1cnt;
-  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
-            DQZ_HIP(hipGetLastError()));
+  if (kFc1M32)
+    DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3((HID / 32) * FC1_S * Z * f1.MG), dim3(256), 0, st, f1);
+              DQZ_HIP(hipGetLastError()));
+  else
+    DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
+              DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
 
