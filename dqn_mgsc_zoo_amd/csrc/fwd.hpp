@@ -506,7 +506,9 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
 // ranges [conv1 4/sample] [conv2 4/sample] [conv3 4/sample] [fc1 tiles]
 // instead of four dependent launches.  Dynamic LDS = conv1's 57.6 KB.
 static_assert(4 * FC1_RW * sizeof(float) <= kConv1FwdSmem, "fc1's partial tiles fit the tangent launch's LDS");
-inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + (HID / 16) * FC1_S * MG; }
+inline int tangent_fwd_blocks(int B, int MG) {
+  return 3 * 4 * ((B + 7) / 8 * 8) + (HID / (kFc1M32 ? 32 : 16)) * FC1_S * MG;
+}
 __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
                                                           Fc1FwdArgs f1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -530,9 +532,14 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
     return;
   }
   i -= n;
-  int z, s, nt, mg;
-  fc1_fwd_tile(f1, smem, i, z, s, nt, mg);
-  fc1_fwd_store(f1, smem, z, s, nt, mg);
+  if constexpr (kFc1M32) {
+    static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
+    fc1_fwd_block32(f1, smem, i);
+  } else {
+    int z, s, nt, mg;
+    fc1_fwd_tile(f1, smem, i, z, s, nt, mg);
+    fc1_fwd_store(f1, smem, z, s, nt, mg);
+  }
 }
 
 }  // namespace dqz
