@@ -17,8 +17,11 @@ world size, so the 1-GPU line goes through the same RCCL calls.
 `--algo` picks the BASELINE config the step follows: dqn (config 2, the
 default and the headline line), double (double-Q on the same uniform
 replay), per (config 4: device PER sample over a 2^20-leaf fp64 sum tree +
-double-Q step with IS weights + |td|^alpha write-back) or mgsc (config 3's
-learner part: softmax-CDF sample over 1M learned f32 logits + DQN step).
+double-Q step with IS weights + |td|^alpha write-back), mgsc (config 3's
+learner part: softmax-CDF sample over 1M learned f32 logits + DQN step) or
+agent (config 1: the whole dqn agent, parts.run_loop over raw 210x160 RGB
+frames through processors.atari, a 1M TransitionReplay, learning every 16
+frames once 5 % of it is full; K learner steps are timed, 16 K frames).
 
 Prints ONE JSON line on rank 0.
 """
@@ -26,9 +29,10 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
-import socket
+import shutil
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -132,7 +136,7 @@ def phase_bytes(algo, batch):
 # libdqz phase -> kernel symbol (rocprofv3 names, template args stripped).
 PHASE_KERNEL = {
     'conv1_fwd': 'conv1_fwd_kernel', 'conv2_fwd': 'conv2_fwd_kernel',
-    'conv3_fwd': 'conv3_fwd_kernel', 'conv_fwd': 'fwd_conv_kernel', 'fc1_fwd': 'fc1_fwd_kernel',
+    'conv3_fwd': 'conv3_fwd_kernel', 'conv_fwd': 'fwd_conv_kernel', 'fc1_fwd': 'fc1_fwd32_kernel',
     'head': 'head_kernel',
     'fc1_dx': 'fc1_dx_kernel', ALL_BWD: 'bwd_bc_kernel',
     'update': 'update_kernel'}
@@ -270,24 +274,31 @@ class StepRunner:
     return i
 
 
-def free_port():
-  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-    s.bind(('127.0.0.1', 0))
-    return s.getsockname()[1]
-
-
-def spawn_ranks(n, argv):
-  """Starts n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE set,
-  rendezvous on 127.0.0.1) and returns the worst exit code.  Called before
+def spawn_ranks(n, argv, script=None):
+  """Starts n rank processes of `script` (default: this one) with
+  RANK/LOCAL_RANK/WORLD_SIZE set and returns the worst exit code.  The ranks
+  rendezvous in a torch.distributed.FileStore whose path this parent names
+  (replicas.STORE_FILE_ENV): no loopback port is probed here and bound later
+  by a child, so nothing else can take it in between.  Called before
   anything touches the GPU; children are started, never exec'd into."""
-  port = free_port()
+  from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
+  tmp = tempfile.mkdtemp(prefix='dqz_ranks_')
+  try:
+    return _run_ranks(n, argv, os.path.join(tmp, 'store'),
+                      script or os.path.abspath(__file__),
+                      replicas_lib.STORE_FILE_ENV)
+  finally:
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _run_ranks(n, argv, store_file, script, store_env):
   procs = []
   for r in range(n):
     env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-               LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1',
-               MASTER_PORT=str(port))
-    procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] +
-                                  list(argv), env=env))
+               LOCAL_WORLD_SIZE=str(n), **{store_env: store_file})
+    env.pop('MASTER_ADDR', None)
+    env.pop('MASTER_PORT', None)
+    procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
   rcs = [None] * n
   while any(rc is None for rc in rcs):
     for i, p in enumerate(procs):
@@ -321,7 +332,10 @@ def parse_args(argv=None):
   ap.add_argument('--steps', type=int, default=5000)
   ap.add_argument('--warmup', type=int, default=200)
   ap.add_argument('--algo', default='dqn',
-                  choices=['dqn', 'double', 'per', 'mgsc'])
+                  choices=['dqn', 'double', 'per', 'mgsc', 'agent'])
+  ap.add_argument('--min-replay-fraction', type=float, default=0.05,
+                  help='--algo agent: min_replay_capacity_fraction '
+                       '(dqn/run_atari.py default 0.05)')
   ap.add_argument('--capacity', type=int, default=1_000_000)
   ap.add_argument('--graph', type=int, default=1, help='hipGraph-replay steps')
   ap.add_argument('--graph-steps', type=int, default=50)
@@ -363,6 +377,8 @@ def main(argv=None):
     return 2
   if args.selftest_cpu:
     return selftest_cpu(args, g, rem)
+  if args.algo == 'agent':
+    return run_agent(args)
   return run_gpu(args, g, rem)
 
 
@@ -832,6 +848,144 @@ def run_gpu(args, g, rem):
     print('bench.py: hand-off status %d, non-finite loss %s, params finite %s: '
           'the timed steps are invalid' % (out['handoff_status'], out['nonfinite_loss'],
                                            finite), file=sys.stderr)
+    return 3
+  return 0
+
+
+# The reference's own training frame rate of this agent: median
+# train_frame_rate of results/dqn/seed_0.csv (iterations 1-50, 1,103-1,168;
+# Pong, its cluster's GPU + JAX, the ALE emulator inside the loop).
+REFERENCE_TRAIN_FRAMES_PER_S = 1136.0
+
+
+def run_agent(args):
+  """BASELINE config 1: the dqn agent (dqn/run_atari.py:204-294) on device.
+
+  parts.run_loop drives agent.Dqn over raw Atari-shaped RGB frames
+  (synthetic.SyntheticAtari: no ALE here) through processors.atari (the
+  observation math on device), a TransitionReplay(capacity) with the
+  RandomState, batch 32, learn period 16, target period 40,000 frames,
+  centered RMSProp.  Frames are stepped until learning has begun and
+  `--warmup` learner steps ran; then exactly `--steps` learner steps (16
+  frames each) are timed, act + preprocess + add + learn included."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import parts  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import processors  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import replay as replay_lib  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import replicas as replicas_lib  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd import synthetic  # pylint: disable=g-import-not-at-top
+  from dqn_mgsc_zoo_amd.dqn import agent as agent_lib  # pylint: disable=g-import-not-at-top
+  json_out = _json_stdout()
+  local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+  torch.cuda.set_device(local_rank)
+  rank = int(os.environ.get('RANK', '0'))
+  dev = torch.device('cuda', local_rank)
+  learn_period = 16
+  random_state = np.random.RandomState(1 + rank)
+  replay = replay_lib.TransitionReplay(
+      args.capacity, replay_lib.Transition(None, None, None, None, None),
+      random_state)
+  agent = agent_lib.Dqn(
+      preprocessor=processors.atari(),
+      sample_network_input=np.zeros((84, 84, 4), np.uint8),
+      network=networks.dqn_atari_network(NUM_ACTIONS),
+      optimizer=learner_lib.rmsprop(2.5e-4, 0.95, 0.01 / 32**2, centered=True),
+      transition_accumulator=replay_lib.TransitionAccumulator(),
+      replay=replay, batch_size=BATCH,
+      # dqn/run_atari.py: epsilon 1 -> 0.1 over 0.02 x 200 iterations x 1M frames
+      exploration_epsilon=parts.LinearSchedule(
+          begin_t=int(args.min_replay_fraction * args.capacity * 4),
+          decay_steps=4_000_000, begin_value=1.0, end_value=0.1),
+      min_replay_capacity_fraction=args.min_replay_fraction,
+      learn_period=learn_period, target_network_update_period=40_000,
+      grad_error_bound=1.0 / 32, rng_key=np.array([0, 1 + rank], np.uint32),
+      device=dev)
+  counts = {'learn': 0}
+  orig_learn = agent._learn  # pylint: disable=protected-access
+
+  def learn():
+    counts['learn'] += 1
+    orig_learn()
+
+  agent._learn = learn  # pylint: disable=protected-access
+  env = synthetic.SyntheticAtari(episode_len=27_000, seed=1 + rank,
+                                 num_actions=NUM_ACTIONS)
+  loop = parts.run_loop(agent, env, max_steps_per_episode=108_000)
+  t_fill = time.perf_counter()
+  fill_frames = 0
+  while counts['learn'] < max(1, args.warmup):
+    next(loop)
+    fill_frames += 1
+  torch.cuda.synchronize(dev)
+  fill_s = time.perf_counter() - t_fill
+  reps = replicas_lib.Replicas('nccl')
+  _barrier(reps)
+  torch.cuda.synchronize(dev)
+  start = counts['learn']
+  frames = 0
+  t0 = time.perf_counter()
+  while counts['learn'] - start < args.steps:
+    next(loop)
+    frames += 1
+  torch.cuda.synchronize(dev)
+  elapsed = time.perf_counter() - t0
+  _barrier(reps)
+  status = agent.check_learner_health()
+  ok, msg = replay.check_valid()
+  elapsed_max = reps.max_over_ranks(elapsed, device=dev)
+  per_rank = reps.gather_stats([args.steps / elapsed, frames / elapsed,
+                                float(frames)], device=dev)
+  finite = bool(torch.isfinite(agent.learner.online).all().item())
+  if rank != 0:
+    reps.close()
+    return 0 if (status == 0 and ok and finite) else 3
+  world = reps.world
+  out = {
+      'metric': METRIC,
+      'value': round(world * args.steps / elapsed_max, 2),
+      'unit': 'steps/s',
+      'n_gpus': world,
+      'steps': args.steps,
+      'warmup': args.warmup,
+      'ms_per_step': round(1e3 * elapsed_max / args.steps, 5),
+      'higher_is_better': True,
+      'scaling': 'weak',
+      'vs_baseline': None,
+      'dtype': 'f32',
+      'data': 'synthetic (Atari-shaped 210x160x3 uint8 RGB frames from a seeded '
+              'pool, lives, rewards; random-init NatureQNetwork)',
+      'config': {'workload': 'BASELINE config 1: dqn agent, parts.run_loop over '
+                             'raw frames through processors.atari (device '
+                             'observation math), TransitionReplay(capacity=%d, '
+                             'RandomState), batch=32, learn_period=16, '
+                             'min_replay_capacity_fraction=%g, A=%d' % (
+                                 args.capacity, args.min_replay_fraction,
+                                 NUM_ACTIONS),
+                 'global_batch': BATCH * world, 'replay_capacity': args.capacity,
+                 'parallelism': 'independent-seed replicas x%d' % world},
+      'frames': frames,
+      'frames_per_s': round(world * frames / elapsed_max, 1),
+      'learner_steps_per_s': round(world * args.steps / elapsed_max, 2),
+      'per_rank_frames_per_s': [round(float(x), 1) for x in per_rank[:, 1]],
+      'reference_train_frames_per_s': REFERENCE_TRAIN_FRAMES_PER_S,
+      'reference_note': 'median train_frame_rate of results/dqn/seed_0.csv '
+                        '(Pong, ALE emulator inside the loop); this loop steps '
+                        'a synthetic environment',
+      'replay_size': replay.size,
+      'replay_valid': bool(ok),
+      'fill_frames': fill_frames,
+      'fill_s': round(fill_s, 2),
+      'handoff_status': int(status) & 1,
+      'params_finite': finite,
+      'roofline': None,
+      'cpu_baseline': None,
+  }
+  print(json.dumps(out), file=json_out, flush=True)
+  reps.close()
+  if status & 1 or not ok or not finite:
+    print('bench.py: agent run invalid (status %d, replay %s, finite %s)' % (
+        status, msg, finite), file=sys.stderr)
     return 3
   return 0
 

@@ -68,6 +68,7 @@ class DeviceDqnAgent(parts.Agent):
     self._frame_t = -1
     self._statistics = {'state_value': np.nan}
     self._learn_steps = 0
+    self._last_health_check = 0  # learn steps done at the previous check
     self._nonfinite_loss_checks = 0
 
   # -- reference surface ----------------------------------------------------
@@ -107,23 +108,27 @@ class DeviceDqnAgent(parts.Agent):
     """Reads the learner's health word (dqz_learner_sync_status).
 
     A hand-off wait that gave up (bit 0) makes every step since the previous
-    check invalid: raises RuntimeError (reading the word has already reset
-    the hand-off words, so the learner itself can continue).  A non-finite
+    check invalid: the online parameters and RMSProp moments may have been
+    updated from partial payloads, so the learner state must be restored
+    from a checkpoint (parts.Checkpoint); raises RuntimeError naming the
+    learn steps since the previous check (reading the word has already reset
+    the hand-off words, so a restored learner can continue).  A non-finite
     batch loss (bit 1) is counted and warned about; the update ran, as the
     reference's jitted update would.  Called every HEALTH_CHECK_PERIOD learn
     steps, at every target sync and from get_state.
     """
     status = self._learner.sync_status()
+    first, last = self._last_health_check, self._learn_steps
+    self._last_health_check = self._learn_steps
     if status & 2:
       self._nonfinite_loss_checks += 1
       warnings.warn('learner: a batch loss since the last check was NaN or '
                     'infinite (frame %d)' % self._frame_t, RuntimeWarning)
     if status & 1:
       raise RuntimeError(
-          'learner hand-off wait timed out between learn steps %d and %d '
-          '(frame %d): those updates are invalid' % (
-              max(0, self._learn_steps - self.HEALTH_CHECK_PERIOD),
-              self._learn_steps, self._frame_t))
+          'learner hand-off wait timed out in learn steps %d..%d (frame %d): '
+          'those updates are invalid; restore the agent from a checkpoint' % (
+              first + 1, last, self._frame_t))
     return status
 
   def reset(self) -> None:

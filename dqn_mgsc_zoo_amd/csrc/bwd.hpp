@@ -57,10 +57,7 @@ constexpr int W3P_N = 4 * 9 * 1024, W2P_N = 8 * 4 * 1024;  // 36864, 32768
 // group only with a stride of 8 (mod 64) dwords: 520 (528 put two lanes on
 // each bank quad: 4 extra LDS cycles per read, the 1.67 conflict cycles per
 // LDS instruction of round 2's counters).
-#ifndef DQZ_FC1DX_LD
-#define DQZ_FC1DX_LD 520
-#endif
-constexpr int FC1X_LD = DQZ_FC1DX_LD;
+constexpr int FC1X_LD = 520;
 
 // dy3 = (dz1 @ W1^T) relu'(y3), the head of the backward chain (conv3
 // backward waits on it).  Block blk owns W1 rows [16 blk, 16 blk + 16) for
@@ -157,7 +154,6 @@ struct Conv3BwdArgs {
   float* part;       // [B][577][64]
   int B;
   Handoff sync;      // per-sample dy2 arrival counters (bwd_bc_kernel)
-  int* dwcnt;        // XCD-group dW reduce counters [8][4] (x Handoff::kStride), or null
 };
 
 // PUB: dy2 is handed to conv2 dX inside the same launch (bwd_bc_kernel): every
@@ -256,116 +252,27 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
   if constexpr (PUB) a.sync.arrive(b);
 }
 
-// XCD-group pre-reduction of per-sample dW partials.  A dW job of sample b
-// runs on XCD b % 8 (xcd_sample_job), so the jobs (b, job) of the samples
-// g, g + 8, ... (g = b % 8) share one L2.  After its own piece is stored
-// (plain stores: the lines stay in that L2) and drained, each job adds to
-// the (g, job) counter; the last of the group's n_g jobs to arrive reads the
-// n_g pieces back with sc1 loads (L1 bypassed, served by the shared L2; the
-// guide's last-arriver hand-off row) and writes their sum, in sample order,
-// over sample g's piece.  update_kernel then reduces min(8, B) slabs instead
-// of B: 8.9 MB -> 2.2 MB of partial reads at B = 32 for conv2 + conv3.
-// NV float4s per lane at byte offsets off[v] of the slab, plus (if nb > 0)
-// nb scalar bias values at float offsets boff[k] of the slab.
-template <int NV, int NB>
-__device__ __forceinline__ void dw_xcd_reduce(float* part, int64_t slab_floats, int b, int B, int* cnt,
-                                              const int (&off)[NV], int nb, const int (&boff)[NB]) {
-  __shared__ int s_last;
-  const int g = b & 7, ng = (B - g + 7) / 8;
-  if (ng <= 1) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-  __syncthreads();
-  if (!s_last) return;
-  const int bytes = (int)min((int64_t)INT32_MAX, (int64_t)B * slab_floats * 4);
-  const float4* base = reinterpret_cast<const float4*>(part);
-  f32x4 acc[NV];
-  float bacc[NB > 0 ? NB : 1];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < NB; ++k) bacc[k] = 0.f;
-  for (int j = 0; j < ng; ++j) {  // sample order g, g + 8, ...
-    const int64_t sb = (int64_t)(g + 8 * j) * slab_floats;
-    float4 x[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) x[v] = load_sc1_f4(base, bytes, (int)((sb * 4 + off[v]) / 16));
-    float y[NB > 0 ? NB : 1];
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-      if (k < nb) y[k] = load_sc1_f1(part, bytes, (int)(sb + boff[k]));
-    if (j == 0) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] = f32x4{x[v].x, x[v].y, x[v].z, x[v].w};
-#pragma unroll
-      for (int k = 0; k < NB; ++k) bacc[k] = k < nb ? y[k] : 0.f;
-    } else {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] += f32x4{x[v].x, x[v].y, x[v].z, x[v].w};
-#pragma unroll
-      for (int k = 0; k < NB; ++k)
-        if (k < nb) bacc[k] += y[k];
-    }
-  }
-  float* dst = part + (int64_t)g * slab_floats;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(dst) + off[v]) = acc[v];
-#pragma unroll
-  for (int k = 0; k < NB; ++k)
-    if (k < nb) dst[boff[k]] = bacc[k];
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Samples per conv3 / conv2 dW job.  A job accumulates the dW of its G
-// samples in its MFMA registers (sample order) and stores one partial slab,
-// so update_kernel reads ceil(B / G) slabs instead of B.  Measured (round 3,
-// tools/abv.sh, 2 x 20,000 steps each): G3 = 1 15,370-15,530 steps/s; G3 = 4
-// 14,050-14,090 (backward 20.5 -> 27.5 us: four samples in series make the
-// conv3 dW jobs the launch's tail) for update 4.1 -> 3.9 us; G3 = 4, G2 = 2
-// 13,530-13,580; G3 = 8 11,740-11,790.  Default: one sample per job.
-#ifndef DQZ_C3DW_G
-#define DQZ_C3DW_G 1
-#endif
-#ifndef DQZ_C2DW_G
-#define DQZ_C2DW_G 1
-#endif
-constexpr int C3DW_G = DQZ_C3DW_G;
-constexpr int C2DW_G = DQZ_C2DW_G;
-static_assert(C3DW_G >= 1 && C2DW_G >= 1, "dW group sizes");
-
-// conv3 dW job (group g of C3DW_G samples, output-channel quarter nq): the
-// next sample's y2 window is loaded while this sample's MFMAs run, its dy3
-// operands right after them (the registers fit the 128-VGPR budget of
-// bwd_bc_kernel's occupancy).
-__device__ __forceinline__ void conv3_dw_load_dy(const Conv3BwdArgs& a, int b, int nq, float (&dr)[13]) {
-  const int lane = threadIdx.x & 63, n = lane & 15, kq = lane >> 4;
+// conv3 dW job (sample b, output-channel quarter nq).  (Round 3 measured
+// jobs that accumulate several samples, and a per-XCD pre-reduction of the
+// per-sample slabs inside the launch: both slower, commit 1a3be58.)
+__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  constexpr int NQ4 = C2M * C2CO / 4;  // 1296
   // B operand: dy3[b][p = 4 kk + kq][16 nq + n], zero for p >= 49
+  float dr[13];
 #pragma unroll
   for (int kk = 0; kk < 13; ++kk) {
     const int p = 4 * kk + kq;
     const float v = a.dy3[((int64_t)b * C3M + min(p, C3M - 1)) * C3CO + 16 * nq + n];
     dr[kk] = p < C3M ? v : 0.f;
   }
-}
-
-__device__ __forceinline__ void conv3_dw_load_y2(const Conv3BwdArgs& a, int b, float4 (&r)[6]) {
-  const float4* src = reinterpret_cast<const float4*>(a.y2 + (int64_t)b * (C2M * C2CO));
-  constexpr int NQ4 = C2M * C2CO / 4;  // 1296
-#pragma unroll
-  for (int q = 0; q < 6; ++q) r[q] = src[min((int)threadIdx.x + 256 * q, NQ4 - 1)];
-}
-
-__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int g, int nq) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int n = lane & 15, kq = lane >> 4;
-  const int b0 = g * C3DW_G, b1 = min(a.B, b0 + C3DW_G);
-  constexpr int NQ4 = C2M * C2CO / 4;  // 1296
-  float dr[13];
   float4 r[6];
-  conv3_dw_load_dy(a, b0, nq, dr);
-  conv3_dw_load_y2(a, b0, r);
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.y2 + (int64_t)b * (C2M * C2CO));
+#pragma unroll
+    for (int q = 0; q < 6; ++q) r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  }
   // A operand: y2 window at (oh + kh, ow + kw), ci = 16 w + n; position p = 4 kk + kq
   int pb[13];
 #pragma unroll
@@ -376,53 +283,39 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
   f32x4 acc[9];
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp) acc[tp] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sb = 0.f;  // bias: sum over the group's positions (lanes kq hold p = 4 kk + kq)
-  for (int b = b0; b < b1; ++b) {
-    if (b > b0) __syncthreads();  // the previous sample's window readers are done
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int i = t + 256 * q;
-      if (i < NQ4) {
-        const int pix = i >> 4;
-        *reinterpret_cast<float4*>(s_win + (pix / C2O) * C3W_RS + (pix % C2O) * C3W_S + (i & 15) * 4) = r[q];
-      }
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NQ4) {
+      const int pix = i >> 4;
+      *reinterpret_cast<float4*>(s_win + (pix / C2O) * C3W_RS + (pix % C2O) * C3W_S + (i & 15) * 4) = r[q];
     }
-    if (b + 1 < b1) conv3_dw_load_y2(a, b + 1, r);  // lands under this sample's MFMAs
-    __syncthreads();
-    if (b == b0) DQZ_STAMP(12, 1);
-    // A = dy3 (rows: co), B = the y2 patch (columns: ci): a lane's four
-    // accumulators are four consecutive co of one (tap, ci) row, stored as one
-    // float4 (the products and their k order are those of the transposed form,
-    // so the values are the same bits)
-#pragma unroll
-    for (int kk = 0; kk < 13; ++kk)
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) {
-        const int off = (tp / 3) * C3W_RS + (tp % 3) * C3W_S;
-        acc[tp] = mfma4(dr[kk], s_win[pb[kk] + off], acc[tp]);
-      }
-#pragma unroll
-    for (int kk = 0; kk < 13; ++kk) sb += dr[kk];
-    if (b + 1 < b1) conv3_dw_load_dy(a, b + 1, nq, dr);
   }
+  __syncthreads();
+  DQZ_STAMP(12, 1);
+  // A = dy3 (rows: co), B = the y2 patch (columns: ci): a lane's four
+  // accumulators are four consecutive co of one (tap, ci) row, stored as one
+  // float4 (the products and their k order are those of the transposed form,
+  // so the values are the same bits)
+#pragma unroll
+  for (int kk = 0; kk < 13; ++kk)
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int off = (tp / 3) * C3W_RS + (tp % 3) * C3W_S;
+      acc[tp] = mfma4(dr[kk], s_win[pb[kk] + off], acc[tp]);
+    }
+  float sb = 0.f;  // bias: sum over positions (lanes kq hold p = 4 kk + kq)
+#pragma unroll
+  for (int kk = 0; kk < 13; ++kk) sb += dr[kk];
   // C layout: row = 4 kq + r -> co = 16 nq + 4 kq + r; col = n -> ci = 16 w + n of tap tp
-  float* slab = a.part + (int64_t)g * (C3KK + 1) * C3CO;
+  float* slab = a.part + (int64_t)b * (C3KK + 1) * C3CO;
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp)
     *reinterpret_cast<f32x4*>(slab + (tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) = acc[tp];
-  float* part = slab + 16 * nq + n;
   if (w == 0) {  // bias row
     sb += __shfl_xor(sb, 16, 64);
     sb += __shfl_xor(sb, 32, 64);
-    if (kq == 0) part[C3KK * C3CO] = sb;
-  }
-  if (kDwXcd && C3DW_G == 1 && a.dwcnt) {
-    int off[9];
-#pragma unroll
-    for (int tp = 0; tp < 9; ++tp) off[tp] = ((tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) * 4;
-    const int boff[1] = {C3KK * C3CO + 16 * nq + n};
-    dw_xcd_reduce<9, 1>(a.part, (int64_t)(C3KK + 1) * C3CO, g, a.B,
-                        a.dwcnt + ((g & 7) * 4 + nq) * Handoff::kStride, off, (w == 0 && kq == 0) ? 1 : 0, boff);
+    if (kq == 0) slab[C3KK * C3CO + 16 * nq + n] = sb;
   }
 }
 
@@ -447,7 +340,6 @@ struct Conv2BwdArgs {
   int B;
   Handoff sync;      // dy2 arrival counters (WAIT)
   Handoff sync1;     // dy1 arrival counters (PUB)
-  int* dwcnt;        // XCD-group dW reduce counters [8][8] (x Handoff::kStride), or null
 };
 
 // WAIT: dy2 of sample b is produced by the 8 conv3 dX jobs of the same launch
@@ -589,29 +481,23 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
 // dy2 comes from this launch's conv3 dX jobs (wait + sc1 loads).
 constexpr int C2V_WIN = 9 * C2W_RS;  // 7272 floats
 
-// conv2 dW job (group g of C2DW_G samples, kernel row kh, output-channel
-// half ch): per sample, y1 rows to LDS (loaded before the wait), the wait
-// for its dy2, then the MFMAs into the group's accumulators.
-__device__ __forceinline__ void conv2_dw_y1(const Conv2BwdArgs& a, int b, int kh, float4 (&r)[6]) {
-  const int t = threadIdx.x;
-  // y1 rows 2 oh + kh, oh = 0..8 (not handed off: plain loads)
-  const float4* src = reinterpret_cast<const float4*>(a.y1 + (int64_t)b * (C1M * C1CO));
-  constexpr int NV4 = 9 * C1O * C1CO / 4;  // 1440
-#pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    const int i = min(t + 256 * q, NV4 - 1);
-    const int oh = i / (C1O * 8), rem = i % (C1O * 8);  // 8 float4 per pixel
-    r[q] = src[((2 * oh + kh) * C1O) * 8 + rem];
-  }
-}
-
-__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int g, int kh, int ch) {
+// conv2 dW job (sample b, kernel row kh, output-channel half ch): y1 rows to
+// LDS (loaded before the wait), the wait for the sample's dy2, the MFMAs.
+__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kw
   const int n = lane & 15, kq = lane >> 4;
-  const int b0 = g * C2DW_G, b1 = min(a.B, b0 + C2DW_G);
   constexpr int NV4 = 9 * C1O * C1CO / 4;  // 1440
   float4 r[6];
-  conv2_dw_y1(a, b0, kh, r);
+  {
+    // y1 rows 2 oh + kh, oh = 0..8 (not handed off: plain loads)
+    const float4* src = reinterpret_cast<const float4*>(a.y1 + (int64_t)b * (C1M * C1CO));
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int i = min(t + 256 * q, NV4 - 1);
+      const int oh = i / (C1O * 8), rem = i % (C1O * 8);  // 8 float4 per pixel
+      r[q] = src[((2 * oh + kh) * C1O) * 8 + rem];
+    }
+  }
   int pb[21];
 #pragma unroll
   for (int kk = 0; kk < 21; ++kk) {
@@ -623,78 +509,61 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sb[2] = {0.f, 0.f};
-  for (int b = b0; b < b1; ++b) {
-    if (b > b0) __syncthreads();  // the previous sample's window readers are done
-    // the y1 rows go to LDS before the wait: held in registers across the spin
-    // loop they were kept in scratch (112 bytes per lane, stored and reloaded)
+  // the y1 rows go to LDS before the wait: held in registers across the spin
+  // loop they were kept in scratch (112 bytes per lane, stored and reloaded)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int i = t + 256 * q;
-      if (i < NV4) {
-        const int oh = i / (C1O * 8), rem = i % (C1O * 8), iw = rem >> 3;
-        *reinterpret_cast<float4*>(s_win + oh * C2W_RS + iw * C2W_S + (rem & 7) * 4) = r[q];
-      }
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NV4) {
+      const int oh = i / (C1O * 8), rem = i % (C1O * 8), iw = rem >> 3;
+      *reinterpret_cast<float4*>(s_win + oh * C2W_RS + iw * C2W_S + (rem & 7) * 4) = r[q];
     }
-    a.sync.wait(b);
-    float dr[21][2];
-#pragma unroll
-    for (int kk = 0; kk < 21; ++kk) {
-      const int p = 4 * kk + kq;
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        const float* gp = a.dy2 + ((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 32 * ch + 16 * ct + n;
-        const float v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dr[kk][ct] = p < C2M ? v : 0.f;
-      }
-    }
-    if (b + 1 < b1) conv2_dw_y1(a, b + 1, kh, r);  // lands under this sample's MFMAs
-    __syncthreads();
-    if (b == b0) DQZ_STAMP(13, 1);
-    // A = dy2 (rows: co), B = y1 (columns: ci): a lane's accumulators are four
-    // consecutive co, stored as one float4 (same bits as the transposed form)
-#pragma unroll
-    for (int kk = 0; kk < 21; ++kk)
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const float av = s_win[pb[kk] + 16 * mt];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = mfma4(dr[kk][ct], av, acc[mt][ct]);
-      }
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int kk = 0; kk < 21; ++kk) sb[ct] += dr[kk][ct];
   }
+  a.sync.wait(b);
+  float dr[21][2];
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk) {
+    const int p = 4 * kk + kq;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const float* gp = a.dy2 + ((int64_t)b * C2M + min(p, C2M - 1)) * C2CO + 32 * ch + 16 * ct + n;
+      const float v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dr[kk][ct] = p < C2M ? v : 0.f;
+    }
+  }
+  __syncthreads();
+  DQZ_STAMP(13, 1);
+  // A = dy2 (rows: co), B = y1 (columns: ci): a lane's accumulators are four
+  // consecutive co, stored as one float4 (same bits as the transposed form)
+#pragma unroll
+  for (int kk = 0; kk < 21; ++kk)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const float av = s_win[pb[kk] + 16 * mt];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) acc[mt][ct] = mfma4(dr[kk][ct], av, acc[mt][ct]);
+    }
+  float sb[2] = {0.f, 0.f};
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int kk = 0; kk < 21; ++kk) sb[ct] += dr[kk][ct];
   // C: row 4 kq + r -> co = 32 ch + 16 ct + 4 kq + r; col n -> ci = 16 mt + n
-  float* slab = a.part + (int64_t)g * (C2KK + 1) * C2CO;
+  float* slab = a.part + (int64_t)b * (C2KK + 1) * C2CO;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
       *reinterpret_cast<f32x4*>(slab + ((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq) =
           acc[mt][ct];
-  float* part = slab + 32 * ch + n;
-  if (kh == 0 && w == 0) {  // bias row (per lane over the group's kk, then over kq)
+  if (kh == 0 && w == 0) {  // bias row (per lane over its kk, then over kq)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       float v = sb[ct];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (kq == 0) part[C2KK * C2CO + 16 * ct] = v;
+      if (kq == 0) slab[C2KK * C2CO + 32 * ch + 16 * ct + n] = v;
     }
-  }
-  if (kDwXcd && C2DW_G == 1 && a.dwcnt) {
-    int off[4];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-        off[2 * mt + ct] = (((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq) * 4;
-    const int boff[2] = {C2KK * C2CO + 32 * ch + n, C2KK * C2CO + 32 * ch + 16 + n};
-    dw_xcd_reduce<4, 2>(a.part, (int64_t)(C2KK + 1) * C2CO, g, a.B,
-                        a.dwcnt + ((g & 7) * 8 + 2 * kh + ch) * Handoff::kStride, off,
-                        (kh == 0 && w == 0 && kq == 0) ? 2 : 0, boff);
   }
 }
 
@@ -834,7 +703,7 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // bwd_bc_kernel: the whole backward after fc1 dX in one launch.  Grid, in
 // dispatch order:
 //   [conv3 dX 8/sample] [fc1 dW 784] [conv2 dX 8/sample]
-//   [conv3 dW 4/group of C3DW_G] [conv1 dW 8/sample] [conv2 dW 8/group of C2DW_G]
+//   [conv3 dW 4/sample] [conv1 dW 8/sample] [conv2 dW 8/sample]
 // Hand-offs inside the launch (common.hpp Handoff): dy2 from
 // the 8 conv3 dX jobs of a sample to its 8 conv2 dX and 8 conv2 dW jobs, dy1
 // from the 8 conv2 dX jobs to its 8 conv1 dW jobs.  Every consumer has a
@@ -891,16 +760,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  const int NG3 = (c3.B + C3DW_G - 1) / C3DW_G, G3 = (NG3 + 7) / 8 * 8;
-  if (i < 4 * G3) {
-    const SampleJob sj = xcd_sample_job_at(i, 4, NG3);  // s = sample group
+  if (i < 4 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
     if (!sj.valid) return;
     DQZ_STAMP(12, 0);
     conv3_bwd_dw(c3, smem, sj.s, sj.job);
     DQZ_STAMP(12, 3);
     return;
   }
-  i -= 4 * G3;
+  i -= 4 * B8;
   // conv1 dW (the launch's tail: it waits for dy1) is dispatched ahead of
   // conv2 dW (whose dy2 is ready early): 14,003-14,012 -> 14,178-14,198
   // steps/s; ahead of conv3 dW as well measured the same
@@ -911,7 +779,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  const SampleJob sj = xcd_sample_job_at(i, 8, (c2.B + C2DW_G - 1) / C2DW_G);  // s = sample group
+  const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
   if (!sj.valid) return;
   DQZ_STAMP(13, 0);
   conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);

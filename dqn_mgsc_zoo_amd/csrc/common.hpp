@@ -12,23 +12,6 @@
 
 namespace dqz {
 
-// Opt-in kernel variants, compiled in only when their -D flag is set (the
-// default kernels carry none of their code):
-// fc1 split-K partials summed inside fc1_fwd_kernel by each tile's last split
-// block (the head then loads one pre-activation row per sample) instead of by
-// the head (DQZ_FC1_REDUCE=0).
-#ifndef DQZ_FC1_REDUCE
-#define DQZ_FC1_REDUCE 0
-#endif
-constexpr bool kFc1Reduce = DQZ_FC1_REDUCE != 0;
-
-// conv2 / conv3 dW partials pre-reduced per XCD group inside the backward
-// launch (bwd.hpp dw_xcd_reduce), so update_kernel reads min(8, B) slabs.
-#ifndef DQZ_DW_XCD
-#define DQZ_DW_XCD 0
-#endif
-constexpr bool kDwXcd = DQZ_DW_XCD != 0;
-
 // MFMA operand / accumulator vectors (v_mfma_f32_16x16x4f32 / 32x32x2f32).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

@@ -284,10 +284,17 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
 }
 
 // ---- fc1: [B][3136] x [3136][512] split-K partials ------------------------
-// grid (32 column tiles of 16, FC1_S K-splits of 448, Z * ceil(B/32)); wave w
-// owns k in [448 s + 112 w, +112).  K is permuted inside each 16-block so a
-// lane's four k for steps e = 0..3 are contiguous: one float4 A load per
-// (row tile, 16-block).  Partials [Z][FC1_S][B][512] are reduced by the head.
+// One block per (32-column tile nt, K split s of 448, network copy z, 32-row
+// group mg), on v_mfma_f32_32x32x2f32: the block owns 32 columns (one 128-byte
+// line of every W1 row it reads) x the 32 rows of its row group x one K
+// split; wave w owns k in [448 s + 112 w, +112).  Lane l = 32 h + c: B column
+// c, and for MFMA step (g, e), g < 14, e < 4, the k pair {8 g + e, 8 g + 4 +
+// e} (half h takes the second), so the A row loads are float4.  Output rows
+// (r & 3) + 8 (r >> 2) + 4 h of column c.  Partials [Z][FC1_S][B][512] are
+// reduced by the head.  (Round 3: fc1 5.8 -> 4.7 us against the 16 x 16 x 4
+// form, whose 16-column B operand fetched 64-byte halves of W1's lines; that
+// kernel and the in-launch split-K reduce variant are in git history, commit
+// 1a3be58.)
 constexpr int FC1_S = 7, FC1_KS = FLAT / FC1_S, FC1_KW = FC1_KS / 4;  // 448, 112
 constexpr int Z_MAX_FC1 = 3;  // network copies of one fc1 launch (online, target, online(s_t))
 
@@ -297,92 +304,8 @@ struct Fc1FwdArgs {
   int64_t w_off;
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
-  // In-launch split-K reduce (or null: the head sums the FC1_S partials):
-  // the last of a tile's FC1_S split blocks to arrive sums them in split
-  // order into sum[Z][B][512] (pre-activation, no bias), so the head loads
-  // one row per sample instead of FC1_S.
-  float* sum;
-  int* cnt;         // [Z * MG * 32] tile arrival counters (x Handoff::kStride ints), zero between launches
 };
 
-// The MFMA body of one fc1 block: its (z, split s, column tile nt, row group
-// mg) and the four waves' [2][16 x 16] K-quarter tiles in s_red[w * FC1_RW ..]
-// (row 16 mt + r, column n at [mt * FC1_RT + red_idx(r, n)]: 16 floats of
-// padding after every 4 rows, so the lanes kq = 0 / 1 of one ds_write_b32
-// group land 16 banks apart).
-constexpr int FC1_RT = red_rows(16), FC1_RW = 2 * FC1_RT;  // 320, 640 floats
-__device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int i, int& z, int& s, int& nt,
-                                             int& mg) {
-  // Block i -> tile map: the two 16-column tiles that share W1's 128-byte
-  // lines (nt = 2 cp, 2 cp + 1) go to blocks i and i + 8, which round-robin
-  // dispatch places on the same XCD, so each line is fetched into one L2.
-  const int slot = i >> 3, pair = (i & 7) + 8 * (slot >> 1);
-  nt = 2 * (pair % 16) + (slot & 1);
-  const int rest = pair / 16;
-  s = rest % FC1_S;
-  const int zm = rest / FC1_S;
-  z = zm / a.MG;
-  mg = zm % a.MG;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int n = lane & 15, kq = lane >> 4;
-  const int k0 = s * FC1_KS + w * FC1_KW;
-  const float* W = a.nz.p[z] + a.w_off + 16 * nt + n;  // [3136][512]
-  constexpr int J = FC1_KW / 16;                        // 7
-  float wr[J][4];
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) wr[j][e] = W[(int64_t)(k0 + 16 * j + 4 * kq + e) * HID];
-  float4 av[2][J];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int row = min(32 * mg + 16 * mt + n, a.B - 1);
-    const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0 + 4 * kq;
-#pragma unroll
-    for (int j = 0; j < J; ++j) av[mt][j] = *reinterpret_cast<const float4*>(x + 16 * j);
-  }
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      acc[mt] = mfma4(av[mt][j].x, wr[j][0], acc[mt]);
-      acc[mt] = mfma4(av[mt][j].y, wr[j][1], acc[mt]);
-      acc[mt] = mfma4(av[mt][j].z, wr[j][2], acc[mt]);
-      acc[mt] = mfma4(av[mt][j].w, wr[j][3], acc[mt]);
-    }
-  }
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * FC1_RW + mt * FC1_RT + red_idx(4 * kq + rr, n)] = acc[mt][rr];
-  __syncthreads();
-}
-
-// The block's 32 x 16 split partial (the four K-quarter tiles summed in order).
-__device__ __forceinline__ void fc1_fwd_store(const Fc1FwdArgs& a, const float* s_red, int z, int s, int nt, int mg) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = 32 * mg + 16 * h + (t >> 4);
-    const float* sr = s_red + h * FC1_RT + red_idx(t >> 4, t & 15);
-    const float v = (sr[0] + sr[FC1_RW]) + (sr[2 * FC1_RW] + sr[3 * FC1_RW]);
-    if (row < a.B) a.part[(((int64_t)z * FC1_S + s) * a.B + row) * HID + 16 * nt + (t & 15)] = v;
-  }
-}
-
-// fc1 forward on v_mfma_f32_32x32x2f32 (DQZ_FC1_32, default on since round
-// 3: fc1 5.8 -> 4.7 us, 15,870-15,960 -> 16,140-16,240 steps/s; 0 keeps the
-// 16x16x4 fc1_fwd_kernel, which the MGSC tangent launch still uses): a block owns
-// 32 columns (one 128-byte line of every W1 row it reads) x the 32 rows of
-// its row group x one K split; wave w owns k in [448 s + 112 w, +112).  Lane
-// l = 32 h + c: B column c, and for MFMA step (g, e), g < 14, e < 4, the k
-// pair {8 g + e, 8 g + 4 + e} (half h takes the second), so the A row loads
-// are float4.  Output rows (r & 3) + 8 (r >> 2) + 4 h of column c.
-#ifndef DQZ_FC1_32
-#define DQZ_FC1_32 1
-#endif
-constexpr bool kFc1M32 = DQZ_FC1_32 != 0;
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
@@ -429,73 +352,12 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   }
 }
 
+inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
+
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_32RW];
   fc1_fwd_block32(a, s_red, blockIdx.x);
-  DQZ_STAMP(3, 3);
-}
-
-__global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
-  DQZ_STAMP(3, 0);
-  __shared__ float s_red[4 * FC1_RW];
-  int z, s, nt, mg;
-  fc1_fwd_tile(a, s_red, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), z, s, nt, mg);
-  DQZ_STAMP(3, 2);
-  const int t = threadIdx.x;
-  if (kFc1Reduce && a.sum) {
-    // 128 threads x 4 columns: row t / 4, columns 16 nt + 4 (t % 4) .. + 3.
-    // Partials go out write-through (16-B sc1 stores) and are read back with
-    // sc1 loads by the tile's last block (the guide's hand-off row: one lane
-    // per storing workgroup adds to one counter after every wave drained;
-    // the workgroup whose add came last reads).  The other blocks' tiles
-    // share this block's XCD (the block -> tile map above), so the reads are
-    // served from that L2's backing MALL lines at worst.
-    __shared__ int s_last;
-    const int row = t >> 2, c4 = 4 * (t & 3);
-    const int mt = row >> 4, r16 = row & 15;
-    const int64_t colo = 16 * nt + c4;
-    const int64_t pbytes = (int64_t)Z_MAX_FC1 * FC1_S * a.B * HID * 4;  // buffer range for the rsrc
-    if (t < 128) {
-      f32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = mt * FC1_RT + red_idx(r16, c4 + e);
-        v[e] = (s_red[k] + s_red[FC1_RW + k]) + (s_red[2 * FC1_RW + k] + s_red[3 * FC1_RW + k]);
-      }
-      if (32 * mg + row < a.B) {
-        const int64_t off = ((((int64_t)z * FC1_S + s) * a.B + 32 * mg + row) * HID + colo) * 4;
-        store_sc1_f4(a.part, (int)min(pbytes, (int64_t)INT32_MAX), (int)off, v);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* cnt = a.cnt + ((z * a.MG + mg) * (HID / 16) + nt) * Handoff::kStride;
-    if (t == 0) s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FC1_S - 1;
-    __syncthreads();
-    if (!s_last) return;
-    if (t < 128 && 32 * mg + row < a.B) {
-      float4 pv[FC1_S];
-#pragma unroll
-      for (int ss = 0; ss < FC1_S; ++ss) {
-        const int64_t e = (((int64_t)z * FC1_S + ss) * a.B + 32 * mg + row) * HID + colo;
-        pv[ss] = load_sc1_f4(reinterpret_cast<const float4*>(a.part), (int)min(pbytes, (int64_t)INT32_MAX), (int)(e / 4));
-      }
-      float4 acc = pv[0];
-#pragma unroll
-      for (int ss = 1; ss < FC1_S; ++ss) {
-        acc.x += pv[ss].x;
-        acc.y += pv[ss].y;
-        acc.z += pv[ss].z;
-        acc.w += pv[ss].w;
-      }
-      *reinterpret_cast<float4*>(a.sum + ((int64_t)z * a.B + 32 * mg + row) * HID + colo) = acc;
-    }
-    if (t == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    DQZ_STAMP(3, 3);
-    return;
-  }
-  fc1_fwd_store(a, s_red, z, s, nt, mg);
   DQZ_STAMP(3, 3);
 }
 
@@ -505,10 +367,8 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(Fc1FwdArgs a) {
 // layers are independent of each other, so one launch holds them as block
 // ranges [conv1 4/sample] [conv2 4/sample] [conv3 4/sample] [fc1 tiles]
 // instead of four dependent launches.  Dynamic LDS = conv1's 57.6 KB.
-static_assert(4 * FC1_RW * sizeof(float) <= kConv1FwdSmem, "fc1's partial tiles fit the tangent launch's LDS");
-inline int tangent_fwd_blocks(int B, int MG) {
-  return 3 * 4 * ((B + 7) / 8 * 8) + (HID / (kFc1M32 ? 32 : 16)) * FC1_S * MG;
-}
+static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
+inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + fc1_fwd_blocks(1, MG); }
 __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
                                                           Fc1FwdArgs f1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -531,15 +391,7 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
     if (sj.valid) conv3_fwd_body<false>(c3, smem, sj);
     return;
   }
-  i -= n;
-  if constexpr (kFc1M32) {
-    static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
-    fc1_fwd_block32(f1, smem, i);
-  } else {
-    int z, s, nt, mg;
-    fc1_fwd_tile(f1, smem, i, z, s, nt, mg);
-    fc1_fwd_store(f1, smem, z, s, nt, mg);
-  }
+  fc1_fwd_block32(f1, smem, i - n);
 }
 
 }  // namespace dqz

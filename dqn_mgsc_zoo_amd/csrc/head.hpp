@@ -302,12 +302,7 @@ inline void launch_head_z(const HeadArgs& h, int grid, hipStream_t st) {
 
 inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
   if (h.S > 7 || h.Z < 1 || h.Z > 3) return hipErrorInvalidValue;
-  if (kFc1Reduce && h.S == 1) {  // fc1 sums reduced in fc1_fwd_kernel: one row per sample
-    if (h.Z <= 2)
-      launch_head_z<1, 2>(h, grid, st);
-    else
-      launch_head_z<1, 3>(h, grid, st);
-  } else if (h.Z <= 2) {
+  if (h.Z <= 2) {
     launch_head_z<7, 2>(h, grid, st);
   } else {
     launch_head_z<7, 3>(h, grid, st);

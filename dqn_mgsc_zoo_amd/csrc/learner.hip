@@ -56,9 +56,6 @@ struct dqz_learner {
   int64_t off[10], sz[10], total;
   int S_fc1, S2, S3;
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
-  float* fc1sum;  // [Z][B][512] fc1 pre-activations summed by fc1_fwd_kernel's last split block
-  int32_t* fc1cnt;  // its tile arrival counters
-  int32_t* dwcnt;   // XCD-group dW reduce counters: conv3 [8][4], conv2 [8][8] (x Handoff::kStride)
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
   int32_t* ga;
@@ -122,12 +119,10 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
                            n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
-                           (int64_t)Z_MAX_FC1 * MAXB * HID, (int64_t)Z_MAX_FC1 * (MAXB / 32) * (HID / 16) * Handoff::kStride,
-                           (int64_t)(8 * 4 + 8 * 8) * Handoff::kStride, 2 * (int64_t)B};
+                           2 * (int64_t)B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p,
-                    &L->fc1sum, reinterpret_cast<float**>(&L->fc1cnt), reinterpret_cast<float**>(&L->dwcnt),
                     reinterpret_cast<float**>(&L->per_wb)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
@@ -260,22 +255,16 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   f1.B = B;
   f1.MG = (B + 31) / 32;
   f1.part = L->fc1p;
-  f1.sum = kFc1Reduce ? L->fc1sum : nullptr;
-  f1.cnt = L->fc1cnt;
-  if (kFc1M32)
-    DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3((HID / 32) * FC1_S * Z * f1.MG), dim3(256), 0, st, f1);
-              DQZ_HIP(hipGetLastError()));
-  else
-    DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd_kernel, dim3(HID / 16, FC1_S, Z * f1.MG), dim3(256), 0, st, f1);
-              DQZ_HIP(hipGetLastError()));
+  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(256), 0, st, f1);
+            DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
 
 static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
   HeadArgs h{};
   memset(&h, 0, sizeof(h));
-  h.fc1p = kFc1Reduce ? L->fc1sum : L->fc1p;
-  h.S = kFc1Reduce ? 1 : L->S_fc1;
+  h.fc1p = L->fc1p;
+  h.S = L->S_fc1;
   h.h1 = L->h1;
   h.nz = nz;
   h.b1_off = L->off[7];
@@ -393,7 +382,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c3b.w3p = L->w3p;
   c3b.dy2 = L->dy2;
   c3b.part = L->p3;
-  c3b.dwcnt = kDwXcd ? L->dwcnt : nullptr;
   c3b.B = B;
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
@@ -406,7 +394,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.w2p = L->w2p;
   c2b.dy1 = L->dy1;
   c2b.part = L->p2;
-  c2b.dwcnt = kDwXcd ? L->dwcnt + 8 * 4 * Handoff::kStride : nullptr;
   c2b.B = B;
   c2b.sync = c3b.sync;
   Conv1DwArgs c1dw;
@@ -426,8 +413,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int G3 = ((B + C3DW_G - 1) / C3DW_G + 7) / 8 * 8, G2 = ((B + C2DW_G - 1) / C2DW_G + 7) / 8 * 8;
-  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * G3 + 8 * B8 + 8 * G2;
+  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
   DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
@@ -445,9 +431,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.p2 = L->p2;
   u.p3 = L->p3;
   u.S1 = B * C1_BLOCKS;
-  // one slab per dW job group (XCD-group sums in slabs 0..7 with per-sample jobs)
-  u.S2 = kDwXcd && C2DW_G == 1 ? min(8, B) : (B + C2DW_G - 1) / C2DW_G;
-  u.S3 = kDwXcd && C3DW_G == 1 ? min(8, B) : (B + C3DW_G - 1) / C3DW_G;
+  u.S2 = L->S2;  // one dW partial slab per sample
+  u.S3 = L->S3;
   u.h1 = L->h1;
   u.dz1 = L->dz1;
   u.gq = L->gq;
@@ -1344,8 +1329,6 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     c3.b_off = L->off[5];
     c3.out = H->zv3;
     Fc1FwdArgs f1;
-    f1.sum = nullptr;
-    f1.cnt = nullptr;
     f1.in = L->y3;
     f1.nz = nv;
     f1.w_off = L->off[6];

@@ -387,8 +387,10 @@ class MetaLearner:
     """One meta_update on replay `slots` (device int32 [M]); logits updated
     in place at `positions` (device int32 [M], distinct).  `logit_buffer`
     (the replay's device logit buffer, replay_circular._DeviceLogits) keeps
-    its running log-sum-exp current through the write; without it the
-    caller must invalidate that state."""
+    its running log-sum-exp and chunk sums current through the write; when
+    it is omitted and `logits` is a live buffer's tensor, that buffer is
+    used (a raw tensor kept from `replay.logits` must not bypass the state
+    its samplers read)."""
     m = self.meta_batch_size
     if slots.dtype != torch.int32 or slots.numel() != m:
       raise ValueError('slots must be a device int32 tensor of meta batch size')
@@ -398,6 +400,9 @@ class MetaLearner:
       raise ValueError('logits must be float32')
     if logit_buffer is not None and logits.data_ptr() != logit_buffer.logits.data_ptr():
       raise ValueError('logit_buffer does not own these logits')
+    if logit_buffer is None:
+      from dqn_mgsc_zoo_amd import replay_circular  # pylint: disable=g-import-not-at-top
+      logit_buffer = replay_circular.logit_buffer_of(logits)
     lrn = self.learner
     _native.check(_native.lib().dqz_meta_update(
         self._h, ctypes.byref(lrn._params_c), store.c_ref(),  # pylint: disable=protected-access

@@ -15,6 +15,12 @@ dqn_mgsc_batched/agent.py:381-400), so its values are optax 0.1.2 states
   64-bit key and the 64-bit draw counter, JAX's uint32[2] threefry key
   widened by the counter JAX folds into its splits.
 
+A reference-shaped uint32[2] key (a JAX PRNGKey, `jax.random.PRNGKey(seed)`
+= [seed >> 32, seed & 0xFFFFFFFF]) restores as that 64-bit seed with the draw
+counter at 0: JAX's threefry stream itself is not reproducible here, so the
+acting stream restarts at the head of the Philox stream of that seed (a
+documented deviation).
+
 Loaders also take the round-2 forms (a {'seed', 'count'} dict, a (mu, nu)
 pair, a {'count', 'mu', 'nu'} dict) so older checkpoints still restore.
 """
@@ -54,14 +60,17 @@ def pack_key(seed: int, count: int) -> np.ndarray:
 
 
 def unpack_key(key) -> Tuple[int, int]:
-  """uint32[4] key array (or the round-2 {'seed', 'count'} dict) ->
-  (seed, count)."""
+  """uint32[4] key array, a JAX-shaped uint32[2] key (seed, counter 0) or
+  the round-2 {'seed', 'count'} dict -> (seed, count)."""
   if isinstance(key, dict):
     return int(key['seed']), int(key['count'])
   a = np.asarray(key)
-  if a.dtype != np.uint32 or a.shape != (4,):
-    raise ValueError('expected a uint32[4] key, got %s%s' % (a.dtype, a.shape))
+  if a.dtype != np.uint32 or a.shape not in ((4,), (2,)):
+    raise ValueError('expected a uint32[4] or uint32[2] key, got %s%s' %
+                     (a.dtype, a.shape))
   v = [int(x) for x in a.tolist()]
+  if a.shape == (2,):  # jax.random.PRNGKey layout: [hi, lo]
+    return (v[0] << 32) | v[1], 0
   return v[0] | (v[1] << 32), v[2] | (v[3] << 32)
 
 

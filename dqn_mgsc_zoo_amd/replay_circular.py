@@ -15,6 +15,7 @@
 
 import typing
 from typing import Any, Iterable, Mapping, Optional, Sequence, Tuple
+import weakref
 
 import numpy as np
 
@@ -46,6 +47,20 @@ def logsumexp(x: np.ndarray) -> np.ndarray:
   return c + np.log(np.sum(np.exp(x - c)))
 
 
+# Live device logit buffers by the address of their logits tensor, so a
+# writer handed only the raw tensor (MetaLearner.update without
+# logit_buffer) can still find the running state it must keep current.
+_LIVE_BUFFERS = weakref.WeakValueDictionary()
+
+
+def logit_buffer_of(logits) -> Optional['_DeviceLogits']:
+  """The live _DeviceLogits whose logits tensor is `logits`, or None."""
+  buf = _LIVE_BUFFERS.get(logits.data_ptr())
+  if buf is None or buf.logits.numel() != logits.numel():
+    return None
+  return buf
+
+
 class _DeviceLogits:
   """f32 logits [capacity] in HBM plus the libdqz reduction scratch."""
 
@@ -68,6 +83,7 @@ class _DeviceLogits:
                           device=self.device)
     self._idx = torch.zeros((max_queries,), dtype=torch.int64,
                             device=self.device)
+    _LIVE_BUFFERS[self.logits.data_ptr()] = self
 
   def __del__(self):
     h = getattr(self, '_h', None)

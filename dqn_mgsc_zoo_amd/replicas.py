@@ -17,6 +17,10 @@ import os
 import numpy as np
 import torch
 
+# Environment variable naming the rendezvous file of ranks started by
+# bench.spawn_ranks (a torch.distributed.FileStore).
+STORE_FILE_ENV = 'DQZ_STORE_FILE'
+
 
 class Replicas:
   """Rank bookkeeping + the two reporting collectives."""
@@ -30,16 +34,28 @@ class Replicas:
     if self.world == 1 and os.environ.get('DQZ_BENCH_NO_GROUP') == '1':
       return  # diagnostic A/B only: a lone rank without a process group
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
+    backend = backend or 'nccl'
     if not dist.is_initialized():
-      if self.world == 1 and 'MASTER_ADDR' not in os.environ:
-        # a lone rank still forms a group, over an in-process store: a
-        # loopback TCP rendezvous on a probed free port can lose the port
-        # to another process before it binds (EADDRINUSE, seen on the box)
-        dist.init_process_group(backend or 'nccl', store=dist.HashStore(),
-                                rank=0, world_size=1)
-      else:
-        dist.init_process_group(backend or 'nccl', rank=self.rank,
-                                world_size=self.world)
+      kw = {}
+      if backend == 'nccl':
+        # bind the communicator to this rank's GPU up front (without it
+        # torch guesses the device from the global rank)
+        kw['device_id'] = torch.device('cuda', self.local_rank)
+      store_file = os.environ.get(STORE_FILE_ENV)
+      if store_file:
+        # ranks started by bench.spawn_ranks meet in a file store the parent
+        # named: no port is probed and later bound (a probed loopback port
+        # was once taken by another process before the bind, EADDRINUSE)
+        store = dist.FileStore(store_file, self.world)
+        dist.init_process_group(backend, store=store, rank=self.rank,
+                                world_size=self.world, **kw)
+      elif self.world == 1 and 'MASTER_ADDR' not in os.environ:
+        # a lone rank still forms a group, over an in-process store
+        dist.init_process_group(backend, store=dist.HashStore(), rank=0,
+                                world_size=1, **kw)
+      else:  # torch.distributed.run: the launcher's env:// rendezvous
+        dist.init_process_group(backend, rank=self.rank, world_size=self.world,
+                                **kw)
     self.dist = dist
     self.backend = dist.get_backend()
 

@@ -8,8 +8,10 @@ pre-filled to capacity directly on device (mirrors the 1e5-transition
 pre-fill of dqn_mgsc_batched_profiling/timing_atari.py).
 """
 
+import numpy as np
 import torch
 
+from dqn_mgsc_zoo_amd import parts
 from dqn_mgsc_zoo_amd import store as store_lib
 
 
@@ -53,3 +55,37 @@ def fill_episodic(capacity, num_actions, episode_len=1000, seed=0,
   st.discount.copy_(torch.where(last, torch.zeros_like(reward),
                                 torch.full_like(reward, 0.99)))
   return st
+
+
+class SyntheticAtari:
+  """Raw-Atari-shaped environment for the agent loop (no ALE here): each
+  observation is (rgb uint8 [210, 160, 3], lives) as gym_atari's
+  (dqn_zoo/gym_atari.py) with lives; env discount 1 (0 at LAST); a life is
+  lost every 97 frames while more than one is left, and an episode ends
+  after `episode_len` frames.  Frames come from a seeded pool of 64 random
+  RGB images (drawing 100 KB of random bytes per step would cost more host
+  time than the agent), rewards 1 on every 7th frame."""
+
+  def __init__(self, episode_len=2000, seed=1, num_actions=6):
+    self._rng = np.random.default_rng(seed)
+    self._len = episode_len
+    self.num_actions = num_actions
+    self._pool = self._rng.integers(0, 256, (64, 210, 160, 3), dtype=np.uint8)
+    self._t, self._lives = 0, 5
+
+  def _obs(self):
+    return (self._pool[self._t % 64], self._lives)
+
+  def reset(self):
+    self._t, self._lives = 0, 5
+    return parts.TimeStep(parts.StepType.FIRST, None, None, self._obs())
+
+  def step(self, action):
+    del action
+    self._t += 1
+    if self._t % 97 == 0 and self._lives > 1:
+      self._lives -= 1
+    last = self._t >= self._len
+    return parts.TimeStep(parts.StepType.LAST if last else parts.StepType.MID,
+                          float(self._t % 7 == 0), 0.0 if last else 1.0,
+                          self._obs())

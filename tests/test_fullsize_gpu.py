@@ -310,3 +310,145 @@ def test_config4_per_1m_sample_step_write_back(device, store):
   np.testing.assert_allclose(tree.storage[1:], host.sum_tree.storage[1:],
                              rtol=1e-15, atol=0)
   assert max_seen.item() == max(1.0, p.max())
+
+
+def test_config3_fused_step_logits_1m(device, store):
+  """Config 3 through the one call the bench and the MGSC agents time
+  (dqz_learner_step_logits: the softmax-CDF draw inside the forward launch,
+  replay_circular.py:205-217,540-545).  At 1M logits the draw runs the
+  multi-chunk level-1 search over 245 chunk sums.  For the replay
+  Generator's uniforms the slots equal the stand-alone `sample_abs(u)` bit
+  for bit and the step matches the oracle; for Philox draws the slots equal
+  the stand-alone Philox sampler's at the same counter, which both advance."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  rng = np.random.default_rng(11)
+  logits = rng.standard_normal(CAP).astype(np.float32)
+  dev = rc._DeviceLogits(CAP, device, max_queries=512)  # pylint: disable=protected-access
+  dev.load(logits)
+  net = networks.dqn_atari_network(A)
+  online = net.init(12)
+  target = helpers.perturbed_tree(online, 13)
+  lrn = learner_lib.Learner(net, B, algo='dqn', device=device)
+  lrn.set_params(online, target)
+  gen = np.random.default_rng(14)
+  for _ in range(32):
+    u = gen.random(B)
+    want = dev.sample_abs(u).cpu().numpy()
+    batch = _host_batch(store, want)
+    if learner_ref.relu_margin(online, batch[0]) >= MARGIN:
+      break
+  else:
+    raise AssertionError('no kink-free batch')
+  assert len(np.unique(want // 4096)) > 8  # draws land in many chunks
+  out = torch.empty((B,), dtype=torch.int32, device=device)
+  u_dev = torch.as_tensor(u, dtype=torch.float64, device=device)
+  lrn.step_logits(store, dev, out, uniforms=u_dev)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(out.cpu().numpy(), want)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t)
+  _check_step(lrn, ref, target)
+
+  # Philox: the fused draw and the stand-alone sampler at one counter value
+  seed = 99
+  c_fused = torch.full((1,), 5, dtype=torch.int64, device=device)
+  c_alone = c_fused.clone()
+  alone = torch.empty((B,), dtype=torch.int32, device=device)
+  for _ in range(3):
+    dev.sample_slots_philox(seed, c_alone, alone)
+    lrn.step_logits(store, dev, out, seed=seed, counter=c_fused)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), alone.cpu().numpy())
+    assert int(c_fused.item()) == int(c_alone.item())
+  assert int(c_fused.item()) == 8
+  assert lrn.sync_status() == 0
+
+
+def test_config4_fused_step_per_draw_1m(device, store):
+  """Config 4 through the one call the bench and the PER agent time
+  (dqz_learner_step_per_draw: the PER draw inside the forward launch — the
+  tree's top 11 levels staged in LDS, five-level rounds below them — the IS
+  weights in the head and the |td|^alpha write-back in the backward launch;
+  replay.py:680-716, prioritized/agent.py:187-206).  With the reference's
+  RandomState draws injected at 2^20 leaves: ids and fp64 probabilities bit
+  for bit the host distribution's, weights within 2e-7, the double-Q step
+  against the oracle, the tree after the fused write-back equal to the host
+  SumTree.set of the same values."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  alpha, usp, beta = 0.6, 1e-3, 0.4
+  host = replay_lib.PrioritizedDistribution(
+      alpha, usp, np.random.RandomState(0), min_capacity=CAP, max_capacity=CAP)
+  ids = np.arange(CAP)
+  host._assign_indices(ids)  # pylint: disable=protected-access
+  rng = np.random.default_rng(17)
+  index = host.index_of(ids)
+  leaves = np.zeros(CAP)
+  leaves[index] = replay_lib._power(rng.uniform(0.01, 2.0, CAP), alpha)  # pylint: disable=protected-access
+  leaves[index[rng.integers(0, CAP, 2000)]] = 0.0
+  host.sum_tree.set_all(leaves)
+  host.note_priorities(leaves)
+  dist = copy.deepcopy(host)
+  dist.to_device(device)
+  tree = dist.sum_tree
+  tree.index_to_slot[torch.as_tensor(index, device=device)] = torch.as_tensor(
+      ids.astype(np.int32), device=device)
+
+  net = networks.double_dqn_atari_network(A)
+  online = net.init(18)
+  target = helpers.perturbed_tree(online, 19)
+  lrn = learner_lib.Learner(net, B, algo='per', device=device)
+  lrn.set_params(online, target)
+  for seed in range(100, 132):
+    host._random_state = np.random.RandomState(seed)  # pylint: disable=protected-access
+    want_ids, want_probs = host.sample(B)
+    batch = _host_batch(store, want_ids)
+    if learner_ref.relu_margin(online, batch[0]) >= MARGIN:
+      break
+  else:
+    raise AssertionError('no kink-free batch')
+  dist._random_state = np.random.RandomState(seed)  # pylint: disable=protected-access
+  uniform_idx, u = dist.draw(B)
+  inj_i = torch.from_numpy(uniform_idx).to(device)
+  inj_u = torch.from_numpy(u).to(device)
+  idx = torch.empty((B,), dtype=torch.int32, device=device)
+  slots = torch.empty((B,), dtype=torch.int32, device=device)
+  w = torch.empty((B,), dtype=torch.float32, device=device)
+  probs = torch.empty((B,), dtype=torch.float64, device=device)
+  max_seen = torch.ones((1,), dtype=torch.float64, device=device)
+  p = _native.ptr
+  draw = _native.DqzPerDraw(
+      p(tree.tree).value, tree.capacity, 0, CAP, CAP, usp, beta, 1, 0, None,
+      p(inj_i).value, p(inj_u).value, p(tree.index_to_slot).value, alpha,
+      p(max_seen).value, p(idx).value, p(slots).value, p(probs).value,
+      p(w).value)
+  lrn.step_per_draw(store, draw)
+  torch.cuda.synchronize()
+  got_idx = idx.cpu().numpy()
+  assert dist.index_to_id(got_idx).tolist() == want_ids.tolist()
+  assert slots.cpu().numpy().tolist() == want_ids.tolist()
+  assert probs.cpu().numpy().tolist() == want_probs.tolist()  # fp64, bit-exact
+  want_w = replay_lib.importance_sampling_weights(want_probs, 1.0 / CAP, beta, True)
+  np.testing.assert_allclose(w.cpu().numpy(), want_w.astype(np.float32), rtol=2e-7)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t,
+                                 algo='per', weights=w.cpu().numpy())
+  _check_step(lrn, ref, target)
+  # the fused write-back: |td|^alpha at the drawn leaves (last draw of a
+  # repeated index wins), ancestors rebuilt, max_seen the running max
+  _, td, _ = lrn.fetch_outputs()
+  torch.cuda.synchronize()
+  pr = np.abs(td.cpu().numpy().astype(np.float64))
+  last = {}
+  for i, v in zip(got_idx.tolist(), pr.tolist()):
+    last[i] = v
+  host.sum_tree.set(list(last), replay_lib._power(np.array(list(last.values())), alpha))  # pylint: disable=protected-access
+  np.testing.assert_allclose(tree.storage[1:], host.sum_tree.storage[1:],
+                             rtol=1e-15, atol=0)
+  assert max_seen.item() == max(1.0, pr.max())

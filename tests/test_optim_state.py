@@ -28,9 +28,15 @@ def test_key_rejects_out_of_range_and_wrong_shapes():
   with pytest.raises(ValueError):
     os_.pack_key(0, 2**64)
   with pytest.raises(ValueError):
-    os_.unpack_key(np.zeros(2, np.uint32))
+    os_.unpack_key(np.zeros(3, np.uint32))
   with pytest.raises(ValueError):
     os_.unpack_key(np.zeros(4, np.int64))
+
+
+def test_jax_shaped_key_restores_as_seed_with_counter_zero():
+  # jax.random.PRNGKey(seed) = uint32[2] [seed >> 32, seed & 0xFFFFFFFF]
+  seed = (5 << 32) | 42
+  assert os_.unpack_key(np.array([5, 42], np.uint32)) == (seed, 0)
 
 
 def test_legacy_dict_key_still_restores():

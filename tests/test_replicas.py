@@ -56,3 +56,35 @@ def test_replicas_single_process():
     np.testing.assert_array_equal(r.gather_stats([1.0, 2.0]), [[1.0, 2.0]])
   finally:
     r.close()
+
+
+def _file_store_worker(rank, world, path, q):
+  os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank))
+  for k in ('MASTER_ADDR', 'MASTER_PORT'):
+    os.environ.pop(k, None)
+  from dqn_mgsc_zoo_amd import replicas  # pylint: disable=g-import-not-at-top
+  os.environ[replicas.STORE_FILE_ENV] = path
+  r = replicas.Replicas(backend='gloo')
+  mx = r.max_over_ranks(float(rank))
+  stats = r.gather_stats([float(rank)])
+  q.put((rank, mx, stats.tolist()))
+  r.close()
+
+
+def test_replicas_file_store_rendezvous(tmp_path):
+  """Ranks spawned by bench.spawn_ranks meet in a FileStore the parent
+  names (no probed port)."""
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  path = str(tmp_path / 'store')
+  procs = [ctx.Process(target=_file_store_worker, args=(i, 2, path, q))
+           for i in range(2)]
+  for p in procs:
+    p.start()
+  out = [q.get(timeout=120) for _ in procs]
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  for _, mx, stats in out:
+    assert mx == 1.0
+    np.testing.assert_array_equal(stats, [[0.0], [1.0]])

@@ -26,35 +26,11 @@ sys.path.insert(0, ROOT)
 from dqn_mgsc_zoo_amd import learner as learner_lib  # noqa: E402
 from dqn_mgsc_zoo_amd import networks, parts  # noqa: E402
 from dqn_mgsc_zoo_amd import replay as replay_lib  # noqa: E402
+from dqn_mgsc_zoo_amd import synthetic  # noqa: E402
 from tests import fake_env  # noqa: E402
 
 
-class FakeRGBAtari:
-  """Raw-Atari-shaped env: (rgb uint8 [210,160,3], lives) observations,
-  env discount 1 (0 at LAST), a life lost now and then."""
-
-  def __init__(self, episode_len=2000, seed=1):
-    self._rng = np.random.default_rng(seed)
-    self._len = episode_len
-    # a pool of frames: drawing 100 KB of random bytes per step would cost
-    # more host time than the agent itself
-    self._pool = self._rng.integers(0, 256, (64, 210, 160, 3), dtype=np.uint8)
-
-  def _obs(self):
-    return (self._pool[self._t % 64], self._lives)
-
-  def reset(self):
-    self._t, self._lives = 0, 5
-    return parts.TimeStep(parts.StepType.FIRST, None, None, self._obs())
-
-  def step(self, action):
-    del action
-    self._t += 1
-    if self._t % 97 == 0 and self._lives > 1:
-      self._lives -= 1
-    last = self._t >= self._len
-    return parts.TimeStep(parts.StepType.LAST if last else parts.StepType.MID,
-                          float(self._t % 7 == 0), 0.0 if last else 1.0, self._obs())
+FakeRGBAtari = synthetic.SyntheticAtari
 
 
 def host_atari_frame(obs):

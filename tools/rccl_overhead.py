@@ -17,6 +17,13 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
+def _free_port():
+  import socket  # pylint: disable=g-import-not-at-top
+  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+    s.bind(('127.0.0.1', 0))
+    return s.getsockname()[1]
+
+
 def main():
   dev = torch.device('cuda:0')
   torch.cuda.set_device(dev)
@@ -24,7 +31,7 @@ def main():
   before = len(sys.argv) > 1 and sys.argv[1] == 'before'
   import torch.distributed as dist  # pylint: disable=g-import-not-at-top
   os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-  os.environ.setdefault('MASTER_PORT', str(bench.free_port()))
+  os.environ.setdefault('MASTER_PORT', str(_free_port()))
   if before:  # the group exists while the workload is built and captured
     dist.init_process_group('nccl', rank=0, world_size=1)
   wl = bench.Workload('dqn', 1_000_000, 0, dev)
