@@ -682,22 +682,27 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
 // and the independent dW job sets share one launch, so the latency-bound dX
 // workgroups and the dW workgroups share the CUs (no cross-stream edges).
 
-__global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
+constexpr int FC1X_BLOCKS = FLAT / 16;  // 196
+__device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, int blk) {
   // W3 / W2 dX copies: element i of the 69,632 is thread i of the grid (the
   // gathers are issued first and land under the block's own work)
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blk * 256 + threadIdx.x;
   float v3 = 0.f, v2 = 0.f;
   if (a.w3p) {
     if (g < W3P_N) v3 = a.w3[w3p_src(g)];
     if (g < W2P_N) v2 = a.w2[w2p_src(g)];
   }
-  fc1_dx_body(a, smem, blockIdx.x);
+  fc1_dx_body(a, smem, blk);
   if (a.w3p) {
     if (g < W3P_N) a.w3p[g] = v3;
     if (g < W2P_N) a.w2p[g] = v2;
   }
   DQZ_STAMP(5, 3);
+}
+
+__global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
+  fc1_dx_block(a, smem, blockIdx.x);
 }
 
 // bwd_bc_kernel: the whole backward after fc1 dX in one launch.  Grid, in

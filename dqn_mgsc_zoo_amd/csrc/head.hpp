@@ -395,25 +395,24 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 // LDS.  Grid: the small head leaves first (their blocks run the longest
 // per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
 // RMSProp operands are loaded at entry, under the reduction's latency.
-__global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
+__device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[UPD_PAIRS], int blk) {
   DQZ_STAMP(9, 0);
-  __shared__ float2 s_part[UPD_GROUPS][UPD_PAIRS];
   const int pl = threadIdx.x % UPD_PAIRS, grp = threadIdx.x / UPD_PAIRS;
   const int64_t nsmall = HID + (int64_t)HID * u.A + u.nb2;
   const int small_blocks = (int)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS);
   const int64_t c1 = u.sz[0] + u.sz[1], c2 = c1 + u.sz[2] + u.sz[3], c3 = c2 + u.sz[4] + u.sz[5];
   float loss = 0.f;
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
+  if (blk == 0 && threadIdx.x < 64) {
     for (int b = threadIdx.x; b < u.B; b += 64) loss += u.loss_part[b];
   }
   int64_t dst[2] = {-1, -1};
   float2 g = make_float2(0.f, 0.f);
-  if ((int)blockIdx.x < small_blocks) {
-    const int64_t e = (int64_t)blockIdx.x * UPD_PARAMS + 2 * pl;
+  if ((int)blk < small_blocks) {
+    const int64_t e = (int64_t)blk * UPD_PARAMS + 2 * pl;
     g.x = small_grad(u, e, grp, dst[0]);
     g.y = small_grad(u, e + 1, grp, dst[1]);
   } else {
-    const int64_t j = (int64_t)(blockIdx.x - small_blocks) * UPD_PARAMS + 2 * pl;  // even; regions are even-sized
+    const int64_t j = (int64_t)(blk - small_blocks) * UPD_PARAMS + 2 * pl;  // even; regions are even-sized
     if (j < c1) {  // conv1: w rows 0..255, bias row 256
       g = sum_split2(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, j, grp);
       for (int h = 0; h < 2; ++h) dst[h] = j + h < u.sz[0] ? u.off[0] + j + h : u.off[1] + (j + h - u.sz[0]);
@@ -439,7 +438,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
       }
   }
   s_part[grp][pl] = g;
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
+  if (blk == 0 && threadIdx.x < 64) {
     loss = wave_sum(loss);
     if (threadIdx.x == 0) {
       u.loss[0] = loss / (float)u.B;
@@ -472,6 +471,17 @@ __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
     }
   }
   DQZ_STAMP(9, 3);
+}
+
+inline unsigned update_blocks(const int64_t sz[10], int A, int nb2) {
+  const int64_t nconv = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
+  const int64_t nsmall = HID + (int64_t)HID * A + nb2;
+  return (unsigned)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS + (nconv + UPD_PARAMS - 1) / UPD_PARAMS);
+}
+
+__global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
+  __shared__ float2 s_part[UPD_GROUPS][UPD_PAIRS];
+  update_body(u, s_part, blockIdx.x);
 }
 
 __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
