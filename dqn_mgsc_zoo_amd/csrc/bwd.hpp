@@ -583,7 +583,7 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   const int kb = blk >> 2, nq = blk & 3;
   const int k0 = 16 * kb, c0 = 128 * nq;
   const Rms& R = a.rms;
-  const bool upd = R.gout == nullptr;
+  const bool upd = R.update();
   // GEMM operands of a 32-sample chunk: dz1[c + row][c0 ..] (LDS) and
   // y3[c + 4 kk + kq][k0 + n] (A operand, registers).
   float4 v[4];
@@ -609,14 +609,16 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   // operands and unconditionally (gradient-output mode re-reads theta: mu /
   // nu may be null there): vmcnt is in order, so the GEMM waits for its own
   // operands only and these loads land under it.
-  const float* pmu = upd ? a.mu : a.th;
-  const float* pnu = upd ? a.nu : a.th;
+  // (meta_rms1 reads theta, mu, nu too; meta_rms2 reads J, mu1, nu1)
+  const float* pth = R.meta == 2 ? R.J : a.th;
+  const float* pmu = R.meta == 2 ? R.mu1 : (upd || R.meta == 1) ? a.mu : a.th;
+  const float* pnu = R.meta == 2 ? R.nu1 : (upd || R.meta == 1) ? a.nu : a.th;
   const int64_t e0 = a.w_off + (int64_t)(k0 + (lane >> 3)) * HID + c0 + 32 * w + 4 * (lane & 7);
   float4 o_th[2], o_mu[2], o_nu[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int64_t e = e0 + (int64_t)8 * h * HID;
-    o_th[h] = *reinterpret_cast<const float4*>(a.th + e);
+    o_th[h] = *reinterpret_cast<const float4*>(pth + e);
     o_mu[h] = *reinterpret_cast<const float4*>(pmu + e);
     o_nu[h] = *reinterpret_cast<const float4*>(pnu + e);
   }
@@ -649,11 +651,30 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tile[(4 * kq + r) * FC1W_TLD + 16 * q + n] = gacc[q][r];
+  float sq = 0.f;  // meta_rms2: this thread's u'^2
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const float4 g = *reinterpret_cast<const float4*>(tile + ((lane >> 3) + 8 * h) * FC1W_TLD + 4 * (lane & 7));
     const int64_t e = e0 + (int64_t)8 * h * HID;
-    if (!upd) {
+    if (R.meta == 1) {
+      float4 t = o_th[h], m = o_mu[h], v = o_nu[h], j;
+      j.x = R.meta1(g.x, t.x, m.x, v.x);
+      j.y = R.meta1(g.y, t.y, m.y, v.y);
+      j.z = R.meta1(g.z, t.z, m.z, v.z);
+      j.w = R.meta1(g.w, t.w, m.w, v.w);
+      *reinterpret_cast<float4*>(R.thp + e) = t;
+      *reinterpret_cast<float4*>(R.mu1 + e) = m;
+      *reinterpret_cast<float4*>(R.nu1 + e) = v;
+      *reinterpret_cast<float4*>(R.J + e) = j;
+      if (R.gout) *reinterpret_cast<float4*>(R.gout + e) = g;
+    } else if (R.meta == 2) {
+      float4 o;
+      o.x = R.meta2(g.x, o_mu[h].x, o_nu[h].x, o_th[h].x, sq);
+      o.y = R.meta2(g.y, o_mu[h].y, o_nu[h].y, o_th[h].y, sq);
+      o.z = R.meta2(g.z, o_mu[h].z, o_nu[h].z, o_th[h].z, sq);
+      o.w = R.meta2(g.w, o_mu[h].w, o_nu[h].w, o_th[h].w, sq);
+      *reinterpret_cast<float4*>(R.vout + e) = o;
+    } else if (!upd) {
       float4 o = g;
       if (R.gacc) {
         const float4 prev = *reinterpret_cast<const float4*>(R.gout + e);
@@ -672,6 +693,15 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
       *reinterpret_cast<float4*>(a.mu + e) = m;
       *reinterpret_cast<float4*>(a.nu + e) = vv;
       *reinterpret_cast<float4*>(a.th + e) = th;
+    }
+  }
+  if (R.meta == 2) {  // the block's u'^2 (each wave's sum in its own tile, then wave 0)
+    sq = wave_sum(sq);
+    if (lane == 0) tile[0] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float* t0 = smem + 32 * FC1W_LD;
+      R.sq_part[R.sq_off + blk] = (t0[0] + t0[16 * FC1W_TLD]) + (t0[2 * 16 * FC1W_TLD] + t0[3 * 16 * FC1W_TLD]);
     }
   }
   DQZ_STAMP(11, 3);

@@ -82,12 +82,23 @@ struct NetZ {
 // optax 0.1.2 scale_by_stddev + scale(-lr) (dqn/run_atari.py:208-213):
 //   mu = (1-decay) g + decay mu ; nu = (1-decay) g^2 + decay nu
 //   theta += -lr * g * rsqrt(nu - mu^2 + eps)
-// Centered RMSProp on one parameter, or — when `gout` is set (gradient-output
-// mode, used by the MGSC meta-update) — store the gradient at gout[i] instead.
+// The epilogue that consumes each parameter's gradient g where it is formed
+// (the fc1 dW blocks of bwd_bc_kernel, update_kernel for every other leaf):
+// centered RMSProp in place, or — gradient-output mode, `gout` set — the
+// gradient stored at gout[i], or one of the MGSC meta-update's elementwise
+// stages (meta.hpp) applied to it instead of in a launch of its own:
+//   meta == 1 (meta_rms1): theta' = theta + u(g; mu, nu) -> thp, the updated
+//             moments -> mu1, nu1, J = du/dg -> J (and g -> gout when set);
+//   meta == 2 (meta_rms2): u' = u(g; mu1, nu1), v = -2 u' J -> vout, and the
+//             block's sum of u'^2 -> sq_part[sq_off + block].
 struct Rms {
   float lr, decay, c1, eps;
   float* gout;
   int gacc;  // gradient-output mode: 1 adds into gout (meta-batch chunks), 0 overwrites
+  int meta;  // 0, 1 or 2 (above)
+  float *thp, *mu1, *nu1, *J, *vout, *sq_part;
+  int sq_off;
+  __device__ __forceinline__ bool update() const { return gout == nullptr && meta == 0; }
   // One centered RMSProp step (optax 0.1.2 scale_by_stddev, eps inside the
   // sqrt).  Every multiply-add is an explicit fma: hipcc contracts a*b + c*d
   // either way round depending on the surrounding code, and fc1/w is updated
@@ -98,16 +109,25 @@ struct Rms {
     nu = __fmaf_rn(c1, g * g, decay * nu);
     th = __fmaf_rn(-lr, g * rsqrtf(__fmaf_rn(-mu, mu, nu) + eps), th);
   }
-  __device__ __forceinline__ void apply(float* th, float* mu, float* nu, int64_t i, float g) const {
-    if (gout) {
-      gout[i] = gacc ? gout[i] + g : g;
-      return;
-    }
-    float t = th[i], m = mu[i], v = nu[i];
-    step(g, t, m, v);
-    mu[i] = m;
-    nu[i] = v;
-    th[i] = t;
+  // meta_rms1 on one parameter: theta' (th), mu' (mu), nu' (nu), J (returned)
+  //   J = du/dg = -lr D^{-3/2} (D - c1 g (g - mu')),  D = nu' - mu'^2 + eps
+  __device__ __forceinline__ float meta1(float g, float& th, float& mu, float& nu) const {
+    const float m = c1 * g + decay * mu;
+    const float v = c1 * (g * g) + decay * nu;
+    const float d = v - m * m + eps;
+    const float rs = rsqrtf(d);
+    th = th + (-lr) * (g * rs);
+    mu = m;
+    nu = v;
+    return -lr * (d - c1 * g * (g - m)) * (rs * rs * rs);
+  }
+  // meta_rms2 on one parameter: u' = u(g; mu1, nu1); returns v = -2 u' J
+  __device__ __forceinline__ float meta2(float g, float m0, float v0, float j, float& sq) const {
+    const float m = c1 * g + decay * m0;
+    const float v = c1 * (g * g) + decay * v0;
+    const float u = (-lr) * (g * rsqrtf(v - m * m + eps));
+    sq += u * u;
+    return -2.f * u * j;
   }
 };
 

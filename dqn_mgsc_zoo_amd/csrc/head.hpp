@@ -428,13 +428,17 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
   }
   const Rms& R = u.rms;
   float o_th[2] = {0.f, 0.f}, o_mu[2] = {0.f, 0.f}, o_nu[2] = {0.f, 0.f};
-  if (grp == 0 && R.gout == nullptr) {
+  if (grp == 0 && (R.gout == nullptr || R.meta != 0)) {
+    // the epilogue's operands: theta, mu, nu (RMSProp, meta_rms1) or J, mu1, nu1 (meta_rms2)
+    const float* pt = R.meta == 2 ? R.J : u.th;
+    const float* pm = R.meta == 2 ? R.mu1 : u.mu;
+    const float* pn = R.meta == 2 ? R.nu1 : u.nu;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (dst[h] >= 0) {
-        o_th[h] = u.th[dst[h]];
-        o_mu[h] = u.mu[dst[h]];
-        o_nu[h] = u.nu[dst[h]];
+        o_th[h] = pt[dst[h]];
+        o_mu[h] = pm[dst[h]];
+        o_nu[h] = pn[dst[h]];
       }
   }
   s_part[grp][pl] = g;
@@ -447,6 +451,7 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     }
   }
   __syncthreads();
+  float sq = 0.f;  // meta_rms2: this thread's u'^2
   if (grp == 0) {
     float2 gs = make_float2(0.f, 0.f);
 #pragma unroll
@@ -459,7 +464,17 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     for (int h = 0; h < 2; ++h) {
       if (dst[h] < 0) continue;
       const int64_t i = dst[h];
-      if (R.gout) {
+      if (R.meta == 1) {
+        float t = o_th[h], m = o_mu[h], v = o_nu[h];
+        const float j = R.meta1(gv[h], t, m, v);
+        R.thp[i] = t;
+        R.mu1[i] = m;
+        R.nu1[i] = v;
+        R.J[i] = j;
+        if (R.gout) R.gout[i] = gv[h];
+      } else if (R.meta == 2) {
+        R.vout[i] = R.meta2(gv[h], o_mu[h], o_nu[h], o_th[h], sq);
+      } else if (R.gout) {
         R.gout[i] = R.gacc ? R.gout[i] + gv[h] : gv[h];
       } else {
         float t = o_th[h], m = o_mu[h], v = o_nu[h];
@@ -469,6 +484,10 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         u.th[i] = t;
       }
     }
+  }
+  if (R.meta == 2 && threadIdx.x < 64) {  // grp 0 is the first half of wave 0
+    sq = wave_sum(sq);
+    if (threadIdx.x == 0) R.sq_part[R.sq_off + blk] = sq;
   }
   DQZ_STAMP(9, 3);
 }

@@ -330,11 +330,13 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
                      int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr,
-                     const PerSampleArgs* pd = nullptr, const UniformDraw* ahead = nullptr) {
+                     const PerSampleArgs* pd = nullptr, const UniformDraw* ahead = nullptr,
+                     const Rms* meta_epi = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (ahead && (pe.on() || gout || meta_p || draw || sm || pd || wb || L->cfg.algo != DQZ_ALGO_DQN))
     return fail(DQZ_ERR_INVALID, "the target lookahead runs plain DQN learner steps only");
-  if (!gout && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
+  if (!gout && !meta_epi && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
+  if (meta_epi && meta_epi->meta == 1 && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
   if (L->cfg.algo == DQZ_ALGO_PER && !is_weights && !pd) return fail(DQZ_ERR_INVALID, "PER step needs is_weights");
   hipStream_t st = (hipStream_t)stream;
@@ -424,6 +426,18 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   rms.eps = L->cfg.eps;
   rms.gout = gout;
   rms.gacc = gacc;
+  rms.meta = 0;
+  rms.thp = rms.mu1 = rms.nu1 = rms.J = rms.vout = rms.sq_part = nullptr;
+  rms.sq_off = 0;
+  if (meta_epi) {  // an MGSC meta stage applied in the gradient epilogues (Rms)
+    rms.meta = meta_epi->meta;
+    rms.thp = meta_epi->thp;
+    rms.mu1 = meta_epi->mu1;
+    rms.nu1 = meta_epi->nu1;
+    rms.J = meta_epi->J;
+    rms.vout = meta_epi->vout;
+    rms.sq_part = meta_epi->sq_part;
+  }
 
   HeadArgs h = make_head(L, nz, Z, B);
   h.fwd_only = 0;
@@ -553,6 +567,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.B = B;
   u.nb2 = L->shared_bias ? 1 : A;
   u.rms = rms;
+  u.rms.sq_off = 4 * (FLAT / 16);  // meta_rms2 partials: the fc1 dW blocks' first, then the update's
   const unsigned nblk = update_blocks(L->sz, A, u.nb2);
   if (ahead) {
     LayerFwdArgs a3 = a2;
@@ -1347,14 +1362,31 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   DQZ_HIP(hipGetLastError());
 
   // G = sum_i p_i g_i: batched backwards with p-weighted cotangents, one per
-  // chunk of C samples, accumulated in chunk order (deterministic).
-  for (int k = 0; k < K; ++k) {
-    if (int rc = step_impl(L, P, S, H->slots_pad + (int64_t)k * C, nullptr, stream, kNoProfile, H->G,
-                           H->p + (int64_t)k * C, nullptr, 0, k > 0 ? 1 : 0))
+  // chunk of C samples, accumulated in chunk order (deterministic).  With one
+  // chunk, meta_rms1 (theta' = theta + u(G), mu', nu', J) runs in the
+  // backward's gradient epilogues (Rms::meta1) instead of its own launch; G
+  // itself is stored only for the second order (meta_second_kernel reads it).
+  const bool so = H->cfg.second_order != 0;
+  Rms epi{};
+  epi.thp = H->thp;
+  epi.mu1 = H->mu1;
+  epi.nu1 = H->nu1;
+  epi.J = H->J;
+  epi.sq_part = H->loss_part;
+  if (K == 1) {
+    epi.meta = 1;
+    if (int rc = step_impl(L, P, S, H->slots_pad, nullptr, stream, kNoProfile, so ? H->G : nullptr, H->p, nullptr,
+                           0, 0, nullptr, nullptr, nullptr, nullptr, &epi))
       return rc;
-    // (one chunk: the batch learner's td stays current until the next update,
+    // (the batch learner's td stays current until the next update,
     // dqz_meta_outputs copies it from there)
-    if (K > 1) DQZ_HIP(hipMemcpyAsync(H->td + (int64_t)k * C, L->td, sizeof(float) * C, hipMemcpyDeviceToDevice, st));
+  } else {
+    for (int k = 0; k < K; ++k) {
+      if (int rc = step_impl(L, P, S, H->slots_pad + (int64_t)k * C, nullptr, stream, kNoProfile, H->G,
+                             H->p + (int64_t)k * C, nullptr, 0, k > 0 ? 1 : 0))
+        return rc;
+      DQZ_HIP(hipMemcpyAsync(H->td + (int64_t)k * C, L->td, sizeof(float) * C, hipMemcpyDeviceToDevice, st));
+    }
   }
 
   MetaRmsArgs ra;
@@ -1364,10 +1396,12 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ra.eps = H->cfg.eps;
   ra.n4 = H->total / 4;
   const dim3 eg((unsigned)((ra.n4 + 255) / 256));
-  hipLaunchKernelGGL(meta_rms1_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)P->online,
-                     (const float4*)P->mu, (const float4*)P->nu, (float4*)H->thp, (float4*)H->mu1,
-                     (float4*)H->nu1, (float4*)H->J);
-  DQZ_HIP(hipGetLastError());
+  if (K > 1) {
+    hipLaunchKernelGGL(meta_rms1_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)P->online,
+                       (const float4*)P->mu, (const float4*)P->nu, (float4*)H->thp, (float4*)H->mu1,
+                       (float4*)H->nu1, (float4*)H->J);
+    DQZ_HIP(hipGetLastError());
+  }
 
   dqz_params P1;
   P1.online = H->thp;
@@ -1375,13 +1409,19 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   P1.mu = nullptr;
   P1.nu = nullptr;
   int nloss = H->nparts;
-  if (!H->cfg.second_order) {
-    // g' = grad loss_fn(theta', target = theta, online transition) -> G buffer.
-    if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->G)) return rc;
-    // v = -2 u' du/dG -> thp buffer; partial sums of u'^2.
-    hipLaunchKernelGGL(meta_rms2_kernel, eg, dim3(256), 0, st, ra, (const float4*)H->G, (const float4*)H->mu1,
-                       (const float4*)H->nu1, (const float4*)H->J, (float4*)H->thp, H->loss_part);
-    DQZ_HIP(hipGetLastError());
+  const float* v = H->thp;
+  if (!so) {
+    // g' = grad loss_fn(theta', target = theta, online transition), consumed
+    // where it is formed by meta_rms2 (Rms::meta2): v = -2 u' du/dG -> the G
+    // buffer (free in the first order), per-block partial sums of u'^2 (the
+    // fc1 dW blocks' then the update's).
+    epi.meta = 2;
+    epi.vout = H->G;
+    if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0,
+                           nullptr, nullptr, nullptr, nullptr, &epi))
+      return rc;
+    v = H->G;
+    nloss = 4 * (FLAT / 16) + (int)update_blocks(H->l1->sz, A, H->l1->shared_bias ? 1 : A);
   } else {
     // grad q[a] at theta' (unit cotangent) -> GQ; the one-sample learner keeps
     // the primal activations, the unit-cotangent backward signals and td'.
@@ -1446,7 +1486,6 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     DQZ_HIP(hipGetLastError());
     nloss = H->nparts2;
   }
-  const float* v = H->thp;
 
   // Tangent forward over the stored online activations: V * y + vb per layer,
   // chunk by chunk (K > 1: the chunk's forward / backward is recomputed first

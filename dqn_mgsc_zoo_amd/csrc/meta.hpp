@@ -79,7 +79,8 @@ struct MetaRmsArgs {
 };
 
 // theta' = theta + u(G; mu, nu); keeps mu', nu' and J = du/dG
-//   = -lr D^{-3/2} (D - c1 G (G - mu')),  D = nu' - mu'^2 + eps.
+//   = -lr D^{-3/2} (D - c1 G (G - mu')),  D = nu' - mu'^2 + eps
+// (meta batches of more than one chunk: G is complete only after the last).
 __global__ __launch_bounds__(256) void meta_rms1_kernel(MetaRmsArgs a, const float4* __restrict__ G,
                                                         const float4* __restrict__ th,
                                                         const float4* __restrict__ mu,
@@ -110,35 +111,9 @@ __global__ __launch_bounds__(256) void meta_rms1_kernel(MetaRmsArgs a, const flo
   J[i] = o_j;
 }
 
-// u' = u(g'; mu', nu') (theta'' - theta'), v = dL/dG = -2 u' J, and per-block
-// partial sums of u'^2 (the meta loss).
-__global__ __launch_bounds__(256) void meta_rms2_kernel(MetaRmsArgs a, const float4* __restrict__ g2,
-                                                        const float4* __restrict__ mu1,
-                                                        const float4* __restrict__ nu1,
-                                                        const float4* __restrict__ J, float4* __restrict__ v_out,
-                                                        float* __restrict__ loss_part) {
-  __shared__ float sbuf[4];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float sq = 0.f;
-  if (i < a.n4) {
-    const float4 g4 = g2[i], m4 = mu1[i], n4 = nu1[i], j4 = J[i];
-    float4 o;
-    auto one = [&](float g, float m0, float v0, float j, float& ov) {
-      const float m = a.c1 * g + a.decay * m0;
-      const float v = a.c1 * (g * g) + a.decay * v0;
-      const float u = (-a.lr) * (g * rsqrtf(v - m * m + a.eps));
-      ov = -2.f * u * j;
-      sq += u * u;
-    };
-    one(g4.x, m4.x, n4.x, j4.x, o.x);
-    one(g4.y, m4.y, n4.y, j4.y, o.y);
-    one(g4.z, m4.z, n4.z, j4.z, o.z);
-    one(g4.w, m4.w, n4.w, j4.w, o.w);
-    v_out[i] = o;
-  }
-  sq = block_sum_f32(sq, sbuf);
-  if (threadIdx.x == 0) loss_part[blockIdx.x] = sq;
-}
+// meta_rms2 (u' = u(g'; mu', nu'), v = dL/dG = -2 u' J, the u'^2 partials)
+// runs in the one-transition backward's gradient epilogues (common.hpp
+// Rms::meta2), and with one meta chunk so does meta_rms1 (Rms::meta1).
 
 struct MetaDotArgs {
   const float* dy1;  // [M][400][32] p-weighted conv1 pre-activation grads
