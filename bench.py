@@ -65,6 +65,23 @@ WORKLOAD = {
             'softmax sample over N(0,1) learned logits + DQN step',
 }
 PER_ALPHA, PER_BETA, PER_USP = 0.6, 0.4, 1e-3  # prioritized/run_atari.py:104-114
+# Algorithmic FLOP of one MGSC meta-update at M = META_BATCH
+# (dqn_mgsc_batched/agent.py:152-220; DESIGN.md §4 "MGSC meta-update"):
+#   the p-weighted loss gradient over the M meta transitions (2 forwards +
+#   backward per sample, SURVEY §8(d)'s 34,107,392 MAC), the one-transition
+#   gradient at theta', the tangent forward V * y of conv1..fc1 (and fc2's
+#   h1 . V2[:, a]) over the M samples, and the per-sample dot products
+#   <dz, V y + vb> (21,632 MAC); the second order (the reservoir agent's
+#   Hessian-vector product of the online transition's q) adds a tangent
+#   forward and a tangent backward of that one sample (2 x (fwd + bwd) MAC).
+#   Elementwise stages (RMSProp tangents, Adam) are counted as bytes, not FLOP.
+_FWD_MAC = 9346048
+_BWD_MAC = 15415296
+META_FLOP = {
+    'first': 2 * (META_BATCH * 34107392 + 34107392 + META_BATCH * (_FWD_MAC - 3072 + 512)
+                  + META_BATCH * 21632),
+}
+META_FLOP['second'] = META_FLOP['first'] + 2 * 2 * (_FWD_MAC + _BWD_MAC)
 STATS_LEN = 3  # the in-loop RCCL statistics vector: steps, loss, seconds
 
 ALL_BWD = 'conv3_dx+conv2_dx+fc1_dw+conv3_dw+conv2_dw+conv1_dw'
@@ -859,6 +876,15 @@ def run_gpu(args, g, rem):
                                     'meta_update_M5': 4.13,
                                     'replay_sample_meta_batch': 55.6}
     out['meta_update_us'] = {k: round(1e3 * v, 2) for k, v in meta_ms.items()}
+    meta_roof = {}
+    for order in ('first', 'second'):
+      ms = meta_ms.get('M%d_%s_order' % (META_BATCH, order))
+      if ms:
+        tf = META_FLOP[order] / (ms * 1e-3) / 1e12
+        meta_roof[order] = {'algorithmic_flop': META_FLOP[order], 'us': round(1e3 * ms, 2),
+                            'achieved_tflops': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS,
+                            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 4)}
+    out['meta_roofline'] = meta_roof
   if world == 1 and args.cpu_seconds > 0:
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
   else:

@@ -133,16 +133,16 @@ struct MetaDotArgs {
   float* s_out;      // [M]  p_i dL/dp_i
 };
 
-// One block (512 threads) per meta-batch sample.
-__global__ __launch_bounds__(512) void meta_dot_kernel(MetaDotArgs a) {
-  __shared__ float sbuf[8];
-  __shared__ float s_fc2[8];
-  const int b = blockIdx.x, t = threadIdx.x;
+// p_i dL/dp_i of sample `b` (256 threads; the block's sum in every thread).
+__device__ __forceinline__ float meta_dot_sample(const MetaDotArgs& a, int b) {
+  __shared__ float sbuf[4];
+  __shared__ float s_fc2[4];
+  const int t = threadIdx.x;
   float acc = 0.f;
   {
     const float4* d = reinterpret_cast<const float4*>(a.dy1 + (int64_t)b * C1M * C1CO);
     const float4* z = reinterpret_cast<const float4*>(a.zv1 + (int64_t)b * C1M * C1CO);
-    for (int i = t; i < C1M * C1CO / 4; i += 512) {
+    for (int i = t; i < C1M * C1CO / 4; i += 256) {
       const float4 x = d[i], y = z[i];
       acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
     }
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(512) void meta_dot_kernel(MetaDotArgs a) {
   {
     const float4* d = reinterpret_cast<const float4*>(a.dy2 + (int64_t)b * C2M * C2CO);
     const float4* z = reinterpret_cast<const float4*>(a.zv2 + (int64_t)b * C2M * C2CO);
-    for (int i = t; i < C2M * C2CO / 4; i += 512) {
+    for (int i = t; i < C2M * C2CO / 4; i += 256) {
       const float4 x = d[i], y = z[i];
       acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
     }
@@ -158,27 +158,36 @@ __global__ __launch_bounds__(512) void meta_dot_kernel(MetaDotArgs a) {
   {
     const float4* d = reinterpret_cast<const float4*>(a.dy3 + (int64_t)b * FLAT);
     const float4* z = reinterpret_cast<const float4*>(a.zv3 + (int64_t)b * FLAT);
-    for (int i = t; i < FLAT / 4; i += 512) {
+    for (int i = t; i < FLAT / 4; i += 256) {
       const float4 x = d[i], y = z[i];
       acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
     }
   }
-  // fc1: dz1 . (vb1 + sum_s partial)
-  float zf = a.v[a.b1_off + t];
-  for (int s = 0; s < a.S; ++s) zf += a.zvp[((int64_t)s * a.M + b) * HID + t];
-  acc += a.dz1[(int64_t)b * HID + t] * zf;
-  // fc2: gq . (h1 . V2[:, a] + vb2[a])
+  // fc1: dz1 . (vb1 + sum_s partial); fc2: gq . (h1 . V2[:, a] + vb2[a])
   const int act = a.ga[b];
-  float f2 = wave_sum(a.h1[(int64_t)b * HID + t] * a.v[a.w2_off + t * a.A + act]);
+  float f2 = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int n = t + 256 * h;
+    float zf = a.v[a.b1_off + n];
+    for (int s = 0; s < a.S; ++s) zf += a.zvp[((int64_t)s * a.M + b) * HID + n];
+    acc += a.dz1[(int64_t)b * HID + n] * zf;
+    f2 += a.h1[(int64_t)b * HID + n] * a.v[a.w2_off + n * a.A + act];
+  }
+  f2 = wave_sum(f2);
   if ((t & 63) == 0) s_fc2[t >> 6] = f2;
   __syncthreads();
-  if (t == 0) {
-    float z2 = a.v[a.b2_off + act];
-    for (int w = 0; w < 8; ++w) z2 += s_fc2[w];
-    acc += a.gq[b] * z2;
-  }
-  acc = block_sum_f32(acc, sbuf);
-  if (t == 0) a.s_out[b] = acc;
+  if (t == 0) acc += a.gq[b] * (a.v[a.b2_off + act] + ((s_fc2[0] + s_fc2[1]) + (s_fc2[2] + s_fc2[3])));
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) sbuf[t >> 6] = acc;
+  __syncthreads();
+  return (sbuf[0] + sbuf[1]) + (sbuf[2] + sbuf[3]);
+}
+
+// One block (256 threads) per meta-batch sample.
+__global__ __launch_bounds__(256) void meta_dot_kernel(MetaDotArgs a) {
+  const float acc = meta_dot_sample(a, blockIdx.x);
+  if (threadIdx.x == 0) a.s_out[blockIdx.x] = acc;
 }
 
 struct MetaAdamArgs {
@@ -201,11 +210,16 @@ struct MetaAdamArgs {
 };
 
 // softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
-// new logits scattered back.  One block striding over the M entries.
-__global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) {
+// new logits scattered back.  One block striding over the M entries; s is
+// read with agent-scope loads (meta_dot_adam_kernel: other workgroups of the
+// same launch wrote it).
+__device__ __forceinline__ float load_s(const float* s, int i) {
+  return __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __shared__ float sbuf[META_THREADS / 64];
   float st = 0.f;
-  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += a.s[i];
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += load_s(a.s, i);
   const float tot = block_sum_f32(st, sbuf);
   float lp = 0.f;
   for (int j = threadIdx.x; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
@@ -220,7 +234,7 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
   __syncthreads();
   double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
   for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
-    const float g = a.s[i] - a.p[i] * tot;
+    const float g = load_s(a.s, i) - a.p[i] * tot;
     const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
     const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
     const float mh = m / c1;
@@ -259,6 +273,26 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
     *a.count = cnt;
     *a.loss = lp;
   }
+}
+
+__global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) { meta_adam_body(a); }
+
+// meta_dot_kernel + meta_adam_kernel in one launch (one meta chunk): block b
+// publishes s[b] write-through and arrives on `done`; the block that arrives
+// last (every s[i] is then visible at agent scope) runs the Adam step and
+// resets the counter for the next launch.
+__global__ __launch_bounds__(META_THREADS) void meta_dot_adam_kernel(MetaDotArgs d, MetaAdamArgs a, int* done) {
+  __shared__ int s_last;
+  const float acc = meta_dot_sample(d, blockIdx.x);
+  if (threadIdx.x == 0) __hip_atomic_store(d.s_out + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  meta_adam_body(a);
+  if (threadIdx.x == 0) __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace dqz
