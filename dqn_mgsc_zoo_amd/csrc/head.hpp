@@ -25,6 +25,13 @@ struct HeadArgs {
   int per_normalize;
   float* per_w_out;
   const float* meta_p;   // MGSC meta mode: per-sample probabilities or null
+  // MGSC meta mode with the softmax formed here (one meta chunk, M <= 512):
+  // p = softmax(logits[pos[0..M)]) (meta_softmax_kernel's quantity), block b
+  // writes x_out[b] = logits[pos[b]] and p_out[b]; meta_p is then unused
+  const float* meta_logits;
+  const int32_t* meta_pos;
+  int meta_M;
+  float *meta_x_out, *meta_p_out;
   const float4* rec;     // batch records {a, r, d, 0} written by conv1, or null (slot chain)
   uint64_t* advance;     // fused sampler's step counter, advanced once here (or null)
   int unit;              // 1: unit cotangent on q[a] (gradient of q itself; HVP pass)
@@ -147,6 +154,33 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
       if (h.per_w_out) h.per_w_out[b] = wper;
     }
   }
+  if (h.meta_logits) {
+    // p = exp(x - (c + log sum exp(x - c))), c = max x, over the M meta-batch
+    // logits (replay_circular.py:79-86 as meta_softmax_kernel forms it; the
+    // block reductions run in a fixed order)
+    __shared__ float s_mx[8], s_se[8], s_pm;
+    const float x = n < h.meta_M ? h.meta_logits[h.meta_pos[n]] : -INFINITY;
+    float m = x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) s_mx[wave] = m;
+    __syncthreads();
+    float c = s_mx[0];
+#pragma unroll
+    for (int w8 = 1; w8 < 8; ++w8) c = fmaxf(c, s_mx[w8]);
+    const float e = wave_sum(n < h.meta_M ? expf(x - c) : 0.f);
+    if (lane == 0) s_se[wave] = e;
+    __syncthreads();
+    const float se = ((s_se[0] + s_se[1]) + (s_se[2] + s_se[3])) + ((s_se[4] + s_se[5]) + (s_se[6] + s_se[7]));
+    if (n == b) {
+      const float pb = expf(x - (c + logf(se)));
+      s_pm = pb;
+      h.meta_x_out[b] = x;
+      h.meta_p_out[b] = pb;
+    }
+    __syncthreads();
+    pm = s_pm;
+  }
   if (!h.fwd_only && n == 0) {  // second hop of the batch record chain, needed only for the TD
     if (chain) {
       a_tm1 = h.action[slot];
@@ -159,7 +193,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     }
     if (h.weights) w = h.weights[b];
     if (h.per_wb) w = wper;
-    if (h.meta_p) pm = h.meta_p[b];
+    if (h.meta_p && !h.meta_logits) pm = h.meta_p[b];
   }
   DQZ_STAMP(4, 1);
   float hz[ZMAX];
@@ -244,7 +278,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
       float g;
       if (h.unit) {
         g = -1.f;  // gq = d q[a] / d q[a] = 1
-      } else if (h.meta_p) {
+      } else if (h.meta_p || h.meta_logits) {
         // meta mode: p_b * grad of loss_fn on the single transition b
         // (dqn_mgsc_batched/agent.py:152-158): batch of one, clip, then weight.
         g = pm * fminf(fmaxf(td, -h.bound), h.bound);

@@ -331,7 +331,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
                      int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr,
                      const PerSampleArgs* pd = nullptr, const UniformDraw* ahead = nullptr,
-                     const Rms* meta_epi = nullptr) {
+                     const Rms* meta_epi = nullptr, const HeadArgs* meta_sm = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (ahead && (pe.on() || gout || meta_p || draw || sm || pd || wb || L->cfg.algo != DQZ_ALGO_DQN))
     return fail(DQZ_ERR_INVALID, "the target lookahead runs plain DQN learner steps only");
@@ -452,6 +452,13 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     h.per_w_out = pd->out_weights;
   }
   h.meta_p = meta_p;
+  if (meta_sm) {  // the meta batch's softmax formed by the head (one meta chunk)
+    h.meta_logits = meta_sm->meta_logits;
+    h.meta_pos = meta_sm->meta_pos;
+    h.meta_M = meta_sm->meta_M;
+    h.meta_x_out = meta_sm->meta_x_out;
+    h.meta_p_out = meta_sm->meta_p_out;
+  }
   h.rec = reinterpret_cast<const float4*>(L->rec);
   // (the lookahead advances its counter in the update launch instead)
   h.advance = draw ? draw->counter : sm ? sm->counter : pd ? (pd->inj_u ? nullptr : pd->counter) : nullptr;
@@ -1358,10 +1365,15 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
 
   const int C = H->C, K = H->K;
 
-  // p = softmax(logits[pos]); slots padded to K C with slots[M - 1] (p = 0 there)
-  hipLaunchKernelGGL(meta_softmax_kernel, dim3(1 + (unsigned)((K * C + META_THREADS - 1) / META_THREADS)),
-                     dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p, slots, K * C, H->slots_pad);
-  DQZ_HIP(hipGetLastError());
+  // p = softmax(logits[pos]); slots padded to K C with slots[M - 1] (p = 0
+  // there).  One chunk (K C = M): no padding, and the batch learner's head
+  // forms p itself (HeadArgs::meta_logits), so no launch of its own.
+  const int32_t* mslots = K == 1 ? slots : H->slots_pad;
+  if (K > 1) {
+    hipLaunchKernelGGL(meta_softmax_kernel, dim3(1 + (unsigned)((K * C + META_THREADS - 1) / META_THREADS)),
+                       dim3(META_THREADS), 0, st, logits, pos, M, H->x, H->p, slots, K * C, H->slots_pad);
+    DQZ_HIP(hipGetLastError());
+  }
 
   // G = sum_i p_i g_i: batched backwards with p-weighted cotangents, one per
   // chunk of C samples, accumulated in chunk order (deterministic).  With one
@@ -1377,8 +1389,14 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   epi.sq_part = H->loss_part;
   if (K == 1) {
     epi.meta = 1;
-    if (int rc = step_impl(L, P, S, H->slots_pad, nullptr, stream, kNoProfile, so ? H->G : nullptr, H->p, nullptr,
-                           0, 0, nullptr, nullptr, nullptr, nullptr, &epi))
+    HeadArgs msm{};
+    msm.meta_logits = logits;
+    msm.meta_pos = pos;
+    msm.meta_M = M;
+    msm.meta_x_out = H->x;
+    msm.meta_p_out = H->p;
+    if (int rc = step_impl(L, P, S, mslots, nullptr, stream, kNoProfile, so ? H->G : nullptr, H->p, nullptr, 0, 0,
+                           nullptr, nullptr, nullptr, nullptr, &epi, &msm))
       return rc;
     // (the batch learner's td stays current until the next update,
     // dqz_meta_outputs copies it from there)
@@ -1497,7 +1515,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   nv.which[0] = nv.which[1] = nv.which[2] = 0;
   MetaDotArgs md;
   for (int k = 0; k < K; ++k) {
-    const int32_t* ks = H->slots_pad + (int64_t)k * C;
+    const int32_t* ks = mslots + (int64_t)k * C;
     if (K > 1) {
       if (int rc = step_impl(L, P, S, ks, nullptr, stream, kNoProfile, H->Gs, H->p + (int64_t)k * C)) return rc;
     }
