@@ -361,9 +361,6 @@ def parse_args(argv=None):
                        'replays (the first kernels start without waiting '
                        'for a graph submission)')
   ap.add_argument('--target-period', type=int, default=2500)
-  ap.add_argument('--lookahead', type=int, default=1,
-                  help='dqn: run the target forward of the next batch inside '
-                       'the current step (dqz_learner_step_uniform_ahead)')
   ap.add_argument('--stats-every', type=int, default=1000)
   ap.add_argument('--profile-iters', type=int, default=100)
   ap.add_argument('--cpu-seconds', type=float, default=20.0)
@@ -491,7 +488,7 @@ class Workload:
   `one_step()` (everything a step launches, capturable in a hipGraph) and
   the sampler launches to time apart from the learner phases."""
 
-  def __init__(self, algo, capacity, rank, dev, lookahead=True):
+  def __init__(self, algo, capacity, rank, dev):
     from dqn_mgsc_zoo_amd import _native  # pylint: disable=g-import-not-at-top
     from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
     from dqn_mgsc_zoo_amd import networks  # pylint: disable=g-import-not-at-top
@@ -513,22 +510,7 @@ class Workload:
     self.samplers = {}  # name -> launch fn (timed apart, HIP events)
     self.sampler_bytes = {}  # name -> algorithmic bytes per launch
 
-    self.sync_target = lrn.sync_target
-    if algo == 'dqn' and lookahead:
-      def one_step():
-        # FIFO replay full: live ids [t - size, t) = slots [0, capacity).
-        # The uniform draw is fused into the step's conv1 kernel; the target
-        # network's forward of the next step's batch runs inside this step's
-        # fc1 / fc1 dX / update launches (ahead.hpp).
-        lrn.step_uniform_ahead(store, 0, capacity, capacity, seed, counter, slots)
-
-      def sync_target():
-        # dqn/agent.py:155-156, then the lookahead of the next batch under the
-        # new target (the captured graphs start from a current lookahead)
-        lrn.sync_target()
-        lrn.prime_ahead(store, 0, capacity, capacity, seed, counter)
-      self.sync_target = sync_target
-    elif algo in ('dqn', 'double'):
+    if algo in ('dqn', 'double'):
       def one_step():
         # FIFO replay full: live ids [t - size, t) = slots [0, capacity).
         # The uniform draw is fused into the step's conv1 kernel.
@@ -674,7 +656,7 @@ def run_gpu(args, g, rem):
   dev = torch.device('cuda', local_rank)
 
   algo = args.algo
-  wl = Workload(algo, args.capacity, rank, dev, lookahead=bool(args.lookahead))
+  wl = Workload(algo, args.capacity, rank, dev)
   lrn, store, slots, one_step = wl.lrn, wl.store, wl.slots, wl.one_step
 
   graphs = {}
@@ -734,7 +716,7 @@ def run_gpu(args, g, rem):
                                                     async_op=True))
     pending[-1].wait()
 
-  runner = StepRunner(one_step, graphs, args.target_period, wl.sync_target,
+  runner = StepRunner(one_step, graphs, args.target_period, lrn.sync_target,
                       args.stats_every, on_stats)
   runner.run(args.warmup, 1, 0)
   for k in graphs:  # first replays of each graph upload it: keep them untimed
@@ -859,9 +841,6 @@ def run_gpu(args, g, rem):
       # learner health word (dqz_learner_sync_status): bit 0 a hand-off wait
       # gave up, bit 1 a step's mean loss was not finite
       'handoff_status': int(max(status_max, status_after)) & 1,
-      # bit 2: a lookahead step ran on a stale lookahead (never expected)
-      'stale_lookahead': bool(int(max(status_max, status_after)) & 4),
-      'lookahead': bool(args.lookahead) and algo == 'dqn',
       'nonfinite_loss': bool(int(max(status_max, status_after)) & 2),
       'fill_s': round(wl.fill_s, 2),
       'last_loss': float(loss.item()),
@@ -891,7 +870,7 @@ def run_gpu(args, g, rem):
     out['cpu_baseline'] = None
   print(json.dumps(out), file=json_out, flush=True)
   reps.close()
-  if out['handoff_status'] != 0 or out['nonfinite_loss'] or out['stale_lookahead'] or not finite:
+  if out['handoff_status'] != 0 or out['nonfinite_loss'] or not finite:
     print('bench.py: hand-off status %d, non-finite loss %s, params finite %s: '
           'the timed steps are invalid' % (out['handoff_status'], out['nonfinite_loss'],
                                            finite), file=sys.stderr)

@@ -151,17 +151,6 @@ SIGNATURES = {
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _i64, _i64,
          _i64, ctypes.c_uint64, _vp, _vp, _vp],
     ),
-    'dqz_learner_step_uniform_ahead': (
-        _int,
-        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _i64, _i64,
-         _i64, ctypes.c_uint64, _vp, _vp, _vp],
-    ),
-    'dqz_learner_ahead_invalidate': (_int, [_vp, _vp]),
-    'dqz_learner_ahead_prime': (
-        _int,
-        [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _i64, _i64,
-         _i64, ctypes.c_uint64, _vp, _vp],
-    ),
     'dqz_learner_step_per': (
         _int,
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp, _vp,

@@ -282,10 +282,6 @@ struct UniformDraw {
   uint64_t seed;
   uint64_t* counter;  // device step counter (read by the sampling kernel, advanced later)
   int32_t* slots_out;
-  int ctr_offset;     // draws are those of step *counter + ctr_offset (1: the next
-                      // step's batch, drawn ahead by the target lookahead)
-  const int* ahead_ok;  // lookahead consumers (Conv1Src::fused == 4): the device word
-  int* err;             // saying the lookahead is current, and the health word (bit 2)
 };
 
 __device__ __forceinline__ int32_t uniform_slot(uint64_t ctr, int i, const UniformDraw& d) {

@@ -21,9 +21,7 @@ struct Conv1Src {
   const uint8_t* states;  // direct uint8 [B][84][84][4] input, or null
   int fused;              // 1: slots come from the fused uniform sampler `draw`;
                           // 2: from the fused learned-logit draw `sm`;
-                          // 3: from the fused prioritized draw `per`;
-                          // 4: from `slots` (drawn ahead by the previous step's
-                          //    target lookahead), published to draw.slots_out
+                          // 3: from the fused prioritized draw `per`
   union {                 // one draw per launch: the kernel argument stays small
     UniformDraw draw;
     SoftmaxDraw sm;
@@ -131,17 +129,8 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
     int slot;
     double per_prob = 0.0;  // F == 3: the draw's probability (thread 0)
     if constexpr (F == 1) {  // fused sampler: draw b of this step; block (0, b, 0) publishes it
-      slot = uniform_slot(*src.draw.counter + (uint64_t)src.draw.ctr_offset, b, src.draw);
+      slot = uniform_slot(*src.draw.counter, b, src.draw);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.draw.slots_out[b] = slot;
-    } else if constexpr (F == 4) {  // drawn ahead: read, and publish as this step's batch
-      slot = src.slots[b];
-      if (threadIdx.x == 0 && rb == 0 && z == 0) {
-        src.draw.slots_out[b] = slot;
-        // a lookahead that was invalidated and never recomputed (a captured
-        // graph replayed after a target sync without dqz_learner_ahead_prime)
-        if (b == 0 && __hip_atomic_load(src.draw.ahead_ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-          __hip_atomic_fetch_or(src.draw.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     } else if constexpr (F == 2) {  // fused learned-logit draw (every block of b runs the search)
       slot = softmax_draw_slot(src.sm, b);
       if (threadIdx.x == 0 && rb == 0 && z == 0) src.sm.slots_out[b] = slot;
@@ -293,7 +282,6 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
   if (!sj.valid) return;
   switch (a.src.fused) {  // the stand-alone conv1 launch (profile / debug layouts)
     case 1: conv1_fwd_body<false, 1>(a, smem, sj); break;
-    case 4: conv1_fwd_body<false, 4>(a, smem, sj); break;
     case 2: conv1_fwd_body<false, 2>(a, smem, sj); break;
     case 3: conv1_fwd_body<false, 3>(a, smem, sj); break;
     default: conv1_fwd_body<false, 0>(a, smem, sj); break;

@@ -27,7 +27,6 @@
 #include "meta.hpp"
 #include "hvp.hpp"
 #include "sampling.hpp"
-#include "ahead.hpp"
 #include "preprocess.hpp"
 
 namespace dqz {
@@ -59,23 +58,8 @@ struct dqz_learner {
   float *y1, *y2, *y3, *fc1p, *h1, *q, *dz1, *dy3, *dy2, *dy1, *p1, *p2, *p3, *td, *loss, *loss_part, *gq, *rec;
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
-  int32_t* slots_next;  // [B] the next batch, drawn by the target lookahead (ahead.hpp)
-  // The target lookahead's inputs: the next step's target forward in the
-  // y[1] sections and slots_next is valid only for these (and only while the
-  // replay contents and theta- are unchanged: callers invalidate otherwise).
-  struct AheadKey {
-    const void *frames, *fidx, *target, *counter;
-    int64_t base, size, capacity;
-    uint64_t seed;
-    bool operator==(const AheadKey& o) const {
-      return frames == o.frames && fidx == o.fidx && target == o.target && counter == o.counter &&
-             base == o.base && size == o.size && capacity == o.capacity && seed == o.seed;
-    }
-  } ahead_key{};
-  bool ahead_valid = false;
   int32_t* ga;
-  int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err,
-                  // then (one line on) the lookahead-current word
+  int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
@@ -88,8 +72,7 @@ static int init_kernel_attrs() {
                               (int)kConv1FwdSmem));
   const void* fwd_kernels[] = {(const void*)fwd_conv_kernel<0>, (const void*)fwd_conv_kernel<1>,
                                (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>,
-                               (const void*)fwd_conv_kernel<4>,
-                               (const void*)tangent_fwd_kernel, (const void*)fc1_ahead_kernel};
+                               (const void*)tangent_fwd_kernel};
   for (const void* k : fwd_kernels)
     DQZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kConv1FwdSmem));
   g_attr_done = 1;
@@ -136,11 +119,11 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
                            n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
-                           2 * (int64_t)B, B};
+                           2 * (int64_t)B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
                     &L->gq,  reinterpret_cast<float**>(&L->ga), &L->rec, reinterpret_cast<float**>(&L->sync), &L->w3p, &L->w2p,
-                    reinterpret_cast<float**>(&L->per_wb), reinterpret_cast<float**>(&L->slots_next)};
+                    reinterpret_cast<float**>(&L->per_wb)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "scratch table");
   int64_t total = 0;
   for (int64_t s : sizes) total += (s + 63) / 64 * 64;
@@ -209,10 +192,8 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
 // fused_conv: conv1 -> conv2 -> conv3 as one hand-off launch (fwd_conv_kernel),
 // used by the learner step (since conv1 runs on bf16 MFMA: 15,590 -> 16,050
 // steps/s; with the f32-MFMA conv1 it had measured 1.5 % slower) and the actor.
-// zoff: the first activation section written (1: the target lookahead's
-// prime writes the target copy's y[1] sections); with_fc1: also launch fc1.
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
-                        PhaseEvents pe, bool fused_conv, int zoff = 0, bool with_fc1 = true) {
+                        PhaseEvents pe, bool fused_conv) {
   Conv1FwdArgs c1;
   c1.src = src;
   c1.nz = nz;
@@ -221,23 +202,23 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.B = B;
   c1.Z = Z;
   c1.linear = 0;
-  c1.out = L->y1 + (int64_t)zoff * B * C1M * C1CO;
+  c1.out = L->y1;
 
   LayerFwdArgs c2;
-  c2.in = c1.out;
+  c2.in = L->y1;
   c2.nz = nz;
   c2.w_off = L->off[2];
   c2.b_off = L->off[3];
   c2.B = B;
   c2.Z = Z;
   c2.linear = 0;
-  c2.out = L->y2 + (int64_t)zoff * B * C2M * C2CO;
+  c2.out = L->y2;
 
   LayerFwdArgs c3 = c2;
-  c3.in = c2.out;
+  c3.in = L->y2;
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
-  c3.out = L->y3 + (int64_t)zoff * B * FLAT;
+  c3.out = L->y3;
   if (fused_conv) {
     // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample.  The
     // word layout follows the learner's configured batch, not this call's n
@@ -253,7 +234,6 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
     const dim3 grid(3 * xcd_grid(4, Z * B).x);
     DQZ_PHASE(0, switch (src.fused) {
       case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
-      case 4: hipLaunchKernelGGL(fwd_conv_kernel<4>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
       case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
       case 3: hipLaunchKernelGGL(fwd_conv_kernel<3>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
       default: hipLaunchKernelGGL(fwd_conv_kernel<0>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
@@ -268,7 +248,6 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
               DQZ_HIP(hipGetLastError()));
   }
 
-  if (!with_fc1) return DQZ_OK;
   Fc1FwdArgs f1;
   f1.in = L->y3;
   f1.nz = nz;
@@ -300,28 +279,6 @@ static HeadArgs make_head(dqz_learner* L, const NetZ& nz, int Z, int B) {
   return h;
 }
 
-// The device word saying the target lookahead is current (1) or was
-// invalidated (0): a lookahead step that finds 0 sets bit 2 of the health word.
-static int* ahead_ok_word(dqz_learner* L) { return L->sync + (16 * L->cfg.batch + 1) * Handoff::kStride; }
-
-// The target lookahead's prime: the target forward of THIS step's batch
-// (draws of the current counter) into the y[1] sections and slots_next.
-static int ahead_prime(dqz_learner* L, const dqz_params* P, const dqz_store* S, const UniformDraw& d,
-                       hipStream_t st) {
-  NetZ tz;
-  for (int z = 0; z < 3; ++z) {
-    tz.p[z] = P->target;
-    tz.which[z] = 1;
-  }
-  Conv1Src psrc{S->frames, S->fidx, nullptr, nullptr, 1, UniformDraw{}};
-  psrc.draw = d;
-  psrc.draw.slots_out = L->slots_next;
-  psrc.draw.ctr_offset = 0;
-  if (int rc = forward_impl(L, tz, 1, L->cfg.batch, psrc, st, kNoProfile, true, 1, false)) return rc;
-  DQZ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ahead_ok_word(L)), 1, 1, st));
-  return DQZ_OK;
-}
-
 // One learner step.  gout == null: centered RMSProp on P->online/mu/nu.
 // gout != null: gradient-output mode — the full gradient is written to gout
 // (dqz parameter layout) and P->online/mu/nu are left untouched.
@@ -330,11 +287,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
                      const float* is_weights, void* stream, PhaseEvents pe, float* gout = nullptr,
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
                      int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr,
-                     const PerSampleArgs* pd = nullptr, const UniformDraw* ahead = nullptr,
-                     const Rms* meta_epi = nullptr, const HeadArgs* meta_sm = nullptr) {
+                     const PerSampleArgs* pd = nullptr, const Rms* meta_epi = nullptr,
+                     const HeadArgs* meta_sm = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
-  if (ahead && (pe.on() || gout || meta_p || draw || sm || pd || wb || L->cfg.algo != DQZ_ALGO_DQN))
-    return fail(DQZ_ERR_INVALID, "the target lookahead runs plain DQN learner steps only");
   if (!gout && !meta_epi && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (meta_epi && meta_epi->meta == 1 && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (int rc = check_store(S)) return rc;
@@ -353,55 +308,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   src.reward = S->reward;
   src.discount = S->discount;
   src.rec = reinterpret_cast<float4*>(L->rec);
-  // the target copy of the lookahead (ahead.hpp): target params on s_t
-  NetZ tz;
-  for (int z = 0; z < 3; ++z) {
-    tz.p[z] = P->target;
-    tz.which[z] = 1;
-  }
-  const dqz_learner::AheadKey key = ahead ? dqz_learner::AheadKey{S->frames, S->fidx, P->target, ahead->counter,
-                                                                  ahead->base, ahead->size, ahead->capacity,
-                                                                  ahead->seed}
-                                          : dqz_learner::AheadKey{};
-  const bool primed = ahead && L->ahead_valid && L->ahead_key == key;
-  L->ahead_valid = false;  // any other step overwrites the y[1] sections it relies on
-  if (ahead) {
-    if (!primed)
-      if (int rc = ahead_prime(L, P, S, *ahead, st)) return rc;
-    // the online copy only: conv1 reads the slots drawn ahead and publishes them
-    Conv1Src fsrc = src;
-    fsrc.fused = 4;
-    fsrc.slots = L->slots_next;
-    fsrc.draw = *ahead;
-    fsrc.draw.ahead_ok = ahead_ok_word(L);
-    fsrc.draw.err = L->sync + 16 * B * Handoff::kStride;
-    if (int rc = forward_impl(L, nz, 1, B, fsrc, st, pe, true, 0, false)) return rc;
-    // fc1 of both copies + conv1 of the next batch's target copy
-    Fc1FwdArgs f1;
-    f1.in = L->y3;
-    f1.nz = nz;
-    f1.w_off = L->off[6];
-    f1.B = B;
-    f1.MG = (B + 31) / 32;
-    f1.part = L->fc1p;
-    const int nf = fc1_fwd_blocks(Z, f1.MG);
-    Conv1FwdArgs a1;
-    a1.src = Conv1Src{S->frames, S->fidx, nullptr, nullptr, 1, UniformDraw{}};
-    a1.src.draw = *ahead;
-    a1.src.draw.slots_out = L->slots_next;
-    a1.src.draw.ctr_offset = 1;
-    a1.nz = tz;
-    a1.w_off = L->off[0];
-    a1.b_off = L->off[1];
-    a1.B = B;
-    a1.Z = 1;
-    a1.linear = 0;
-    a1.out = L->y1 + (int64_t)B * C1M * C1CO;
-    a1.pub = Handoff{};
-    hipLaunchKernelGGL(fc1_ahead_kernel, dim3(nf + xcd_grid(C1_BLOCKS, B).x), dim3(256), kConv1FwdSmem, st, f1, nf,
-                       a1);
-    DQZ_HIP(hipGetLastError());
-  } else if (draw || sm || pd) {  // conv1 draws the batch itself; later kernels read the published slots
+  if (draw || sm || pd) {  // conv1 draws the batch itself; later kernels read the published slots
     Conv1Src fsrc = src;
     if (draw) {
       fsrc.fused = 1;
@@ -460,7 +367,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     h.meta_p_out = meta_sm->meta_p_out;
   }
   h.rec = reinterpret_cast<const float4*>(L->rec);
-  // (the lookahead advances its counter in the update launch instead)
   h.advance = draw ? draw->counter : sm ? sm->counter : pd ? (pd->inj_u ? nullptr : pd->counter) : nullptr;
   h.unit = unit;
   h.bound = L->cfg.grad_error_bound;
@@ -487,23 +393,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
   DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
-  LayerFwdArgs a2;  // the lookahead's conv2 / conv3 (target copy, y[1] sections)
-  a2.nz = tz;
-  a2.B = B;
-  a2.Z = 1;
-  a2.linear = 0;
-  a2.wait = a2.pub = Handoff{};
-  if (ahead) {
-    a2.in = L->y1 + (int64_t)B * C1M * C1CO;
-    a2.w_off = L->off[2];
-    a2.b_off = L->off[3];
-    a2.out = L->y2 + (int64_t)B * C2M * C2CO;
-    hipLaunchKernelGGL(fc1_dx_ahead_kernel, dim3(pad8(FC1X_BLOCKS) + xcd_grid(4, B).x), dim3(256), 0, st, fb, a2);
-    DQZ_HIP(hipGetLastError());
-  } else {
-    DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FC1X_BLOCKS), dim3(256), 0, st, fb);
-              DQZ_HIP(hipGetLastError()));
-  }
+  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+            DQZ_HIP(hipGetLastError()));
 
   Conv3BwdArgs c3b;
   c3b.dy3 = L->dy3;
@@ -576,21 +467,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.rms = rms;
   u.rms.sq_off = 4 * (FLAT / 16);  // meta_rms2 partials: the fc1 dW blocks' first, then the update's
   const unsigned nblk = update_blocks(L->sz, A, u.nb2);
-  if (ahead) {
-    LayerFwdArgs a3 = a2;
-    a3.in = L->y2 + (int64_t)B * C2M * C2CO;
-    a3.w_off = L->off[4];
-    a3.b_off = L->off[5];
-    a3.out = L->y3 + (int64_t)B * FLAT;
-    hipLaunchKernelGGL(update_ahead_kernel, dim3(pad8((int)nblk) + xcd_grid(4, B).x), dim3(256), 0, st, u, (int)nblk,
-                       a3, ahead->counter);
-    DQZ_HIP(hipGetLastError());
-    L->ahead_key = key;
-    L->ahead_valid = true;
-  } else {
-    DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
-              DQZ_HIP(hipGetLastError()));
-  }
+  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
+            DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
 
@@ -621,39 +499,6 @@ int dqz_learner_step_uniform(dqz_learner* L, const dqz_params* P, const dqz_stor
   if (L && L->cfg.algo == DQZ_ALGO_PER) return fail(DQZ_ERR_INVALID, "PER samples by priority, not uniformly");
   const UniformDraw d{base % capacity, size, capacity, seed, counter_dev, slots_out};
   return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, &d);
-}
-
-int dqz_learner_step_uniform_ahead(dqz_learner* L, const dqz_params* P, const dqz_store* S, int64_t base,
-                                   int64_t size, int64_t capacity, uint64_t seed, uint64_t* counter_dev,
-                                   int32_t* slots_out, void* stream) {
-  if (!L || !counter_dev || !slots_out) return fail(DQZ_ERR_INVALID, "null argument");
-  if (size < 1) return fail(DQZ_ERR_INVALID, "cannot sample from an empty replay (size=%lld)", (long long)size);
-  if (capacity < size || base < 0) return fail(DQZ_ERR_INVALID, "bad replay geometry");
-  if (L->cfg.algo != DQZ_ALGO_DQN) return fail(DQZ_ERR_INVALID, "the target lookahead runs DQN learners only");
-  const UniformDraw d{base % capacity, size, capacity, seed, counter_dev, slots_out};
-  return step_impl(L, P, S, slots_out, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr,
-                   nullptr, &d);
-}
-
-int dqz_learner_ahead_invalidate(dqz_learner* L, void* stream) {
-  if (!L) return fail(DQZ_ERR_INVALID, "null learner");
-  L->ahead_valid = false;
-  DQZ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ahead_ok_word(L)), 0, 1, (hipStream_t)stream));
-  return DQZ_OK;
-}
-
-int dqz_learner_ahead_prime(dqz_learner* L, const dqz_params* P, const dqz_store* S, int64_t base, int64_t size,
-                            int64_t capacity, uint64_t seed, uint64_t* counter_dev, void* stream) {
-  if (!L || !P || !P->target || !counter_dev) return fail(DQZ_ERR_INVALID, "null argument");
-  if (int rc = check_store(S)) return rc;
-  if (size < 1) return fail(DQZ_ERR_INVALID, "cannot sample from an empty replay (size=%lld)", (long long)size);
-  if (capacity < size || base < 0) return fail(DQZ_ERR_INVALID, "bad replay geometry");
-  if (L->cfg.algo != DQZ_ALGO_DQN) return fail(DQZ_ERR_INVALID, "the target lookahead runs DQN learners only");
-  const UniformDraw d{base % capacity, size, capacity, seed, counter_dev, nullptr};
-  if (int rc = ahead_prime(L, P, S, d, (hipStream_t)stream)) return rc;
-  L->ahead_key = dqz_learner::AheadKey{S->frames, S->fidx, P->target, counter_dev, d.base, size, capacity, seed};
-  L->ahead_valid = true;
-  return DQZ_OK;
 }
 
 int dqz_learner_grad(dqz_learner* L, const dqz_params* P, const dqz_store* S, const int32_t* slots,
@@ -687,7 +532,6 @@ int dqz_learner_sync_status(dqz_learner* L, int* status) {
     // the steps since the previous check as invalid.
     DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
     DQZ_HIP(hipDeviceSynchronize());
-    L->ahead_valid = false;  // the clear also marked the lookahead stale on the device
   }
   return DQZ_OK;
 }
@@ -1396,7 +1240,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     msm.meta_x_out = H->x;
     msm.meta_p_out = H->p;
     if (int rc = step_impl(L, P, S, mslots, nullptr, stream, kNoProfile, so ? H->G : nullptr, H->p, nullptr, 0, 0,
-                           nullptr, nullptr, nullptr, nullptr, &epi, &msm))
+                           nullptr, nullptr, nullptr, &epi, &msm))
       return rc;
     // (the batch learner's td stays current until the next update,
     // dqz_meta_outputs copies it from there)
@@ -1438,7 +1282,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     epi.meta = 2;
     epi.vout = H->G;
     if (int rc = step_impl(H->l1, &P1, S1, online_slot, nullptr, stream, kNoProfile, nullptr, nullptr, nullptr, 0, 0,
-                           nullptr, nullptr, nullptr, nullptr, &epi))
+                           nullptr, nullptr, nullptr, &epi))
       return rc;
     v = H->G;
     nloss = 4 * (FLAT / 16) + (int)update_blocks(H->l1->sz, A, H->l1->shared_bias ? 1 : A);

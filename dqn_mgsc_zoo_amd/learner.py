@@ -85,7 +85,6 @@ class Learner:
   # -- state -------------------------------------------------------------
 
   def set_params(self, tree, target_tree=None):
-    self.invalidate_ahead()
     flat = torch.from_numpy(self.network.flatten(tree))
     self.online.copy_(flat)
     if target_tree is None:
@@ -107,7 +106,6 @@ class Learner:
     _native.check(_native.lib().dqz_target_copy(
         _native.ptr(self.target), _native.ptr(self.online), self.total,
         _native.stream_handle(stream)))
-    self.invalidate_ahead(stream)
 
   # -- hot path ------------------------------------------------------------
 
@@ -146,38 +144,6 @@ class Learner:
         self._h, ctypes.byref(self._params_c), store.c_ref(), int(base),
         int(size), int(capacity), int(seed) & (2**64 - 1), _native.ptr(counter),
         _native.ptr(slots_out), _native.stream_handle(stream)))
-
-  def step_uniform_ahead(self, store, base, size, capacity, seed, counter,
-                         slots_out, stream=None):
-    """step_uniform with the target lookahead (dqz_learner_step_uniform_ahead):
-    the same results bit for bit; the target network's forward of the next
-    step's batch runs inside this step's fc1 / fc1 dX / update launches.
-    For learner-only loops over an unchanged replay: call
-    `invalidate_ahead()` after changing the replay contents (sync_target and
-    set_params do it themselves)."""
-    if self.algo != 'dqn':
-      raise ValueError('the target lookahead runs DQN learners only')
-    if slots_out.dtype != torch.int32 or slots_out.numel() != self.batch_size:
-      raise ValueError('slots_out must be a device int32 tensor of batch size')
-    _native.check(_native.lib().dqz_learner_step_uniform_ahead(
-        self._h, ctypes.byref(self._params_c), store.c_ref(), int(base),
-        int(size), int(capacity), int(seed) & (2**64 - 1), _native.ptr(counter),
-        _native.ptr(slots_out), _native.stream_handle(stream)))
-
-  def invalidate_ahead(self, stream=None):
-    """Drops the target lookahead (dqz_learner_ahead_invalidate)."""
-    _native.check(_native.lib().dqz_learner_ahead_invalidate(
-        self._h, _native.stream_handle(stream)))
-
-  def prime_ahead(self, store, base, size, capacity, seed, counter,
-                  stream=None):
-    """Recomputes the lookahead for the next ahead step with these arguments
-    (dqz_learner_ahead_prime): run after a target sync when the ahead steps
-    are replayed from a captured graph."""
-    _native.check(_native.lib().dqz_learner_ahead_prime(
-        self._h, ctypes.byref(self._params_c), store.c_ref(), int(base),
-        int(size), int(capacity), int(seed) & (2**64 - 1), _native.ptr(counter),
-        _native.stream_handle(stream)))
 
   def step_logits(self, store, logit_buffer, slots_out, seed=0, counter=None,
                   uniforms=None, stream=None):

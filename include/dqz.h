@@ -132,35 +132,6 @@ int dqz_learner_step_uniform(dqz_learner* learner, const dqz_params* params, con
                              int64_t base, int64_t size, int64_t capacity, uint64_t seed,
                              uint64_t* counter_dev, int32_t* slots_out, void* stream);
 
-/* dqz_learner_step_uniform with the target lookahead (DQN learners only):
- * the same results bit for bit (slots_out, params, moments, q / td / loss,
- * counter), but the target network's forward of the NEXT step's batch
- * (drawn at *counter_dev + 1) runs inside this step's fc1, fc1 dX and update
- * launches, so the next call's forward launch carries only the online copy.
- * A call whose (store, target params, base, size, capacity, seed,
- * counter_dev) differ from the previous lookahead call's — or the first
- * call, or any call after another step on this learner — first computes the
- * lookahead for its own batch (one extra launch).  The caller must call
- * dqz_learner_ahead_invalidate after changing the replay contents or the
- * target params (a target sync) between calls.  For learner-only loops
- * over an unchanged replay (BASELINE config 2); replaces the jitted
- * `update` + `replay.sample` pair of dqn/agent.py:109-119,147-153. */
-int dqz_learner_step_uniform_ahead(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
-                                   int64_t base, int64_t size, int64_t capacity, uint64_t seed,
-                                   uint64_t* counter_dev, int32_t* slots_out, void* stream);
-/* Drops the lookahead (the next ahead call recomputes it), and marks it
- * stale on the device in stream order: a lookahead step that runs while it
- * is stale — a hipGraph of ahead steps replayed after a target sync without
- * a prime — sets bit 2 of dqz_learner_sync_status. */
-int dqz_learner_ahead_invalidate(dqz_learner* learner, void* stream);
-/* Computes the lookahead for the batch the next ahead step with these
- * arguments will draw (the target forward of the draws of *counter_dev),
- * outside any step: what a loop replaying captured ahead steps runs after a
- * target sync. */
-int dqz_learner_ahead_prime(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
-                            int64_t base, int64_t size, int64_t capacity, uint64_t seed,
-                            uint64_t* counter_dev, void* stream);
-
 /* PER learner step with the priority write-back folded in
  * (prioritized/agent.py:187-206): dqz_learner_step on `slots` with the IS
  * weights, then — inside the same backward launch, in its first workgroup,

@@ -243,70 +243,6 @@ def test_fused_uniform_step_matches_sample_then_step(device):
     assert torch.equal(getattr(lrn, which), getattr(lrn2, which))
 
 
-@pytest.mark.parametrize('batch', [32, 20])
-def test_target_lookahead_steps_equal_plain_steps(device, batch):
-  """dqz_learner_step_uniform_ahead == dqz_learner_step_uniform, bit for bit,
-  over a sequence that exercises every lookahead transition: the first call
-  (prime), steady ahead steps, a target sync between steps (invalidated:
-  re-prime), a plain step in between (invalidated), a changed replay window
-  (key mismatch: re-prime), and ahead steps captured in a hipGraph and
-  replayed.  Slots, q / td / loss of every step, the counter and the final
-  online / target / mu / nu must match exactly."""
-  _, ref, st, _, _, _, _, _ = _setup('dqn', batch, seed=21)
-  _, lrn, _, _, _, _, _, _ = _setup('dqn', batch, seed=21)
-  c1 = torch.zeros((1,), dtype=torch.int64, device=device)
-  c2 = torch.zeros((1,), dtype=torch.int64, device=device)
-  s1 = torch.zeros((batch,), dtype=torch.int32, device=device)
-  s2 = torch.zeros((batch,), dtype=torch.int32, device=device)
-
-  def check(tag):
-    torch.cuda.synchronize()
-    assert torch.equal(s1, s2), tag
-    q1, td1, l1 = [t.clone() for t in ref.fetch_outputs()]
-    q2, td2, l2 = lrn.fetch_outputs()
-    assert torch.equal(q1, q2) and torch.equal(td1, td2) and torch.equal(l1, l2), tag
-    assert int(c1.item()) == int(c2.item()), tag
-
-  def both(base, size, k, seed=5):
-    for i in range(k):
-      ref.step_uniform(st, base, size, st.capacity, seed, c1, s1)
-      lrn.step_uniform_ahead(st, base, size, st.capacity, seed, c2, s2)
-      check('step %d of %d (base %d)' % (i, k, base))
-
-  both(3, 200, 7)
-  ref.sync_target()
-  lrn.sync_target()
-  both(3, 200, 4)
-  ref.step_uniform(st, 3, 200, st.capacity, 5, c1, s1)  # a plain step on both
-  lrn.step_uniform(st, 3, 200, st.capacity, 5, c2, s2)
-  check('plain')
-  both(3, 200, 3)
-  both(40, 150, 3)  # another replay window
-  # ahead steps inside a captured graph, replayed twice
-  g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-  side = torch.cuda.Stream()
-  side.wait_stream(torch.cuda.current_stream())
-  with torch.cuda.stream(side):
-    ref.step_uniform(st, 40, 150, st.capacity, 5, c1, s1)
-    lrn.step_uniform_ahead(st, 40, 150, st.capacity, 5, c2, s2)
-  torch.cuda.current_stream().wait_stream(side)
-  check('before capture')
-  with torch.cuda.graph(g1):
-    for _ in range(5):
-      ref.step_uniform(st, 40, 150, st.capacity, 5, c1, s1)
-  with torch.cuda.graph(g2):
-    for _ in range(5):
-      lrn.step_uniform_ahead(st, 40, 150, st.capacity, 5, c2, s2)
-  for r in range(2):
-    g1.replay()
-    g2.replay()
-    check('replay %d' % r)
-  assert int(c1.item()) == 7 + 4 + 1 + 3 + 3 + 1 + 10
-  for which in ('online', 'target', 'mu', 'nu'):
-    assert torch.equal(getattr(ref, which), getattr(lrn, which)), which
-  assert lrn.sync_status() == 0
-
-
 @pytest.mark.parametrize('algo,batch,num_actions', [
     ('dqn', 1, 6), ('dqn', 20, 18), ('double', 48, 4), ('per', 40, 18)])
 def test_learner_step_odd_shapes(device, algo, batch, num_actions):
