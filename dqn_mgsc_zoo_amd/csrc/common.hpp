@@ -74,6 +74,17 @@ __device__ __forceinline__ float u8n(unsigned v) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
+// MGSC tangent forward with the meta-update's dot products in its epilogues
+// (meta.hpp): instead of storing V * y + vb, a block adds <output, dy> over
+// the outputs it owns and writes one partial at part[b * META_DOT_SLOTS +
+// slot].  part == null: the outputs are stored as usual.
+constexpr int META_DOT_SLOTS = 128;
+struct TangentDot {
+  const float* dy;  // the layer's p-weighted pre-activation gradients, laid out as its output
+  float* part;      // [M][META_DOT_SLOTS]
+  int slot0;        // the layer's first slot
+};
+
 struct NetZ {
   const float* p[3];  // parameter buffer of network copy z
   int which[3];       // input stack of copy z: 0 = s_tm1, 1 = s_t
@@ -169,6 +180,17 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<0x142, 0xa>(v);
   v += dpp_f<0x143, 0xc>(v);
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+// Sum of a 256-thread block's values v (wave sums in a fixed order),
+// deterministic, result in every thread.  s: 4 floats of LDS.
+__device__ __forceinline__ float block_sum256(float v, float* s) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  return r;
 }
 
 // Philox4x32-10 (Salmon et al., SC'11).

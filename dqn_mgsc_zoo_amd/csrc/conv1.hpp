@@ -44,6 +44,7 @@ struct Conv1FwdArgs {
   int linear;  // 1: write the pre-activation (no ReLU)
   float* out;  // y1 [Z][B][400][32]
   Handoff pub;  // PUB: y1 rows handed to conv2 in the same launch (fwd_conv_kernel)
+  TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: dot products instead of stores (part != null)
 };
 
 // bf16 operand fragments of v_mfma_f32_32x32x16_bf16
@@ -253,6 +254,9 @@ __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* sme
   // (fields read once: inside the store loop they could alias `out`)
   float* out = a.out + (((int64_t)z * a.B + b) * C1M + rb * C1_POS) * C1CO;
   const bool linear = a.linear;
+  const bool dot = a.dot.part != nullptr;
+  const float* dyp = a.dot.dy + (((int64_t)z * a.B + b) * C1M + rb * C1_POS) * C1CO;
+  float dacc = 0.f;
   constexpr int PL = C1_POS * C1_RLD;
   for (int i = threadIdx.x; i < C1_POS * C1CO / 4; i += 256) {
     const int o = (i >> 3) * C1_RLD + 4 * c4;
@@ -268,12 +272,21 @@ __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* sme
       const float y = div255(sum[e]) + bb[e];
       v[e] = linear ? y : relu(y);
     }
-    if constexpr (PUB)
+    if constexpr (PUB) {
       store_sc1_f4(out, C1_POS * C1CO * 4, 16 * i, v);
-    else
+    } else if (dot) {
+      const f32x4 d = *reinterpret_cast<const f32x4*>(dyp + 4 * i);
+      dacc += ((v[0] * d[0] + v[1] * d[1]) + (v[2] * d[2] + v[3] * d[3]));
+    } else {
       *reinterpret_cast<f32x4*>(out + 4 * i) = v;
+    }
   }
   if constexpr (PUB) a.pub.arrive(sj.s);
+  if (!PUB && dot) {
+    __syncthreads();  // every thread is past its partial-row reads: smem is free
+    const float r = block_sum256(dacc, smem);
+    if (threadIdx.x == 0) a.dot.part[(int64_t)b * META_DOT_SLOTS + a.dot.slot0 + rb] = r;
+  }
   DQZ_STAMP(0, 3);
 }
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {

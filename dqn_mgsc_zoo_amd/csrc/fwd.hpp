@@ -51,6 +51,7 @@ struct LayerFwdArgs {
   int linear;  // 1: pre-activation output, no ReLU (tangent forward)
   float* out;  // [Z][B][...]
   Handoff wait, pub;  // fwd_conv_kernel: input produced / output consumed in the same launch
+  TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: dot products instead of stores
 };
 
 // ---- conv2: 20x20x32 -> 9x9x64, 4x4 stride 2 -------------------------------
@@ -134,16 +135,26 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
+  const bool dot = a.dot.part != nullptr;
+  const float* dyp = a.dot.dy + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
+  float dacc = 0.f;
   for (int i = t; i < C2M * 16; i += 256) {
     const int k = red_idx(i >> 4, i & 15);
     const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
     if constexpr (PUB)
       __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+    else if (dot)
+      dacc += v * dyp[(i >> 4) * C2CO + (i & 15)];
     else
       out[(i >> 4) * C2CO + (i & 15)] = linear ? v : relu(v);
   }
   if constexpr (PUB) a.pub.arrive(sj.s);
+  if (!PUB && dot) {
+    __syncthreads();
+    const float r = block_sum256(dacc, s_in);
+    if (t == 0) a.dot.part[(int64_t)b * META_DOT_SLOTS + a.dot.slot0 + nq] = r;
+  }
   DQZ_STAMP(1, 3);
 }
 
@@ -234,10 +245,21 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
+  const bool dot = a.dot.part != nullptr;
+  const float* dyp = a.dot.dy + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
+  float dacc = 0.f;
   for (int i = t; i < C3M * 16; i += 256) {
     const int k = red_idx(i >> 4, i & 15);
     const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
-    out[(i >> 4) * C3CO + (i & 15)] = linear ? v : relu(v);
+    if (dot)
+      dacc += v * dyp[(i >> 4) * C3CO + (i & 15)];
+    else
+      out[(i >> 4) * C3CO + (i & 15)] = linear ? v : relu(v);
+  }
+  if (dot) {
+    __syncthreads();
+    const float r = block_sum256(dacc, s_in);
+    if (t == 0) a.dot.part[(int64_t)b * META_DOT_SLOTS + a.dot.slot0 + nq] = r;
   }
   DQZ_STAMP(2, 3);
 }
@@ -304,6 +326,7 @@ struct Fc1FwdArgs {
   int64_t w_off;
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
+  TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
@@ -340,16 +363,29 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   __syncthreads();
   // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
   const int q = t >> 3, c4 = 4 * (t & 7);
-  if (32 * mg + q < a.B) {
-    float v[4];
+  const bool live = 32 * mg + q < a.B;
+  float v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = q * 33 + c4 + e;
-      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+  for (int e = 0; e < 4; ++e) {
+    const int k = q * 33 + c4 + e;
+    v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+  }
+  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+    float d = 0.f;
+    if (live) {
+      const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
+      d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
     }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (live && (t & 7) == 0)
+      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
+    return;
+  }
+  if (live)
     *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
         make_float4(v[0], v[1], v[2], v[3]);
-  }
 }
 
 inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
@@ -359,39 +395,6 @@ __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   __shared__ float s_red[4 * FC1_32RW];
   fc1_fwd_block32(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
-}
-
-// ---- MGSC meta tangent forward in one launch ------------------------------
-// V * y_{l-1} + vb of every layer over the meta batch's stored primal
-// activations (linear mode, the tangent v as weights; meta.hpp): the four
-// layers are independent of each other, so one launch holds them as block
-// ranges [conv1 4/sample] [conv2 4/sample] [conv3 4/sample] [fc1 tiles]
-// instead of four dependent launches.  Dynamic LDS = conv1's 57.6 KB.
-static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
-inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + fc1_fwd_blocks(1, MG); }
-__global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
-                                                          Fc1FwdArgs f1) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int n = 4 * ((c1.B + 7) / 8 * 8);
-  int i = blockIdx.x;
-  if (i < n) {
-    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, c1.B);
-    if (sj.valid) conv1_fwd_body<false, 0>(c1, smem, sj);
-    return;
-  }
-  i -= n;
-  if (i < n) {
-    const SampleJob sj = xcd_sample_job_at(i, 4, c2.B);
-    if (sj.valid) conv2_fwd_body<false, false>(c2, smem, sj);
-    return;
-  }
-  i -= n;
-  if (i < n) {
-    const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
-    if (sj.valid) conv3_fwd_body<false>(c3, smem, sj);
-    return;
-  }
-  fc1_fwd_block32(f1, smem, i - n);
 }
 
 }  // namespace dqz

@@ -53,17 +53,6 @@ __device__ __forceinline__ float hvp_x(const HvpArgs& a, int ih, int iw, int ci)
   return f < 0 ? 0.f : u8n(a.frames[(int64_t)f * FB + ih * FW + iw]);
 }
 
-// Sum of the block's 256 values v (thread order), deterministic, result in
-// every thread.  s: 4 floats of LDS.
-__device__ __forceinline__ float block_sum256(float v, float* s) {
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-  __syncthreads();
-  const float r = (s[0] + s[1]) + (s[2] + s[3]);
-  __syncthreads();
-  return r;
-}
-
 // 1. conv1 tangent: ty1[p][co] = relu'(y1) (bdot1[co] + sum_k x_p[k] Wdot1[k][co]).
 // Block p (400), thread (kh = t / 32, co = t % 32) sums kw, ci; the 8 kh
 // partials are summed in order.  Block 400 sums the s1 partials.

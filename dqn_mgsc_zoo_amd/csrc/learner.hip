@@ -1113,7 +1113,7 @@ struct dqz_meta {
   // second-order (reservoir) meta-gradient
   float *GQ, *HQ, *s1_part, *hpart;
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
-  int32_t* done;  // meta_dot_adam_kernel's arrival counter
+  float* dotp;  // [C][META_DOT_SLOTS] the tangent launch's dot-product partials (one chunk)
   int nparts2;
   void* block;
 };
@@ -1159,13 +1159,14 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            M, KC, KC, M, 1, H->nparts2, KC, KC, multi * H->total,
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
-                           so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID, 64};
+                           so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID,
+                           (int64_t)C * META_DOT_SLOTS};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
                     &H->ty1, &H->ty2, &H->ty3, &H->td4, &H->td3, &H->td2, &H->td1, &H->s1, &H->hpart,
-                    reinterpret_cast<float**>(&H->done)};
+                    &H->dotp};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
@@ -1357,7 +1358,6 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   NetZ nv;
   nv.p[0] = nv.p[1] = nv.p[2] = v;
   nv.which[0] = nv.which[1] = nv.which[2] = 0;
-  MetaDotArgs md;
   for (int k = 0; k < K; ++k) {
     const int32_t* ks = mslots + (int64_t)k * C;
     if (K > 1) {
@@ -1393,11 +1393,21 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     f1.B = C;
     f1.MG = (C + 31) / 32;
     f1.part = H->zvp;
+    MetaExtra ex{};
+    if (K == 1) {  // dot products in the tangent epilogues (meta.hpp)
+      c1.dot = TangentDot{L->dy1, H->dotp, 0};
+      c2.dot = TangentDot{L->dy2, H->dotp, 4};
+      c3.dot = TangentDot{L->dy3, H->dotp, 8};
+      f1.dot = TangentDot{L->dz1, H->dotp, 12};
+      ex = MetaExtra{L->dz1, L->h1, L->gq, L->ga, v, L->off[7], L->off[8], L->off[9], A, H->dotp};
+    }
     // the four layers' tangent outputs are independent: one launch
     hipLaunchKernelGGL(tangent_fwd_kernel, dim3((unsigned)tangent_fwd_blocks(C, f1.MG)), dim3(256), kConv1FwdSmem,
-                       st, c1, c2, c3, f1);
+                       st, c1, c2, c3, f1, ex);
     DQZ_HIP(hipGetLastError());
+    if (K == 1) break;
 
+    MetaDotArgs md;
     md.dy1 = L->dy1;
     md.dy2 = L->dy2;
     md.dy3 = L->dy3;
@@ -1417,7 +1427,6 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     md.b2_off = L->off[9];
     md.h1 = L->h1;
     md.s_out = H->s + (int64_t)k * C;
-    if (K == 1) break;  // the dot products run with the Adam step below
     hipLaunchKernelGGL(meta_dot_kernel, dim3(C), dim3(256), 0, st, md);
     DQZ_HIP(hipGetLastError());
   }
@@ -1426,6 +1435,8 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.x = H->x;
   ad.p = H->p;
   ad.s = H->s;
+  ad.dot_part = K == 1 ? H->dotp : nullptr;
+  ad.s_out = H->s;
   ad.M = M;
   ad.logits = logits;
   ad.pos = pos;
@@ -1446,10 +1457,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.run = keep ? logit_buf->run : nullptr;
   ad.dirty = keep ? logit_buf->dirty : nullptr;
   ad.n_logits = keep ? logit_buf->capacity : 0;
-  if (K == 1)
-    hipLaunchKernelGGL(meta_dot_adam_kernel, dim3(C), dim3(META_THREADS), 0, st, md, ad, H->done);
-  else
-    hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
+  hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
   DQZ_HIP(hipGetLastError());
   if (keep) return chunk_sums(logit_buf, logits, true, st);
   return DQZ_OK;

@@ -15,6 +15,8 @@
 //        optax.adam on the logits (meta_adam_kernel).
 #pragma once
 #include "common.hpp"
+#include "conv1.hpp"
+#include "fwd.hpp"
 #include "sampling.hpp"
 
 namespace dqz {
@@ -71,6 +73,77 @@ __global__ __launch_bounds__(META_THREADS) void meta_softmax_kernel(const float*
   for (int i = threadIdx.x; i < M; i += META_THREADS) se += expf(x_out[i] - c);
   const float lse = c + logf(block_sum_f32(se, sbuf));
   for (int i = threadIdx.x; i < M; i += META_THREADS) p_out[i] = expf(x_out[i] - lse);
+}
+
+// ---- MGSC meta tangent forward in one launch ------------------------------
+// V * y_{l-1} + vb of every layer over the meta batch's stored primal
+// activations (linear mode, the tangent v as weights): the four layers are
+// independent of each other, so one launch holds them as block ranges
+// [conv1 4/sample] [conv2 4/sample] [conv3 4/sample] [fc1 tiles] instead of
+// four dependent launches.  Dynamic LDS = conv1's 57.6 KB.
+// With one meta chunk the blocks do not store V * y + vb: each adds
+// <V * y + vb, dz> over its outputs (the p-weighted pre-activation gradient
+// of the same layer, TangentDot) into its slot of part[b][META_DOT_SLOTS]
+// (conv1 rows rb: slots 0..3, conv2 / conv3 quarters: 4..7 / 8..11, fc1
+// (column tile nt, split s): 12 + 7 nt + s), and the conv3 quarter-0 block
+// of sample b also the fc1 bias and fc2 terms (slot META_EXTRA_SLOT), so
+// meta_dot_kernel's pass over the stored tangents disappears.
+constexpr int META_EXTRA_SLOT = 12 + (HID / 32) * FC1_S;  // 124
+static_assert(META_EXTRA_SLOT < META_DOT_SLOTS, "meta dot slots");
+
+struct MetaExtra {
+  const float* dz1;   // [M][512]
+  const float* h1;    // [M][512] online fc1 output
+  const float* gq;    // [M]
+  const int32_t* ga;  // [M]
+  const float* v;     // tangent (param layout)
+  int64_t b1_off, w2_off, b2_off;
+  int A;
+  float* part;        // [M][META_DOT_SLOTS] (null: no dot products)
+};
+
+// vb1 . dz1[b] + gq[b] (h1[b] . V2[:, a_b] + vb2[a_b])  (256 threads)
+__device__ __forceinline__ void meta_extra_term(const MetaExtra& e, int b, float* s_tmp) {
+  const int t = threadIdx.x, act = e.ga[b];
+  float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int n = t + 256 * h;
+    f1 += e.v[e.b1_off + n] * e.dz1[(int64_t)b * HID + n];
+    f2 += e.h1[(int64_t)b * HID + n] * e.v[e.w2_off + n * e.A + act];
+  }
+  f1 = block_sum256(f1, s_tmp);
+  f2 = block_sum256(f2, s_tmp);
+  if (t == 0) e.part[(int64_t)b * META_DOT_SLOTS + META_EXTRA_SLOT] = f1 + e.gq[b] * (e.v[e.b2_off + act] + f2);
+}
+
+static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
+inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + fc1_fwd_blocks(1, MG); }
+__global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
+                                                          Fc1FwdArgs f1, MetaExtra ex) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n = 4 * ((c1.B + 7) / 8 * 8);
+  int i = blockIdx.x;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, c1.B);
+    if (sj.valid) conv1_fwd_body<false, 0>(c1, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c2.B);
+    if (sj.valid) conv2_fwd_body<false, false>(c2, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
+    if (!sj.valid) return;
+    conv3_fwd_body<false>(c3, smem, sj);
+    if (ex.part && sj.job == 0) meta_extra_term(ex, sj.s, smem);
+    return;
+  }
+  fc1_fwd_block32(f1, smem, i - n);
 }
 
 struct MetaRmsArgs {
@@ -194,6 +267,8 @@ struct MetaAdamArgs {
   const float* x;   // [M] gathered logits
   const float* p;   // [M]
   const float* s;   // [M] p_i dL/dp_i
+  const float* dot_part;  // or null: s_i = sum of the tangent launch's partials [M][META_DOT_SLOTS] (stored to s_out)
+  float* s_out;
   int M;
   float* logits;
   const int32_t* pos;
@@ -210,16 +285,33 @@ struct MetaAdamArgs {
 };
 
 // softmax backward + optax.adam (scale_by_adam, bias-corrected; scale(-lr)),
-// new logits scattered back.  One block striding over the M entries; s is
-// read with agent-scope loads (meta_dot_adam_kernel: other workgroups of the
-// same launch wrote it).
-__device__ __forceinline__ float load_s(const float* s, int i) {
-  return __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// new logits scattered back.  One block striding over the M entries.  With
+// dot_part, s_i is first summed from the tangent launch's partials (fixed
+// slot order) and stored; thread i handles entry i in both loops, so it
+// reads back its own store.
+__device__ __forceinline__ float meta_s(const MetaAdamArgs& a, int i) {
+  if (!a.dot_part) return a.s[i];
+  const float4* q = reinterpret_cast<const float4*>(a.dot_part + (int64_t)i * META_DOT_SLOTS);
+  float4 r[META_DOT_SLOTS / 4];
+#pragma unroll
+  for (int k = 0; k < META_DOT_SLOTS / 4; ++k) r[k] = q[k];
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < META_DOT_SLOTS / 4; ++k) {
+    acc += r[k].x;
+    if (4 * k + 1 <= META_EXTRA_SLOT) acc += r[k].y;
+    if (4 * k + 2 <= META_EXTRA_SLOT) acc += r[k].z;
+    if (4 * k + 3 <= META_EXTRA_SLOT) acc += r[k].w;
+    if (4 * k + 4 > META_EXTRA_SLOT) break;
+  }
+  a.s_out[i] = acc;
+  return acc;
 }
+
 __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __shared__ float sbuf[META_THREADS / 64];
   float st = 0.f;
-  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += load_s(a.s, i);
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += meta_s(a, i);
   const float tot = block_sum_f32(st, sbuf);
   float lp = 0.f;
   for (int j = threadIdx.x; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
@@ -234,7 +326,7 @@ __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __syncthreads();
   double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
   for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
-    const float g = load_s(a.s, i) - a.p[i] * tot;
+    const float g = (a.dot_part ? a.s_out[i] : a.s[i]) - a.p[i] * tot;
     const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
     const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
     const float mh = m / c1;
@@ -276,23 +368,5 @@ __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
 }
 
 __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) { meta_adam_body(a); }
-
-// meta_dot_kernel + meta_adam_kernel in one launch (one meta chunk): block b
-// publishes s[b] write-through and arrives on `done`; the block that arrives
-// last (every s[i] is then visible at agent scope) runs the Adam step and
-// resets the counter for the next launch.
-__global__ __launch_bounds__(META_THREADS) void meta_dot_adam_kernel(MetaDotArgs d, MetaAdamArgs a, int* done) {
-  __shared__ int s_last;
-  const float acc = meta_dot_sample(d, blockIdx.x);
-  if (threadIdx.x == 0) __hip_atomic_store(d.s_out + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  meta_adam_body(a);
-  if (threadIdx.x == 0) __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 }  // namespace dqz
