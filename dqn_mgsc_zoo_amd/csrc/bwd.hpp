@@ -609,10 +609,10 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   // operands and unconditionally (gradient-output mode re-reads theta: mu /
   // nu may be null there): vmcnt is in order, so the GEMM waits for its own
   // operands only and these loads land under it.
-  // (meta_rms1 reads theta, mu, nu too; meta_rms2 reads J, mu1, nu1)
-  const float* pth = R.meta == 2 ? R.J : a.th;
-  const float* pmu = R.meta == 2 ? R.mu1 : (upd || R.meta == 1) ? a.mu : a.th;
-  const float* pnu = R.meta == 2 ? R.nu1 : (upd || R.meta == 1) ? a.nu : a.th;
+  // (meta_rms1 reads theta, mu, nu too; meta_rms2 J, mu1, nu1; meta 3 G, mu1, nu1)
+  const float* pth = R.meta == 2 ? R.J : R.meta == 3 ? R.G2 : a.th;
+  const float* pmu = R.meta >= 2 ? R.mu1 : (upd || R.meta == 1) ? a.mu : a.th;
+  const float* pnu = R.meta >= 2 ? R.nu1 : (upd || R.meta == 1) ? a.nu : a.th;
   const int64_t e0 = a.w_off + (int64_t)(k0 + (lane >> 3)) * HID + c0 + 32 * w + 4 * (lane & 7);
   float4 o_th[2], o_mu[2], o_nu[2];
 #pragma unroll
@@ -651,7 +651,8 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tile[(4 * kq + r) * FC1W_TLD + 16 * q + n] = gacc[q][r];
-  float sq = 0.f;  // meta_rms2: this thread's u'^2
+  float sq = 0.f, s1 = 0.f;  // meta_rms2 / meta 3: this thread's u'^2 (and grad q . w)
+  const float clip = R.meta == 3 ? fminf(fmaxf(R.td[0], -R.bound), R.bound) : 0.f;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const float4 g = *reinterpret_cast<const float4*>(tile + ((lane >> 3) + 8 * h) * FC1W_TLD + 4 * (lane & 7));
@@ -674,6 +675,15 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
       o.z = R.meta2(g.z, o_mu[h].z, o_nu[h].z, o_th[h].z, sq);
       o.w = R.meta2(g.w, o_mu[h].w, o_nu[h].w, o_th[h].w, sq);
       *reinterpret_cast<float4*>(R.vout + e) = o;
+    } else if (R.meta == 3) {
+      float4 m = o_mu[h], v = o_nu[h];
+      R.meta3(g.x, o_th[h].x, m.x, v.x, clip, sq, s1);
+      R.meta3(g.y, o_th[h].y, m.y, v.y, clip, sq, s1);
+      R.meta3(g.z, o_th[h].z, m.z, v.z, clip, sq, s1);
+      R.meta3(g.w, o_th[h].w, m.w, v.w, clip, sq, s1);
+      *reinterpret_cast<float4*>(R.gout + e) = g;
+      *reinterpret_cast<float4*>(R.mu1 + e) = m;
+      *reinterpret_cast<float4*>(R.nu1 + e) = v;
     } else if (!upd) {
       float4 o = g;
       if (R.gacc) {
@@ -695,13 +705,19 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
       *reinterpret_cast<float4*>(a.th + e) = th;
     }
   }
-  if (R.meta == 2) {  // the block's u'^2 (each wave's sum in its own tile, then wave 0)
+  if (R.meta >= 2) {  // the block's u'^2 (and grad q . w): each wave's sums in its own tile, then wave 0
     sq = wave_sum(sq);
-    if (lane == 0) tile[0] = sq;
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+      tile[0] = sq;
+      tile[1] = s1;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       const float* t0 = smem + 32 * FC1W_LD;
-      R.sq_part[R.sq_off + blk] = (t0[0] + t0[16 * FC1W_TLD]) + (t0[2 * 16 * FC1W_TLD] + t0[3 * 16 * FC1W_TLD]);
+      constexpr int WT = 16 * FC1W_TLD;
+      R.sq_part[R.sq_off + blk] = (t0[0] + t0[WT]) + (t0[2 * WT] + t0[3 * WT]);
+      if (R.meta == 3) R.s1_part[R.sq_off + blk] = (t0[1] + t0[WT + 1]) + (t0[2 * WT + 1] + t0[3 * WT + 1]);
     }
   }
   DQZ_STAMP(11, 3);

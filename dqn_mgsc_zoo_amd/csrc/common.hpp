@@ -101,14 +101,21 @@ struct NetZ {
 //   meta == 1 (meta_rms1): theta' = theta + u(g; mu, nu) -> thp, the updated
 //             moments -> mu1, nu1, J = du/dg -> J (and g -> gout when set);
 //   meta == 2 (meta_rms2): u' = u(g; mu1, nu1), v = -2 u' J -> vout, and the
-//             block's sum of u'^2 -> sq_part[sq_off + block].
+//             block's sum of u'^2 -> sq_part[sq_off + block];
+//   meta == 3 (meta_second_kernel, second order): g = grad q (-> gout), with
+//             g' = -clip(td) g: v_dir -> mu1, w -> nu1 (from G2, mu1, nu1),
+//             the block's sums of u'^2 and of g . w -> sq_part / s1_part.
 struct Rms {
   float lr, decay, c1, eps;
   float* gout;
   int gacc;  // gradient-output mode: 1 adds into gout (meta-batch chunks), 0 overwrites
-  int meta;  // 0, 1 or 2 (above)
+  int meta;  // 0 .. 3 (above)
   float *thp, *mu1, *nu1, *J, *vout, *sq_part;
   int sq_off;
+  const float* G2;  // meta 3: the meta batch's gradient G
+  const float* td;  // meta 3: td' of the one-transition step (device scalar)
+  float bound;      // meta 3: grad_error_bound
+  float* s1_part;   // meta 3: block sums of grad q . w
   __device__ __forceinline__ bool update() const { return gout == nullptr && meta == 0; }
   // One centered RMSProp step (optax 0.1.2 scale_by_stddev, eps inside the
   // sqrt).  Every multiply-add is an explicit fma: hipcc contracts a*b + c*d
@@ -131,6 +138,26 @@ struct Rms {
     mu = m;
     nu = v;
     return -lr * (d - c1 * g * (g - m)) * (rs * rs * rs);
+  }
+  // The second order's u' / v pieces on one parameter: gq = grad q[a],
+  // g' = -clip(td') gq, mu'' = d mu1 + c g', nu'' = d nu1 + c g'^2,
+  // D2 = nu'' - mu''^2 + eps, u' = -lr g' D2^{-1/2} (sq += u'^2),
+  // v_dir = 2 u' c d lr g' D2^{-3/2} (G - mu'') -> mu,
+  // w = 2 u' (-lr) D2^{-3/2} (D2 - c g' (g' - mu'')) -> nu (s1 += gq w)
+  __device__ __forceinline__ void meta3(float gq, float G, float& mu, float& nu, float clip, float& sq,
+                                        float& s1) const {
+    const float g = -clip * gq;
+    const float m = c1 * g + decay * mu;
+    const float v = c1 * (g * g) + decay * nu;
+    const float d2 = v - m * m + eps;
+    const float rs = rsqrtf(d2);
+    const float rs3 = rs * rs * rs;
+    const float u = (-lr) * (g * rs);
+    mu = 2.f * u * c1 * decay * lr * g * rs3 * (G - m);
+    const float w = 2.f * u * (-lr) * rs3 * (d2 - c1 * g * (g - m));
+    nu = w;
+    sq += u * u;
+    s1 += gq * w;
   }
   // meta_rms2 on one parameter: u' = u(g; mu1, nu1); returns v = -2 u' J
   __device__ __forceinline__ float meta2(float g, float m0, float v0, float j, float& sq) const {

@@ -463,10 +463,11 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
   const Rms& R = u.rms;
   float o_th[2] = {0.f, 0.f}, o_mu[2] = {0.f, 0.f}, o_nu[2] = {0.f, 0.f};
   if (grp == 0 && (R.gout == nullptr || R.meta != 0)) {
-    // the epilogue's operands: theta, mu, nu (RMSProp, meta_rms1) or J, mu1, nu1 (meta_rms2)
-    const float* pt = R.meta == 2 ? R.J : u.th;
-    const float* pm = R.meta == 2 ? R.mu1 : u.mu;
-    const float* pn = R.meta == 2 ? R.nu1 : u.nu;
+    // the epilogue's operands: theta, mu, nu (RMSProp, meta_rms1), J, mu1, nu1
+    // (meta_rms2) or G, mu1, nu1 (meta 3)
+    const float* pt = R.meta == 2 ? R.J : R.meta == 3 ? R.G2 : u.th;
+    const float* pm = R.meta >= 2 ? R.mu1 : u.mu;
+    const float* pn = R.meta >= 2 ? R.nu1 : u.nu;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (dst[h] >= 0) {
@@ -485,7 +486,8 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     }
   }
   __syncthreads();
-  float sq = 0.f;  // meta_rms2: this thread's u'^2
+  float sq = 0.f, s1 = 0.f;  // meta_rms2 / meta 3: this thread's u'^2 (and grad q . w)
+  const float clip = R.meta == 3 ? fminf(fmaxf(R.td[0], -R.bound), R.bound) : 0.f;
   if (grp == 0) {
     float2 gs = make_float2(0.f, 0.f);
 #pragma unroll
@@ -508,6 +510,12 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         if (R.gout) R.gout[i] = gv[h];
       } else if (R.meta == 2) {
         R.vout[i] = R.meta2(gv[h], o_mu[h], o_nu[h], o_th[h], sq);
+      } else if (R.meta == 3) {
+        float m = o_mu[h], v = o_nu[h];
+        R.meta3(gv[h], o_th[h], m, v, clip, sq, s1);
+        R.gout[i] = gv[h];
+        R.mu1[i] = m;
+        R.nu1[i] = v;
       } else if (R.gout) {
         R.gout[i] = R.gacc ? R.gout[i] + gv[h] : gv[h];
       } else {
@@ -519,9 +527,13 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
       }
     }
   }
-  if (R.meta == 2 && threadIdx.x < 64) {  // grp 0 is the first half of wave 0
+  if (R.meta >= 2 && threadIdx.x < 64) {  // grp 0 is the first half of wave 0
     sq = wave_sum(sq);
     if (threadIdx.x == 0) R.sq_part[R.sq_off + blk] = sq;
+    if (R.meta == 3) {
+      s1 = wave_sum(s1);
+      if (threadIdx.x == 0) R.s1_part[R.sq_off + blk] = s1;
+    }
   }
   DQZ_STAMP(9, 3);
 }

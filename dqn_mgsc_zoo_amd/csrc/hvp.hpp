@@ -44,6 +44,32 @@ struct HvpArgs {
   const float* s1_part;
   int s1_nparts;
   float* s1;  // [1]
+  // meta_combine in hvp_g_kernel's epilogue (vout != null): instead of H_q w
+  // -> hq, v = v_dir + J (alpha s1 grad q - clip(td') H_q w) -> vout,
+  // alpha = [|td'| < bound]
+  const float *vdir, *J, *gq, *td;
+  float bound;
+  float* vout;
+};
+
+// One element of hvp_g_kernel's output: H_q w itself, or meta_combine's v.
+struct HqOut {
+  float a_s1, clip;  // alpha s1, clip(td')
+  __device__ __forceinline__ HqOut(const HvpArgs& a) {
+    if (a.vout) {
+      const float td = a.td[0];
+      a_s1 = fabsf(td) < a.bound ? a.s1[0] : 0.f;
+      clip = fminf(fmaxf(td, -a.bound), a.bound);
+    } else {
+      a_s1 = clip = 0.f;
+    }
+  }
+  __device__ __forceinline__ void put(const HvpArgs& a, int64_t i, float hq) const {
+    if (a.vout)
+      a.vout[i] = a.vdir[i] + a.J[i] * (a_s1 * a.gq[i] - clip * hq);
+    else
+      a.hq[i] = hq;
+  }
 };
 
 constexpr int HVP_T4_KC = 16, HVP_T4_CHUNKS = FLAT / HVP_T4_KC;  // 196 chunks of 16 rows
@@ -278,7 +304,8 @@ constexpr int HVP_G_BLOCKS = HVP_G_C1 + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC
 
 template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
-                                               const float* dd, int k, float* dst_w, float* dst_b, float (*s_r)[64]) {
+                                               const float* dd, int k, int64_t off_w, int64_t off_b, float (*s_r)[64],
+                                               const HqOut& ho) {
   const int t = threadIdx.x, co = t & 63, sp = t >> 6;  // 4 position splits
   constexpr int P = OH * OH, PS = (P + 3) / 4;
   const int p0 = sp * PS, p1 = min(P, p0 + PS);
@@ -297,9 +324,9 @@ __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y,
   if (t < CO) {
     const float v = (s_r[0][t] + s_r[1][t]) + (s_r[2][t] + s_r[3][t]);
     if (k == K * K * CI)
-      dst_b[t] = v;
+      ho.put(a, off_b + t, v);
     else
-      dst_w[k * CO + t] = v;
+      ho.put(a, off_w + (int64_t)k * CO + t, v);
   }
 }
 
@@ -307,6 +334,7 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
   const int t = threadIdx.x;
+  const HqOut ho(a);
   int i = blockIdx.x;
   if (i < HVP_G_C1) {  // conv1: thread (split = t / 32 of 50 positions, co)
     // the row's 400 patch values x_p[k] staged once (a loop of scattered
@@ -331,20 +359,18 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
       float v = 0.f;
 #pragma unroll
       for (int s = 0; s < 8; ++s) v += s_r[s][t];
-      a.hq[a.off[0] + (int64_t)k * C1CO + t] = v;  // row 256 is the bias (off[1] = off[0] + 8192)
+      ho.put(a, a.off[0] + (int64_t)k * C1CO + t, v);  // row 256 is the bias (off[1] = off[0] + 8192)
     }
     return;
   }
   i -= HVP_G_C1;
   if (i < HVP_G_C2) {
-    hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i, a.hq + a.off[2], a.hq + a.off[3],
-                                                   s_r);
+    hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i, a.off[2], a.off[3], s_r, ho);
     return;
   }
   i -= HVP_G_C2;
   if (i < HVP_G_C3) {
-    hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i, a.hq + a.off[4], a.hq + a.off[5],
-                                                 s_r);
+    hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i, a.off[4], a.off[5], s_r, ho);
     return;
   }
   i -= HVP_G_C3;
@@ -353,9 +379,9 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
     float z = a.tw[a.off[7] + n];
     for (int c = 0; c < HVP_T4_CHUNKS; ++c) z += a.part[(int64_t)c * HID + n];
     const float hd = a.h[n] > 0.f ? z : 0.f;
-    for (int col = 0; col < a.A; ++col) a.hq[a.off[8] + (int64_t)n * a.A + col] = col == act ? hd : 0.f;
-    a.hq[a.off[7] + n] = a.td4[n];
-    if (i == 0 && t < a.A) a.hq[a.off[9] + t] = 0.f;
+    for (int col = 0; col < a.A; ++col) ho.put(a, a.off[8] + (int64_t)n * a.A + col, col == act ? hd : 0.f);
+    ho.put(a, a.off[7] + n, a.td4[n]);
+    if (i == 0 && t < a.A) ho.put(a, a.off[9] + t, 0.f);
     return;
   }
   i -= HVP_G_H;
@@ -365,69 +391,25 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
     const float ty = a.ty3[k], y = a.y3[k];
     const float4 d = *reinterpret_cast<const float4*>(a.d4 + n);
     const float4 dd = *reinterpret_cast<const float4*>(a.td4 + n);
-    *reinterpret_cast<float4*>(a.hq + a.off[6] + e) =
+    const float4 hq =
         make_float4(ty * d.x + y * dd.x, ty * d.y + y * dd.y, ty * d.z + y * dd.z, ty * d.w + y * dd.w);
+    if (a.vout) {
+      const int64_t j = a.off[6] + e;
+      const float4 vd = *reinterpret_cast<const float4*>(a.vdir + j);
+      const float4 jj = *reinterpret_cast<const float4*>(a.J + j);
+      const float4 g = *reinterpret_cast<const float4*>(a.gq + j);
+      *reinterpret_cast<float4*>(a.vout + j) =
+          make_float4(vd.x + jj.x * (ho.a_s1 * g.x - ho.clip * hq.x), vd.y + jj.y * (ho.a_s1 * g.y - ho.clip * hq.y),
+                      vd.z + jj.z * (ho.a_s1 * g.z - ho.clip * hq.z), vd.w + jj.w * (ho.a_s1 * g.w - ho.clip * hq.w));
+    } else {
+      *reinterpret_cast<float4*>(a.hq + a.off[6] + e) = hq;
+    }
   }
 }
 
-// Second-order u' / v pieces (meta.hpp naming): g' = -clip(td') grad q,
-// mu'' = d mu' + c g', nu'' = d nu' + c g'^2, D2 = nu'' - mu''^2 + eps,
-//   u'    = -lr g' D2^{-1/2}                       (loss partials: u'^2)
-//   v_dir = 2 u' c d lr g' D2^{-3/2} (G - mu'')     -> written over mu1
-//   w     = 2 u' (-lr) D2^{-3/2} (D2 - c g'(g' - mu''))  -> written over nu1
-// and partial sums of grad q . w.
-struct MetaSecondArgs {
-  float lr, decay, c1, eps, bound;
-  int64_t n;
-  const float* td;  // [1] online transition TD at theta' (one-sample learner)
-};
-
-__global__ __launch_bounds__(256) void meta_second_kernel(MetaSecondArgs a, const float* __restrict__ gq,
-                                                          const float* __restrict__ G, float* mu1, float* nu1,
-                                                          float* __restrict__ loss_part, float* __restrict__ s1_part) {
-  __shared__ float sbuf[4];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float sq = 0.f, s1 = 0.f;
-  if (i < a.n) {
-    const float clip = fminf(fmaxf(a.td[0], -a.bound), a.bound);
-    const float gqv = gq[i];
-    const float g = -clip * gqv;
-    const float m = a.c1 * g + a.decay * mu1[i];
-    const float v = a.c1 * (g * g) + a.decay * nu1[i];
-    const float d2 = v - m * m + a.eps;
-    const float rs = rsqrtf(d2);
-    const float rs3 = rs * rs * rs;
-    const float u = (-a.lr) * (g * rs);
-    mu1[i] = 2.f * u * a.c1 * a.decay * a.lr * g * rs3 * (G[i] - m);
-    const float w = 2.f * u * (-a.lr) * rs3 * (d2 - a.c1 * g * (g - m));
-    nu1[i] = w;
-    sq = u * u;
-    s1 = gqv * w;
-  }
-  sq = wave_sum(sq);
-  s1 = wave_sum(s1);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) sbuf[wave] = sq;
-  __syncthreads();
-  if (threadIdx.x == 0) loss_part[blockIdx.x] = (sbuf[0] + sbuf[1]) + (sbuf[2] + sbuf[3]);
-  __syncthreads();
-  if (lane == 0) sbuf[wave] = s1;
-  __syncthreads();
-  if (threadIdx.x == 0) s1_part[blockIdx.x] = (sbuf[0] + sbuf[1]) + (sbuf[2] + sbuf[3]);
-}
-
-// v = v_dir + J (alpha s1 grad q - clip(td') H_q w), alpha = [|td'| < bound];
-// s1 = grad q . w, summed once by hvp_t1_kernel's last block.
-__global__ __launch_bounds__(256) void meta_combine_kernel(MetaSecondArgs a, const float* __restrict__ vdir,
-                                                           const float* __restrict__ J, const float* __restrict__ gq,
-                                                           const float* __restrict__ hq, const float* __restrict__ s1,
-                                                           float* __restrict__ v_out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const float td = a.td[0];
-  const float alpha = fabsf(td) < a.bound ? 1.f : 0.f;
-  const float clip = fminf(fmaxf(td, -a.bound), a.bound);
-  v_out[i] = vdir[i] + J[i] * (alpha * s1[0] * gq[i] - clip * hq[i]);
-}
+// The second order's elementwise stages run in gradient epilogues: the
+// u' / v_dir / w pieces in the one-transition backward's (common.hpp
+// Rms::meta3), v = v_dir + J (alpha s1 grad q - clip(td') H_q w) in
+// hvp_g_kernel's (HqOut).
 
 }  // namespace dqz

@@ -1291,21 +1291,17 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     // grad q[a] at theta' (unit cotangent) -> GQ; the one-sample learner keeps
     // the primal activations, the unit-cotangent backward signals and td'.
     dqz_learner* L1 = H->l1;
-    if (int rc = step_impl(L1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->GQ, nullptr, nullptr, 1))
+    // ... consumed where it is formed (Rms::meta3, meta_second_kernel's
+    // stage): v_dir -> mu1, w -> nu1, block sums of u'^2 and grad q . w
+    epi.meta = 3;
+    epi.G2 = H->G;
+    epi.td = L1->td;
+    epi.bound = H->cfg.grad_error_bound;
+    epi.s1_part = H->s1_part;
+    if (int rc = step_impl(L1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->GQ, nullptr, nullptr, 1, 0,
+                           nullptr, nullptr, nullptr, &epi))
       return rc;
-    MetaSecondArgs sa;
-    sa.lr = ra.lr;
-    sa.decay = ra.decay;
-    sa.c1 = ra.c1;
-    sa.eps = ra.eps;
-    sa.bound = H->cfg.grad_error_bound;
-    sa.n = H->total;
-    sa.td = L1->td;
-    const dim3 eg1((unsigned)H->nparts2);
-    // v_dir -> mu1, w -> nu1, partial sums of u'^2 and grad q . w
-    hipLaunchKernelGGL(meta_second_kernel, eg1, dim3(256), 0, st, sa, H->GQ, H->G, H->mu1, H->nu1, H->loss_part,
-                       H->s1_part);
-    DQZ_HIP(hipGetLastError());
+    const int nparts1 = 4 * (FLAT / 16) + (int)update_blocks(L1->sz, A, L1->shared_bias ? 1 : A);
     HvpArgs hv;
     hv.frames = S1->frames;
     hv.fidx = S1->fidx;
@@ -1333,8 +1329,16 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hv.hq = H->HQ;
     hv.part = H->hpart;
     hv.s1_part = H->s1_part;
-    hv.s1_nparts = H->nparts2;
+    hv.s1_nparts = nparts1;
     hv.s1 = H->s1;
+    // meta_combine in hvp_g's epilogue: v = v_dir + J (alpha s1 grad q -
+    // clip(td') H w) -> thp (theta' is no longer needed)
+    hv.vdir = H->mu1;
+    hv.J = H->J;
+    hv.gq = H->GQ;
+    hv.td = L1->td;
+    hv.bound = H->cfg.grad_error_bound;
+    hv.vout = H->thp;
     // eight dependent stages (hvp.hpp): tangent forward, tangent backward,
     // then every parameter block of H_q w
     hipLaunchKernelGGL(hvp_t1_kernel, dim3(C1M + 1), dim3(256), 0, st, hv);
@@ -1346,10 +1350,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hipLaunchKernelGGL(hvp_b1_kernel, dim3(C1M), dim3(256), 0, st, hv);
     hipLaunchKernelGGL(hvp_g_kernel, dim3(HVP_G_BLOCKS), dim3(256), 0, st, hv);
     DQZ_HIP(hipGetLastError());
-    // v = v_dir + J (alpha s1 grad q - clip(td') H w) -> thp (theta' is no longer needed)
-    hipLaunchKernelGGL(meta_combine_kernel, eg1, dim3(256), 0, st, sa, H->mu1, H->J, H->GQ, H->HQ, H->s1, H->thp);
-    DQZ_HIP(hipGetLastError());
-    nloss = H->nparts2;
+    nloss = nparts1;
   }
 
   // Tangent forward over the stored online activations: V * y + vb per layer,
