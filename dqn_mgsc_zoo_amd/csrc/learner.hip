@@ -326,25 +326,17 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     if (int rc = forward_impl(L, nz, Z, B, src, st, pe, true)) return rc;
   }
 
-  Rms rms;
+  // an MGSC meta stage applied in the gradient epilogues (Rms), or plain
+  // RMSProp / gradient output: every field set (value-initialised first)
+  Rms rms{};
+  if (meta_epi) rms = *meta_epi;
   rms.lr = L->cfg.learning_rate;
   rms.decay = L->cfg.decay;
   rms.c1 = (float)(1.0 - (double)L->cfg.decay);
   rms.eps = L->cfg.eps;
   rms.gout = gout;
   rms.gacc = gacc;
-  rms.meta = 0;
-  rms.thp = rms.mu1 = rms.nu1 = rms.J = rms.vout = rms.sq_part = nullptr;
   rms.sq_off = 0;
-  if (meta_epi) {  // an MGSC meta stage applied in the gradient epilogues (Rms)
-    rms.meta = meta_epi->meta;
-    rms.thp = meta_epi->thp;
-    rms.mu1 = meta_epi->mu1;
-    rms.nu1 = meta_epi->nu1;
-    rms.J = meta_epi->J;
-    rms.vout = meta_epi->vout;
-    rms.sq_part = meta_epi->sq_part;
-  }
 
   HeadArgs h = make_head(L, nz, Z, B);
   h.fwd_only = 0;
