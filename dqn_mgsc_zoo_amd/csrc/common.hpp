@@ -74,18 +74,11 @@ __device__ __forceinline__ float u8n(unsigned v) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
-// fc1 split-K ways (fwd.hpp fc1_fwd_block32: K = 3136 in FC1_S splits; the
-// head sums the FC1_S partials)
-#ifndef DQZ_FC1_S
-#define DQZ_FC1_S 7
-#endif
-constexpr int FC1_S = DQZ_FC1_S;
-
 // MGSC tangent forward with the meta-update's dot products in its epilogues
 // (meta.hpp): instead of storing V * y + vb, a block adds <output, dy> over
 // the outputs it owns and writes one partial at part[b * META_DOT_SLOTS +
 // slot].  part == null: the outputs are stored as usual.
-constexpr int META_DOT_SLOTS = (12 + 16 * FC1_S + 1 + 31) / 32 * 32;  // 128 at FC1_S = 7
+constexpr int META_DOT_SLOTS = 128;
 struct TangentDot {
   const float* dy;  // the layer's p-weighted pre-activation gradients, laid out as its output
   float* part;      // [M][META_DOT_SLOTS]

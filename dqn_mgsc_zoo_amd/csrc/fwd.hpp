@@ -317,8 +317,7 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
 // form, whose 16-column B operand fetched 64-byte halves of W1's lines; that
 // kernel and the in-launch split-K reduce variant are in git history, commit
 // 1a3be58.)
-constexpr int FC1_KS = FLAT / FC1_S, FC1_KW = FC1_KS / 4;  // 448, 112 at FC1_S = 7
-static_assert(FLAT % FC1_S == 0 && FC1_KW % 8 == 0, "fc1 K splits: whole 8-row MFMA groups per wave");
+constexpr int FC1_S = 7, FC1_KS = FLAT / FC1_S, FC1_KW = FC1_KS / 4;  // 448, 112
 constexpr int Z_MAX_FC1 = 3;  // network copies of one fc1 launch (online, target, online(s_t))
 
 struct Fc1FwdArgs {
@@ -330,98 +329,66 @@ struct Fc1FwdArgs {
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
 };
 
-// Columns per lane: a block owns 32 FC1_NJ columns; lane c loads FC1_NJ
-// consecutive columns of a W1 row as one vector and feeds them to FC1_NJ
-// accumulators (accumulator j's column c is column FC1_NJ c + j), so the
-// y3 operand is shared by 32 FC1_NJ columns.
-#ifndef DQZ_FC1_NJ
-#define DQZ_FC1_NJ 1
-#endif
-constexpr int FC1_NJ = DQZ_FC1_NJ;
-static_assert(FC1_NJ == 1 || FC1_NJ == 2 || FC1_NJ == 4, "fc1 columns per lane");
-constexpr int FC1_NC = 32 * FC1_NJ;                 // columns per block
-constexpr int FC1_32RW = 32 * (FC1_NC + 1);         // one wave's 32 x FC1_NC tile, row stride FC1_NC + 1
-template <int NJ> struct FVec;
-template <> struct FVec<1> { typedef float T; };
-template <> struct FVec<2> { typedef float2 T; };
-template <> struct FVec<4> { typedef float4 T; };
-__device__ __forceinline__ float fv_get(float v, int) { return v; }
-__device__ __forceinline__ float fv_get(float2 v, int j) { return j == 0 ? v.x : v.y; }
-__device__ __forceinline__ float fv_get(float4 v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
-
+constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
-  constexpr int NJ = FC1_NJ, NC = FC1_NC, NT = HID / NC;
-  typedef typename FVec<NJ>::T wvec;
-  const int nt = i % NT;
-  const int rest = i / NT;
+  const int nt = i % (HID / 32);
+  const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
   const int z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
-  const float* W = a.nz.p[z] + a.w_off + NC * nt + NJ * c;  // [3136][512]
-  constexpr int G = FC1_KW / 8;
-  wvec wr[G][4];
+  const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
+  constexpr int G = FC1_KW / 8;                         // 14
+  float wr[G][4];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) wr[g][e] = *reinterpret_cast<const wvec*>(W + (int64_t)(k0 + 8 * g + e) * HID);
+    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   const int row = min(32 * mg + c, a.B - 1);
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float4 av[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
-  f32x16 acc[NJ];
+  f32x16 acc = {};
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] = f32x16{};
+  for (int g = 0; g < G; ++g) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
+  }
 #pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, fv_get(wr[g][0], j), acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, fv_get(wr[g][1], j), acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, fv_get(wr[g][2], j), acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, fv_get(wr[g][3], j), acc[j], 0, 0, 0);
-    }
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * (NC + 1) + NJ * c + j] = acc[j][r];
+  for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
   __syncthreads();
-  // 256 threads x 4 NJ outputs: row q = t / 8 (0..31), columns 4 NJ (t % 8) ..
-  const int q = t >> 3;
+  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
+  const int q = t >> 3, c4 = 4 * (t & 7);
   const bool live = 32 * mg + q < a.B;
-  float dsum = 0.f;
+  float v[4];
 #pragma unroll
-  for (int u = 0; u < NJ; ++u) {
-    const int c4 = 4 * NJ * (t & 7) + 4 * u;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = q * (NC + 1) + c4 + e;
-      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
-    }
-    if (a.dot.part) {
-      if (live) {
-        const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + NC * nt + c4);
-        dsum += (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
-      }
-    } else if (live) {
-      *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + NC * nt + c4) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    }
+  for (int e = 0; e < 4; ++e) {
+    const int k = q * 33 + c4 + e;
+    v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
   }
-  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 NJ columns
-    dsum += __shfl_xor(dsum, 1, 64);
-    dsum += __shfl_xor(dsum, 2, 64);
-    dsum += __shfl_xor(dsum, 4, 64);
+  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+    float d = 0.f;
+    if (live) {
+      const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
+      d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
+    }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
     if (live && (t & 7) == 0)
-      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = dsum;
+      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
+    return;
   }
+  if (live)
+    *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
+        make_float4(v[0], v[1], v[2], v[3]);
 }
 
-inline int fc1_fwd_blocks(int Z, int MG) { return (HID / FC1_NC) * FC1_S * Z * MG; }
+inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);

@@ -335,11 +335,11 @@ inline void launch_head_z(const HeadArgs& h, int grid, hipStream_t st) {
 }
 
 inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
-  if (h.S > FC1_S || h.Z < 1 || h.Z > 3) return hipErrorInvalidValue;
+  if (h.S > 7 || h.Z < 1 || h.Z > 3) return hipErrorInvalidValue;
   if (h.Z <= 2) {
-    launch_head_z<FC1_S, 2>(h, grid, st);
+    launch_head_z<7, 2>(h, grid, st);
   } else {
-    launch_head_z<FC1_S, 3>(h, grid, st);
+    launch_head_z<7, 3>(h, grid, st);
   }
   return hipGetLastError();
 }
