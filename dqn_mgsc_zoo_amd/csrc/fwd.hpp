@@ -158,6 +158,98 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   DQZ_STAMP(1, 3);
 }
 
+// fwd_conv_kernel's conv2: 8 jobs per sample, job j = output rows
+// [5 (j >> 2), +5 or +4) (45 / 36 positions) x output channels [16 (j & 3),
+// +16).  Against the 4 channel-quarter jobs of conv2_fwd_body each job stages
+// 60 % / 50 % of y1 (input rows [10 (j >> 2), +12 or +10): the bytes that
+// arrive after the hand-off wait) and runs 3 MFMA row tiles instead of 5, so
+// the per-sample chain after conv1 is shorter; y2 goes out as 16-byte
+// write-through stores (4 channels per lane) and conv3 waits for 8 arrivals.
+#ifndef DQZ_C2F_JOBS
+#define DQZ_C2F_JOBS 8
+#endif
+constexpr int C2F_JOBS = DQZ_C2F_JOBS, C2F_ROWS0 = 5;  // 4: conv2_fwd_body's channel quarters
+static_assert(C2F_JOBS == 4 || C2F_JOBS == 8, "fused conv2 jobs per sample");
+__device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
+  DQZ_STAMP(1, 0);
+  const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
+  const int oh0 = rh * C2F_ROWS0, npos = (rh ? C2O - C2F_ROWS0 : C2F_ROWS0) * C2O;  // 45 / 36
+  const int ih0 = C2S * oh0, nrows = C2S * (npos / C2O - 1) + C2K;               // 12 / 10
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
+  const int n = lane & 15, kq = lane >> 4;
+  const float* W = a.nz.p[z] + a.w_off;  // [512][64], k = kh*128 + kw*32 + ci
+  // epilogue bias of this lane's channels 16 nq + 4 (t & 3) .. + 3, loaded early
+  const float4 bias4 = *reinterpret_cast<const float4*>(a.nz.p[z] + a.b_off + 16 * nq + 4 * (t & 3));
+  float wr[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) wr[kk] = W[(w * 128 + 4 * kk + kq) * C2CO + 16 * nq + n];
+  const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C1M * C1CO)) +
+                      ih0 * C1O * (C1CO / 4);
+  const int nq4 = nrows * C1O * (C1CO / 4);  // 1920 / 1600 float4
+  a.wait.wait(sj.s);
+  constexpr int NL = (2 * C2F_ROWS0 + 2) * C1O * (C1CO / 4) / 256;  // 7.5 -> 8 loads per thread at most
+  float4 r[NL + 1];
+#pragma unroll
+  for (int q = 0; q <= NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
+#pragma unroll
+  for (int q = 0; q <= NL; ++q) {
+    const int i = t + 256 * q;
+    if (i < nq4) {
+      const int pix = i >> 3, ci = (i & 7) * 4;  // 8 float4 per pixel
+      float* d = s_in + (pix / C1O) * C2L_RS + (pix % C1O) * C2L_S + ci;
+      d[0] = r[q].x;
+      d[1] = r[q].y;
+      d[2] = r[q].z;
+      d[3] = r[q].w;
+    }
+  }
+  DQZ_STAMP(1, 1);
+  __syncthreads();
+  constexpr int MT = 3;  // 48 rows: the tail rows clamp to the last position and are not stored
+  int base[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int p = min(16 * m + n, npos - 1);
+    base[m] = (2 * (p / C2O) + w) * C2L_RS + 2 * (p % C2O) * C2L_S + kq;
+  }
+  f32x4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    const int off = (kk >> 3) * C2L_S + 4 * (kk & 7);  // kw, ci block
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+  }
+  DQZ_STAMP(1, 2);
+  __syncthreads();
+  float* s_red = s_in;  // [4][48 rows, padded][16]
+  constexpr int RW = red_rows(16 * MT);
+  static_assert(4 * RW <= C2L_WIN, "conv2 partials fit the window");
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
+  __syncthreads();
+  float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + oh0 * C2O * C2CO + 16 * nq;
+  const int out_bytes = (C2M * C2CO - oh0 * C2O * C2CO - 16 * nq) * 4;
+  const bool linear = a.linear;  // read once (see conv1_fwd_body)
+  for (int i = t; i < npos * 4; i += 256) {
+    const int p = i >> 2, c4 = 4 * (i & 3);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = red_idx(p, c4 + e);
+      const float bb = e == 0 ? bias4.x : e == 1 ? bias4.y : e == 2 ? bias4.z : bias4.w;
+      const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bb;
+      o[e] = linear ? v : relu(v);
+    }
+    store_sc1_f4(out, out_bytes, 4 * (p * C2CO + c4), f32x4{o[0], o[1], o[2], o[3]});
+  }
+  a.pub.arrive(sj.s);
+  DQZ_STAMP(1, 3);
+}
+
 __global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
   __shared__ float s_in[C2L_WIN];
   const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
@@ -296,12 +388,18 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
     return;
   }
   i -= n;
-  if (i < n) {
-    const SampleJob sj = xcd_sample_job_at(i, 4, zb);
-    if (sj.valid) conv2_fwd_body<true, true>(c2, smem, sj);
+  constexpr int n2f = C2F_JOBS / 4;  // conv2 range = n2f x n
+  if (i < n2f * n) {
+    const SampleJob sj = xcd_sample_job_at(i, C2F_JOBS, zb);
+    if (sj.valid) {
+      if constexpr (C2F_JOBS == 8)
+        conv2_fwd8_body(c2, smem, sj);
+      else
+        conv2_fwd_body<true, true>(c2, smem, sj);
+    }
     return;
   }
-  const SampleJob sj = xcd_sample_job_at(i - n, 4, zb);
+  const SampleJob sj = xcd_sample_job_at(i - n2f * n, 4, zb);
   if (sj.valid) conv3_fwd_body<true>(c3, smem, sj);
 }
 
