@@ -1,17 +1,18 @@
 #!/bin/bash
-# fc1 forward placement A/B: learner / meta / full-size GPU tests on the
-# default library, an interleaved A/B of the default bench against the
-# -DDQZ_FC1_XCD=0 build (XCD-matched W1 slices), and the M = 100 meta-update
-# against the -DDQZ_FC1_MGLOOP=0 build (row groups looped inside the block).
+# Round-4 kernel A/B: the GPU suite on the default library, an interleaved
+# A/B of the default bench against -DDQZ_FC1_XCD=0 (fc1 W1 slices without the
+# XCD-matched placement) and -DDQZ_C2F_JOBS=4 (conv2 forward as 4 channel-
+# quarter jobs per sample), the M = 100 meta-update against
+# -DDQZ_FC1_MGLOOP=0 (one block per fc1 row group), and a meta kernel trace.
 set -o pipefail
 OUT=gpurun_out/xcdab
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_learner_gpu.py tests/test_meta_gpu.py tests/test_fullsize_gpu.py -m gpu -q -rf --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $OUT/tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 set -e
-bash tools/abv.sh 3 dqn_mgsc_zoo_amd/libdqz.so dqn_mgsc_zoo_amd/libdqz_noxcd.so > $OUT/abv.txt 2>&1
+bash tools/abv.sh 3 dqn_mgsc_zoo_amd/libdqz.so dqn_mgsc_zoo_amd/libdqz_noxcd.so dqn_mgsc_zoo_amd/libdqz_c2x4.so > $OUT/abv.txt 2>&1
 for r in 1 2; do
   for V in libdqz libdqz_nomg; do
     DQZ_LIB=$PWD/dqn_mgsc_zoo_amd/$V.so timeout -k 10 300 python tools/meta_bench.py --steps 100 > $OUT/meta_${V}_$r.json 2> $OUT/meta_${V}_$r.err
