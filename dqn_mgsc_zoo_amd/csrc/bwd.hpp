@@ -723,25 +723,6 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   DQZ_STAMP(11, 3);
 }
 
-// fc1 dW slot i of the backward's 784 -> block (kb, nq) = (b >> 2, b & 3):
-// XCD x = i % 8 takes column quarter nq = x / 2 and the K splits s (28 row
-// blocks each, fwd.hpp FC1_S) of parity x & 1, so the W1 slices it writes are
-// the ones the next step's fc1 forward reads on that XCD (fc1_xcd_block);
-// the even XCDs' surplus (split 6, rows 14..27 of it) goes to the odd sibling
-// so that every XCD gets 98 slots.
-__device__ __forceinline__ int fc1_dw_slot(int i) {
-#if DQZ_FC1_XCD
-  const int x = i & 7, j = i >> 3, nq = x >> 1;
-  int kb;
-  if (!(x & 1)) kb = 56 * (j / 28) + j % 28;            // s = 0, 2, 4; split 6 rows 0..13
-  else if (j < 84) kb = 28 * (1 + 2 * (j / 28)) + j % 28;  // s = 1, 3, 5
-  else kb = 168 + 14 + (j - 84);                          // split 6 rows 14..27
-  return 4 * kb + nq;
-#else
-  return i;
-#endif
-}
-
 // ---- backward launches ----------------------------------------------------
 // fc1_dx_kernel (fc1 dX), then bwd_bc_kernel: the critical-path dX job chain
 // and the independent dW job sets share one launch, so the latency-bound dX
@@ -817,7 +798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
   i -= 8 * B8;
   if (i < NF) {
-    fc1_dw_body(f1, smem, fc1_dw_slot(i));
+    fc1_dw_body(f1, smem, i);
     return;
   }
   i -= NF;

@@ -425,46 +425,14 @@ struct Fc1FwdArgs {
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
-  int xcd = 0;      // 1: fc1_xcd_block's placement (Z 2 or 3, MG 1)
 };
 
-#ifndef DQZ_FC1_XCD
-#define DQZ_FC1_XCD 1
-#endif
-// XCD placement of the learner step's fc1 forward (Z 2 / 3, one row group):
-// the online copies' block (nt, s) goes to XCD 2 (nt / 4) + (s & 1), the XCD
-// whose fc1 dW + RMSProp blocks (bwd.hpp fc1_dw_slot) last wrote that slice
-// of W1, so the step's re-read of the updated weights can hit that XCD's L2;
-// the target blocks (z = 1) fill each XCD up to 14 Z.  Returns the linear
-// index fc1_fwd_block32 decodes.  (Workgroup i runs on XCD i % 8.)
-__device__ __forceinline__ int fc1_xcd_block(int i, int Z) {
-  const int x = i & 7, j = i >> 3, nq = x >> 1, p = x & 1;
-  const int ns = p ? 3 : 4;                  // K splits of parity p
-  const int n_on = (Z - 1) * 4 * ns;         // online blocks on this XCD
-  if (j < n_on) {
-    const int zo = j / (4 * ns), jj = j % (4 * ns);
-    const int s = p + 2 * (jj >> 2), nt = 4 * nq + (jj & 3);
-    return nt + (HID / 32) * (s + FC1_S * (zo ? 2 : 0));
-  }
-  const int te = 14 * Z - (Z - 1) * 16, to = 14 * Z - (Z - 1) * 12;  // target shares, even / odd XCD
-  const int t = (x >> 1) * (te + to) + p * te + (j - n_on);
-  return (t & 15) + (HID / 32) * ((t >> 4) + FC1_S);
-}
-
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
-#ifndef DQZ_FC1_MGLOOP
-#define DQZ_FC1_MGLOOP 1
-#endif
-// One block = (column tile nt, split s, copy z) and, with DQZ_FC1_MGLOOP, every
-// row group of the batch in turn: the block's W1 slice stays in registers and
-// only the 32 x 448 y3 tile (an L2 hit after the first column tile) is
-// re-read per row group, instead of MG blocks each fetching the W1 slice.
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
-  const int z = DQZ_FC1_MGLOOP ? zm : zm / a.MG;
-  const int mg0 = DQZ_FC1_MGLOOP ? 0 : zm % a.MG, mg1 = DQZ_FC1_MGLOOP ? a.MG : mg0 + 1;
+  const int z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
@@ -475,57 +443,55 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
-  for (int mg = mg0; mg < mg1; ++mg) {
-    const int row = min(32 * mg + c, a.B - 1);
-    const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
-    float4 av[G];
+  const int row = min(32 * mg + c, a.B - 1);
+  const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
+  float4 av[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
-    f32x16 acc = {};
+  for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
+  f32x16 acc = {};
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
-    }
-    if (mg > mg0) __syncthreads();  // the previous row group's readers of s_red are done
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
-    __syncthreads();
-    // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
-    const int q = t >> 3, c4 = 4 * (t & 7);
-    const bool live = 32 * mg + q < a.B;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = q * 33 + c4 + e;
-      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
-    }
-    if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
-      float d = 0.f;
-      if (live) {
-        const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
-        d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
-      }
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      if (live && (t & 7) == 0)
-        a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
-    } else if (live) {
-      *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    }
+  for (int g = 0; g < G; ++g) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
+  __syncthreads();
+  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
+  const int q = t >> 3, c4 = 4 * (t & 7);
+  const bool live = 32 * mg + q < a.B;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = q * 33 + c4 + e;
+    v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+  }
+  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+    float d = 0.f;
+    if (live) {
+      const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
+      d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
+    }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (live && (t & 7) == 0)
+      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
+    return;
+  }
+  if (live)
+    *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
+        make_float4(v[0], v[1], v[2], v[3]);
 }
 
-inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * (DQZ_FC1_MGLOOP ? 1 : MG); }
+inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_32RW];
-  fc1_fwd_block32(a, s_red, a.xcd ? fc1_xcd_block(blockIdx.x, gridDim.x / ((HID / 32) * FC1_S)) : blockIdx.x);
+  fc1_fwd_block32(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 
