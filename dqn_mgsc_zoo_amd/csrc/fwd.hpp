@@ -356,6 +356,94 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   DQZ_STAMP(2, 3);
 }
 
+// fwd_conv_kernel's conv3: 8 jobs per sample, job j = output rows
+// [4 (j >> 2), +4 or +3) (28 / 21 positions, 2 MFMA row tiles instead of 3 +
+// the VALU position) x output channels [16 (j & 3), +16); each stages input
+// rows [4 (j >> 2), +6 or +5) of y2 (67 % / 56 %) after its hand-off wait.
+#ifndef DQZ_C3F_JOBS
+#define DQZ_C3F_JOBS 8
+#endif
+constexpr int C3F_JOBS = DQZ_C3F_JOBS, C3F_ROWS0 = 4;  // 4: conv3_fwd_body's channel quarters
+static_assert(C3F_JOBS == 4 || C3F_JOBS == 8, "fused conv3 jobs per sample");
+__device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
+  DQZ_STAMP(2, 0);
+  const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
+  const int oh0 = rh * C3F_ROWS0, npos = (rh ? C3O - C3F_ROWS0 : C3F_ROWS0) * C3O;  // 28 / 21
+  const int nrows = npos / C3O + C3K - 1;                                          // 6 / 5
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, kq = lane >> 4;
+  const float* W = a.nz.p[z] + a.w_off;  // [576][64], k = (kh*3 + kw)*64 + ci
+  const float4 bias4 = *reinterpret_cast<const float4*>(a.nz.p[z] + a.b_off + 16 * nq + 4 * (t & 3));
+  float wr[36];
+#pragma unroll
+  for (int kk = 0; kk < 36; ++kk)
+    wr[kk] = W[((kk >> 2) * C3CI + 16 * w + 4 * (kk & 3) + kq) * C3CO + 16 * nq + n];
+  const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C2M * C2CO)) +
+                      oh0 * C2O * (C2CO / 4);
+  const int nq4 = nrows * C2O * (C2CO / 4);  // 864 / 720 float4
+  a.wait.wait(sj.s);
+  constexpr int NL = ((C3F_ROWS0 + C3K - 1) * C2O * (C2CO / 4) + 255) / 256;  // 4
+  float4 r[NL];
+#pragma unroll
+  for (int q = 0; q < NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
+#pragma unroll
+  for (int q = 0; q < NL; ++q) {
+    const int i = t + 256 * q;
+    if (i < nq4) {
+      const int pix = i >> 4, ci = (i & 15) * 4;
+      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + ci;
+      d[0] = r[q].x;
+      d[1] = r[q].y;
+      d[2] = r[q].z;
+      d[3] = r[q].w;
+    }
+  }
+  DQZ_STAMP(2, 1);
+  __syncthreads();
+  constexpr int MT = 2;  // 32 rows: the tail rows clamp to the last position and are not stored
+  int base[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int p = min(16 * m + n, npos - 1);
+    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + 16 * w + kq;
+  }
+  f32x4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 36; ++kk) {
+    const int tap = kk >> 2;
+    const int off = (tap / 3) * C3L_RS + (tap % 3) * C3L_S + 4 * (kk & 3);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
+  }
+  DQZ_STAMP(2, 2);
+  __syncthreads();
+  float* s_red = s_in;  // [4][32 rows, padded][16]
+  constexpr int RW = red_rows(16 * MT);
+  static_assert(4 * RW <= C3L_WIN, "conv3 partials fit the window");
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
+  __syncthreads();
+  float* out = a.out + ((int64_t)z * a.B + b) * FLAT + oh0 * C3O * C3CO + 16 * nq;
+  const bool linear = a.linear;  // read once (see conv1_fwd_body)
+  for (int i = t; i < npos * 4; i += 256) {
+    const int p = i >> 2, c4 = 4 * (i & 3);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = red_idx(p, c4 + e);
+      const float bb = e == 0 ? bias4.x : e == 1 ? bias4.y : e == 2 ? bias4.z : bias4.w;
+      const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bb;
+      o[e] = linear ? v : relu(v);
+    }
+    *reinterpret_cast<float4*>(out + p * C3CO + c4) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  DQZ_STAMP(2, 3);
+}
+
 __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
   __shared__ float s_in[C3L_WIN];
   const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
@@ -399,8 +487,13 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
     }
     return;
   }
-  const SampleJob sj = xcd_sample_job_at(i - n2f * n, 4, zb);
-  if (sj.valid) conv3_fwd_body<true>(c3, smem, sj);
+  const SampleJob sj = xcd_sample_job_at(i - n2f * n, C3F_JOBS, zb);
+  if (sj.valid) {
+    if constexpr (C3F_JOBS == 8)
+      conv3_fwd8_body(c3, smem, sj);
+    else
+      conv3_fwd_body<true>(c3, smem, sj);
+  }
 }
 
 // ---- fc1: [B][3136] x [3136][512] split-K partials ------------------------
