@@ -51,6 +51,7 @@ struct LayerFwdArgs {
   int linear;  // 1: pre-activation output, no ReLU (tangent forward)
   float* out;  // [Z][B][...]
   Handoff wait, pub;  // fwd_conv_kernel: input produced / output consumed in the same launch
+  int jobs = 4;       // fwd_conv_kernel: jobs per sample of this layer (4 or 8, fwd_conv_jobs)
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: dot products instead of stores
 };
 
@@ -165,11 +166,7 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
 // arrive after the hand-off wait) and runs 3 MFMA row tiles instead of 5, so
 // the per-sample chain after conv1 is shorter; y2 goes out as 16-byte
 // write-through stores (4 channels per lane) and conv3 waits for 8 arrivals.
-#ifndef DQZ_C2F_JOBS
-#define DQZ_C2F_JOBS 8
-#endif
-constexpr int C2F_JOBS = DQZ_C2F_JOBS, C2F_ROWS0 = 5;  // 4: conv2_fwd_body's channel quarters
-static_assert(C2F_JOBS == 4 || C2F_JOBS == 8, "fused conv2 jobs per sample");
+constexpr int C2F_ROWS0 = 5;
 __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(1, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
@@ -360,11 +357,17 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
 // [4 (j >> 2), +4 or +3) (28 / 21 positions, 2 MFMA row tiles instead of 3 +
 // the VALU position) x output channels [16 (j & 3), +16); each stages input
 // rows [4 (j >> 2), +6 or +5) of y2 (67 % / 56 %) after its hand-off wait.
-#ifndef DQZ_C3F_JOBS
-#define DQZ_C3F_JOBS 8
+constexpr int C3F_ROWS0 = 4;
+// fwd_conv_kernel runs conv2 / conv3 as 8 jobs per sample when the launch
+// has at most DQZ_FWD8_ZB samples (Z x B): with every block resident from
+// the start the launch is one latency chain per sample, and halving each
+// job's rows shortens it (the actor's and the MGSC one-transition forward);
+// at the learner's 64 samples the 4-job bodies are faster (fewer, fuller
+// MFMA row tiles and every conv2 block resident from the start).
+#ifndef DQZ_FWD8_ZB
+#define DQZ_FWD8_ZB 16
 #endif
-constexpr int C3F_JOBS = DQZ_C3F_JOBS, C3F_ROWS0 = 4;  // 4: conv3_fwd_body's channel quarters
-static_assert(C3F_JOBS == 4 || C3F_JOBS == 8, "fused conv3 jobs per sample");
+inline int fwd_conv_jobs(int zb) { return zb <= DQZ_FWD8_ZB ? 8 : 4; }
 __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
@@ -453,9 +456,9 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
 
 // ---- conv1 -> conv2 -> conv3 forward in one launch ------------------------
 // Grid, in dispatch order, over the Z x B samples s = z B + b:
-//   [conv1 4/sample] [conv2 4/sample] [conv3 4/sample]
+//   [conv1 4/sample] [conv2 J/sample] [conv3 J/sample], J = fwd_conv_jobs(Z B)
 // conv2 blocks of sample s wait for the 4 conv1 blocks of s (y1 hand-off),
-// conv3 blocks for the 4 conv2 blocks (y2).  Producers always have lower
+// conv3 blocks for the J conv2 blocks (y2).  Producers always have lower
 // block indices (workgroups are dispatched in index order), so every wait
 // terminates; each range starts at a multiple of 8, so a sample's producer
 // and consumer blocks share an XCD (and its L2).  Consumers stage their
@@ -476,20 +479,20 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
     return;
   }
   i -= n;
-  constexpr int n2f = C2F_JOBS / 4;  // conv2 range = n2f x n
-  if (i < n2f * n) {
-    const SampleJob sj = xcd_sample_job_at(i, C2F_JOBS, zb);
+  const int j2 = c2.jobs, j3 = c3.jobs;  // 4 or 8 per sample (fwd_conv_jobs)
+  if (i < (j2 / 4) * n) {
+    const SampleJob sj = xcd_sample_job_at(i, j2, zb);
     if (sj.valid) {
-      if constexpr (C2F_JOBS == 8)
+      if (j2 == 8)
         conv2_fwd8_body(c2, smem, sj);
       else
         conv2_fwd_body<true, true>(c2, smem, sj);
     }
     return;
   }
-  const SampleJob sj = xcd_sample_job_at(i - n2f * n, C3F_JOBS, zb);
+  const SampleJob sj = xcd_sample_job_at(i - (j2 / 4) * n, j3, zb);
   if (sj.valid) {
-    if constexpr (C3F_JOBS == 8)
+    if (j3 == 8)
       conv3_fwd8_body(c3, smem, sj);
     else
       conv3_fwd_body<true>(c3, smem, sj);

@@ -227,11 +227,13 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
     const int Bc = L->cfg.batch;
     int* hw = L->sync + 2 * Bc * Handoff::kStride;
     int* err = L->sync + 16 * Bc * Handoff::kStride;
-    c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, C2F_JOBS};
+    const int jobs = fwd_conv_jobs(Z * B);
+    c2.jobs = c3.jobs = jobs;
+    c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, jobs};
     c2.wait = c1.pub;
-    c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, C2F_JOBS, C3F_JOBS};
+    c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
     c3.wait = c2.pub;
-    const dim3 grid(xcd_grid(4, Z * B).x + xcd_grid(C2F_JOBS, Z * B).x + xcd_grid(C3F_JOBS, Z * B).x);
+    const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
     DQZ_PHASE(0, switch (src.fused) {
       case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
       case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
