@@ -387,7 +387,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
   DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
-  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(FLAT / 16), dim3(256), 0, st, fb);
+  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
             DQZ_HIP(hipGetLastError()));
 
   Conv3BwdArgs c3b;
