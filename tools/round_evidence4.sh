@@ -22,5 +22,5 @@ timeout -k 10 300 python bench.py --algo agent --steps 2000 --warmup 50 > $OUT/b
 bash tools/bench_median.sh $OUT/median > $OUT/bench_median5.json
 bash profiles/run_profile.sh ${TAG}_dqn
 bash profiles/run_pmc.sh $TAG
-timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_step.txt 2>&1
+DQZ_TRACE_PREBUILT=1 timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_step.txt 2>&1
 exit $rc

@@ -1,7 +1,7 @@
 """Per-kernel timeline of one learner step from in-kernel s_memrealtime stamps.
 
 usage (GPU box): [ALGO=dqn|double|per|mgsc] python tools/trace_step.py
-(builds libdqz_trace.so first)
+(builds libdqz_trace.so first, unless DQZ_TRACE_PREBUILT=1)
 Prints, per kernel in launch order: first-block start relative to the previous
 kernel's last-block end (the boundary), kernel span, median block lifetime and
 the median of the named intervals between stamps (10 ns ticks -> us).
@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')
 sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
-__graft_entry__._compile_lib(LIB, ['-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split()])  # pylint: disable=protected-access
+if os.environ.get('DQZ_TRACE_PREBUILT') != '1':  # 1: libdqz_trace.so was built beforehand (off the GPU box)
+  __graft_entry__._compile_lib(LIB, ['-DDQZ_TRACE', *os.environ.get('DQZ_TRACE_FLAGS', '').split()])  # pylint: disable=protected-access
 os.environ['DQZ_LIB'] = LIB
 from dqn_mgsc_zoo_amd import _native as _nat  # noqa: E402
 _nat.LIB_PATH = LIB  # imported by the build above, before DQZ_LIB was set
