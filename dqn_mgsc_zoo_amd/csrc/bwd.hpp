@@ -195,6 +195,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     const float4 v = src[(in ? ph * C3O + pw : 0) * 16 + (i & 15)];
     r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int i = t + 256 * q;
@@ -392,6 +393,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
       v = src[e];
     r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int i = t + 256 * q;

@@ -22,6 +22,12 @@
 
 namespace dqz {
 
+// 1: the conv2 / conv3 input-window loads are all issued before the first
+// LDS store (a scheduling barrier behind them)
+#ifndef DQZ_STAGE_SB
+#define DQZ_STAGE_SB 1
+#endif
+
 // 1: the mostly-empty last MFMA row tile of conv2 / conv3 forward and conv2
 // dX is replaced by VALU dot products of its few live positions
 #ifndef DQZ_TRIM
@@ -84,6 +90,10 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     else
       r[q] = src[min(t + 256 * q, NQ4 - 1)];
   }
+  // all 13 window loads in flight before the first LDS store (left alone the
+  // scheduler issued the 13th only after ten had returned: one more round
+  // trip after the hand-off)
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < 13; ++q) {
     const int i = t + 256 * q;
@@ -188,6 +198,7 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
   float4 r[NL + 1];
 #pragma unroll
   for (int q = 0; q <= NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q <= NL; ++q) {
     const int i = t + 256 * q;
@@ -282,6 +293,7 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     else
       r[q] = src[min(t + 256 * q, NQ4 - 1)];
   }
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const int i = t + 256 * q;
@@ -389,6 +401,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
   float4 r[NL];
 #pragma unroll
   for (int q = 0; q < NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
+  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < NL; ++q) {
     const int i = t + 256 * q;
@@ -524,103 +537,82 @@ struct Fc1FwdArgs {
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
-#ifndef DQZ_FC1_RG
-#define DQZ_FC1_RG 2
-#endif
 #ifndef DQZ_FC1_SB
 #define DQZ_FC1_SB 1
 #endif
-// RG row groups per block (RG = 2 when the batch has more than one, e.g. the
-// MGSC meta batch): both groups' MFMA chains run interleaved on the one W1
-// slice held in registers, so W1 is fetched MG / 2 times instead of MG times;
-// each group's sums are formed exactly as with RG = 1 (same bits).
-template <int RG>
+// SB (the learner's one-row-group launch, with DQZ_FC1_SB): every W1 / y3
+// load of the block is issued before the first MFMA, in the order the MFMAs
+// consume them (left alone the scheduler interleaves them with the MFMAs,
+// ~12 loads in flight per lane).  The meta-update's multi-row-group launches
+// keep the interleaved order, which measured faster there.
+template <bool SB>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
-  const int MGB = (a.MG + RG - 1) / RG;  // blocks per copy along the batch
-  const int z = zm / MGB, mg0 = RG * (zm % MGB);
+  const int z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
   const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
   constexpr int G = FC1_KW / 8;                         // 14
-  const float* x[RG];
-#pragma unroll
-  for (int r = 0; r < RG; ++r) x[r] = a.in + ((int64_t)z * a.B + min(32 * (mg0 + r) + c, a.B - 1)) * FLAT + k0;
-  // loads in the order the MFMAs consume them (vmcnt retires in order)
+  const int row = min(32 * mg + c, a.B - 1);
+  const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
-  float4 av[RG][G];
+  float4 av[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-#pragma unroll
-    for (int r = 0; r < RG; ++r) av[r][g] = *reinterpret_cast<const float4*>(x[r] + 8 * g);
+    av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   }
-#if DQZ_FC1_SB
-  // every W1 / y3 load of the block is issued before the first MFMA (left to
-  // itself the scheduler interleaves them, ~12 loads in flight per lane: a
-  // chain of dependent round trips); the MFMAs then wait per operand
-  __builtin_amdgcn_sched_barrier(0);
-#endif
-  f32x16 acc[RG];
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+  f32x16 acc = {};
 #pragma unroll
-  for (int r = 0; r < RG; ++r) acc[r] = f32x16{};
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].x, wr[g][0], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].y, wr[g][1], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].z, wr[g][2], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].w, wr[g][3], acc[r], 0, 0, 0);
-    }
-#pragma unroll
-  for (int r = 0; r < RG; ++r) {
-    const int mg = mg0 + r;
-    if (r > 0) __syncthreads();  // the previous group's readers of s_red are done
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s_red[w * FC1_32RW + ((k & 3) + 8 * (k >> 2) + 4 * h) * 33 + c] = acc[r][k];
-    __syncthreads();
-    // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
-    const int q = t >> 3, c4 = 4 * (t & 7);
-    const bool live = 32 * mg + q < a.B;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = q * 33 + c4 + e;
-      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
-    }
-    if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
-      float d = 0.f;
-      if (live) {
-        const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
-        d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
-      }
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      if (live && (t & 7) == 0)
-        a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
-    } else if (live) {
-      *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    }
+  for (int g = 0; g < G; ++g) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
+  __syncthreads();
+  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
+  const int q = t >> 3, c4 = 4 * (t & 7);
+  const bool live = 32 * mg + q < a.B;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = q * 33 + c4 + e;
+    v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+  }
+  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+    float d = 0.f;
+    if (live) {
+      const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
+      d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
+    }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (live && (t & 7) == 0)
+      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
+    return;
+  }
+  if (live)
+    *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
+        make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// RG of a launch: 1 for one row group (the learner's B <= 32), else DQZ_FC1_RG
-inline int fc1_fwd_rg(int MG) { return MG > 1 ? DQZ_FC1_RG : 1; }
 __device__ __forceinline__ void fc1_fwd_block(const Fc1FwdArgs& a, float* s_red, int i) {
-  if (a.MG > 1 && DQZ_FC1_RG == 2)
-    fc1_fwd_block32<2>(a, s_red, i);
+  if (DQZ_FC1_SB && a.MG == 1)
+    fc1_fwd_block32<true>(a, s_red, i);
   else
-    fc1_fwd_block32<1>(a, s_red, i);
+    fc1_fwd_block32<false>(a, s_red, i);
 }
 
-inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * ((MG + fc1_fwd_rg(MG) - 1) / fc1_fwd_rg(MG)); }
+inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
