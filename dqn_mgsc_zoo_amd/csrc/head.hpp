@@ -385,12 +385,18 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stri
       a[u].y += v.y;
     }
   }
+  // the tail without branches: each load is unconditional (clamped to the
+  // last slab) and its sum selected, so all eight are in flight together (a
+  // conditional load per branch waited for each one in turn)
+  float2 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(p + (int64_t)min(s + u * G, S - 1) * stride + j);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < 8; ++u)
     if (s + u * G < S) {
-      const float2 v = *reinterpret_cast<const float2*>(p + (int64_t)(s + u * G) * stride + j);
-      a[u].x += v.x;
-      a[u].y += v.y;
+      a[u].x += v[u].x;
+      a[u].y += v[u].y;
     }
   return make_float2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
                      ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
@@ -398,26 +404,62 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stri
 
 // One gradient element of the small head leaves (fc1/b, fc2/w, fc2/b): this
 // thread's share (samples grp, grp + G, ...) and its destination offset.
+// Eight samples' operands are loaded per round (unconditional, clamped to the
+// last sample) before any is summed, so they are in flight together; the
+// sum keeps the sample order.
 __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp, int64_t& dst) {
+  constexpr int G = UPD_GROUPS, R = 8;
   float g = 0.f;
   if (e < HID) {  // fc1 bias: sum_b dz1
     const int j = (int)e;
-#pragma unroll 4
-    for (int b = grp; b < u.B; b += UPD_GROUPS) g += u.dz1[(int64_t)b * HID + j];
+    for (int b0 = grp; b0 < u.B; b0 += R * G) {
+      float x[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = u.dz1[(int64_t)min(b0 + r * G, u.B - 1) * HID + j];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (b0 + r * G < u.B) g += x[r];
+    }
     dst = u.off[7] + j;
   } else if (e < HID + (int64_t)HID * u.A) {  // fc2 w[j][a] = sum_{b: a_b = a} h1[b][j] gq[b]
     const int64_t jj = e - HID;
     const int j = (int)(jj / u.A), a = (int)(jj % u.A);
-#pragma unroll 4
-    for (int b = grp; b < u.B; b += UPD_GROUPS) {
-      const float v = u.h1[(int64_t)b * HID + j] * u.gq[b];
-      g += u.ga[b] == a ? v : 0.f;
+    for (int b0 = grp; b0 < u.B; b0 += R * G) {
+      float h[R], q[R];
+      int32_t act[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = min(b0 + r * G, u.B - 1);
+        h[r] = u.h1[(int64_t)b * HID + j];
+        q[r] = u.gq[b];
+        act[r] = u.ga[b];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (b0 + r * G < u.B) {
+          const float v = h[r] * q[r];
+          g += act[r] == a ? v : 0.f;
+        }
     }
     dst = u.off[8] + jj;
   } else if (e < HID + (int64_t)HID * u.A + u.nb2) {  // fc2 b
     const int a = (int)(e - HID - (int64_t)HID * u.A);
-#pragma unroll 4
-    for (int b = grp; b < u.B; b += UPD_GROUPS) g += (u.nb2 == 1 || u.ga[b] == a) ? u.gq[b] : 0.f;
+    for (int b0 = grp; b0 < u.B; b0 += R * G) {
+      float q[R];
+      int32_t act[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = min(b0 + r * G, u.B - 1);
+        q[r] = u.gq[b];
+        act[r] = u.ga[b];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (b0 + r * G < u.B) g += (u.nb2 == 1 || act[r] == a) ? q[r] : 0.f;
+    }
     dst = u.off[9] + a;
   }
   return g;
@@ -435,30 +477,40 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
   const int64_t nsmall = HID + (int64_t)HID * u.A + u.nb2;
   const int small_blocks = (int)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS);
   const int64_t c1 = u.sz[0] + u.sz[1], c2 = c1 + u.sz[2] + u.sz[3], c3 = c2 + u.sz[4] + u.sz[5];
-  float loss = 0.f;
+  // block 0 wave 0: the batch loss partials (unconditional clamped loads,
+  // summed below in sample order; a guarded loop waited for them here)
+  constexpr int LR = (MAXB + 63) / 64;
+  float lv[LR];
   if (blk == 0 && threadIdx.x < 64) {
-    for (int b = threadIdx.x; b < u.B; b += 64) loss += u.loss_part[b];
+#pragma unroll
+    for (int r = 0; r < LR; ++r) lv[r] = u.loss_part[min((int)threadIdx.x + 64 * r, u.B - 1)];
   }
+  // destination offsets first (no loads), then the RMSProp / meta operands
+  // of grp 0, then the partial sums: the operands are in flight under the
+  // reduction's loads instead of a round trip after them
   int64_t dst[2] = {-1, -1};
-  float2 g = make_float2(0.f, 0.f);
-  if ((int)blk < small_blocks) {
-    const int64_t e = (int64_t)blk * UPD_PARAMS + 2 * pl;
-    g.x = small_grad(u, e, grp, dst[0]);
-    g.y = small_grad(u, e + 1, grp, dst[1]);
-  } else {
-    const int64_t j = (int64_t)(blk - small_blocks) * UPD_PARAMS + 2 * pl;  // even; regions are even-sized
-    if (j < c1) {  // conv1: w rows 0..255, bias row 256
-      g = sum_split2(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, j, grp);
-      for (int h = 0; h < 2; ++h) dst[h] = j + h < u.sz[0] ? u.off[0] + j + h : u.off[1] + (j + h - u.sz[0]);
-    } else if (j < c2) {
-      const int64_t k = j - c1;
-      g = sum_split2(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, k, grp);
-      for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[2] ? u.off[2] + k + h : u.off[3] + (k + h - u.sz[2]);
-    } else if (j < c3) {
-      const int64_t k = j - c2;
-      g = sum_split2(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, k, grp);
-      for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[4] ? u.off[4] + k + h : u.off[5] + (k + h - u.sz[4]);
+  const bool small = (int)blk < small_blocks;
+  const int64_t e = small ? (int64_t)blk * UPD_PARAMS + 2 * pl
+                          : (int64_t)(blk - small_blocks) * UPD_PARAMS + 2 * pl;  // even; regions are even-sized
+  if (small) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t f = e + h;
+      if (f < HID)
+        dst[h] = u.off[7] + f;
+      else if (f < HID + (int64_t)HID * u.A)
+        dst[h] = u.off[8] + (f - HID);
+      else if (f < nsmall)
+        dst[h] = u.off[9] + (f - HID - (int64_t)HID * u.A);
     }
+  } else if (e < c1) {  // conv1: w rows 0..255, bias row 256
+    for (int h = 0; h < 2; ++h) dst[h] = e + h < u.sz[0] ? u.off[0] + e + h : u.off[1] + (e + h - u.sz[0]);
+  } else if (e < c2) {
+    const int64_t k = e - c1;
+    for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[2] ? u.off[2] + k + h : u.off[3] + (k + h - u.sz[2]);
+  } else if (e < c3) {
+    const int64_t k = e - c2;
+    for (int h = 0; h < 2; ++h) dst[h] = k + h < u.sz[4] ? u.off[4] + k + h : u.off[5] + (k + h - u.sz[4]);
   }
   const Rms& R = u.rms;
   float o_th[2] = {0.f, 0.f}, o_mu[2] = {0.f, 0.f}, o_nu[2] = {0.f, 0.f};
@@ -476,8 +528,24 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         o_nu[h] = pn[dst[h]];
       }
   }
+  float2 g = make_float2(0.f, 0.f);
+  int64_t unused;
+  if (small) {
+    g.x = small_grad(u, e, grp, unused);
+    g.y = small_grad(u, e + 1, grp, unused);
+  } else if (e < c1) {
+    g = sum_split2(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
+  } else if (e < c2) {
+    g = sum_split2(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
+  } else if (e < c3) {
+    g = sum_split2(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
+  }
   s_part[grp][pl] = g;
   if (blk == 0 && threadIdx.x < 64) {
+    float loss = 0.f;
+#pragma unroll
+    for (int r = 0; r < LR; ++r)
+      if ((int)threadIdx.x + 64 * r < u.B) loss += lv[r];
     loss = wave_sum(loss);
     if (threadIdx.x == 0) {
       u.loss[0] = loss / (float)u.B;
