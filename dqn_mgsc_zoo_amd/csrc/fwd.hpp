@@ -537,15 +537,6 @@ struct Fc1FwdArgs {
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
-#ifndef DQZ_FC1_SB
-#define DQZ_FC1_SB 1
-#endif
-// SB (the learner's one-row-group launch, with DQZ_FC1_SB): every W1 / y3
-// load of the block is issued before the first MFMA, in the order the MFMAs
-// consume them (left alone the scheduler interleaves them with the MFMAs,
-// ~12 loads in flight per lane).  The meta-update's multi-row-group launches
-// keep the interleaved order, which measured faster there.
-template <bool SB>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
@@ -566,7 +557,6 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   }
-  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   f32x16 acc = {};
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -605,19 +595,12 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
         make_float4(v[0], v[1], v[2], v[3]);
 }
 
-__device__ __forceinline__ void fc1_fwd_block(const Fc1FwdArgs& a, float* s_red, int i) {
-  if (DQZ_FC1_SB && a.MG == 1)
-    fc1_fwd_block32<true>(a, s_red, i);
-  else
-    fc1_fwd_block32<false>(a, s_red, i);
-}
-
 inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_32RW];
-  fc1_fwd_block(a, s_red, blockIdx.x);
+  fc1_fwd_block32(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
     if (ex.part && sj.job == 0) meta_extra_term(ex, sj.s, smem);
     return;
   }
-  fc1_fwd_block(f1, smem, i - n);
+  fc1_fwd_block32(f1, smem, i - n);
 }
 
 struct MetaRmsArgs {
