@@ -534,102 +534,68 @@ struct Fc1FwdArgs {
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
-  int pair = 0;     // 1: copies 0 and 2 share a buffer and one block (fc1_fwd_block32)
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
-// Rows [32 mg, 32 mg + 32) of NZ network copies zs[0..NZ) that share one
-// parameter buffer (the double-Q / PER launch's online copies at s_tm1 and
-// s_t: their W1 slice is fetched once for both).
-template <int NZ>
-__device__ __forceinline__ void fc1_fwd_tile(const Fc1FwdArgs& a, float* s_red, int nt, int s, int mg,
-                                             const int (&zs)[NZ]) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
-  const float* W = a.nz.p[zs[0]] + a.w_off + 32 * nt + c;  // [3136][512]
-  constexpr int G = FC1_KW / 8;                             // 14
-  const int row = min(32 * mg + c, a.B - 1);
-  float wr[G][4];
-  float4 av[NZ][G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-#pragma unroll
-    for (int r = 0; r < NZ; ++r)
-      av[r][g] = *reinterpret_cast<const float4*>(a.in + ((int64_t)zs[r] * a.B + row) * FLAT + k0 + 8 * g);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
-  }
-  f32x16 acc[NZ];
-#pragma unroll
-  for (int r = 0; r < NZ; ++r) acc[r] = f32x16{};
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int r = 0; r < NZ; ++r) {
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].x, wr[g][0], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].y, wr[g][1], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].z, wr[g][2], acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][g].w, wr[g][3], acc[r], 0, 0, 0);
-    }
-  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
-  const int q = t >> 3, c4 = 4 * (t & 7);
-  const bool live = 32 * mg + q < a.B;
-#pragma unroll
-  for (int r = 0; r < NZ; ++r) {
-    if (r > 0) __syncthreads();  // the previous copy's readers of s_red are done
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s_red[w * FC1_32RW + ((k & 3) + 8 * (k >> 2) + 4 * h) * 33 + c] = acc[r][k];
-    __syncthreads();
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = q * 33 + c4 + e;
-      v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
-    }
-    if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
-      float d = 0.f;
-      if (live) {
-        const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
-        d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
-      }
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      if (live && (t & 7) == 0)
-        a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
-    } else if (live) {
-      *reinterpret_cast<float4*>(a.part + (((int64_t)zs[r] * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    }
-  }
-}
-
-// Block i of the fc1 launch: column tile nt, K split s, then the copy (and
-// row group).  With a.pair (Z = 3, one row group, copies 0 and 2 on the
-// online buffer) the copies are {0, 2} and {1}: 224 blocks instead of 336.
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
-  if (a.pair) {
-    if (zm == 0) {
-      const int zs[2] = {0, 2};
-      fc1_fwd_tile<2>(a, s_red, nt, s, 0, zs);
-    } else {
-      const int zs[1] = {1};
-      fc1_fwd_tile<1>(a, s_red, nt, s, 0, zs);
+  const int z = zm / a.MG, mg = zm % a.MG;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
+  const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
+  constexpr int G = FC1_KW / 8;                         // 14
+  const int row = min(32 * mg + c, a.B - 1);
+  const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
+  float wr[G][4];
+  float4 av[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
+  }
+  f32x16 acc = {};
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].x, wr[g][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].y, wr[g][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].z, wr[g][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[g].w, wr[g][3], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
+  __syncthreads();
+  // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
+  const int q = t >> 3, c4 = 4 * (t & 7);
+  const bool live = 32 * mg + q < a.B;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = q * 33 + c4 + e;
+    v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
+  }
+  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+    float d = 0.f;
+    if (live) {
+      const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
+      d = (v[0] * dz.x + v[1] * dz.y) + (v[2] * dz.z + v[3] * dz.w);
     }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (live && (t & 7) == 0)
+      a.dot.part[(int64_t)(32 * mg + q) * META_DOT_SLOTS + a.dot.slot0 + nt * FC1_S + s] = d;
     return;
   }
-  const int zs[1] = {zm / a.MG};
-  fc1_fwd_tile<1>(a, s_red, nt, s, zm % a.MG, zs);
+  if (live)
+    *reinterpret_cast<float4*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c4) =
+        make_float4(v[0], v[1], v[2], v[3]);
 }
 
-#ifndef DQZ_FC1_PAIR
-#define DQZ_FC1_PAIR 1
-#endif
-inline int fc1_fwd_blocks(int Z, int MG, bool pair = false) { return (HID / 32) * FC1_S * (pair ? 2 : Z * MG); }
+inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
