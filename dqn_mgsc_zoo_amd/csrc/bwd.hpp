@@ -195,7 +195,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     const float4 v = src[(in ? ph * C3O + pw : 0) * 16 + (i & 15)];
     r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int i = t + 256 * q;
@@ -393,7 +393,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
       v = src[e];
     r[q] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int i = t + 256 * q;
@@ -408,8 +408,8 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   __syncthreads();
   DQZ_STAMP(7, 1);
-  // 100 pixels = 6 MFMA row tiles + pixels 96..99 on the VALU (fwd.hpp DQZ_TRIM)
-  constexpr int MT = DQZ_TRIM ? 6 : 7;
+  // 100 pixels = 6 MFMA row tiles + pixels 96..99 on the VALU (fwd.hpp's trim)
+  constexpr int MT = 6;
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -426,13 +426,13 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     const int off = (tp >> 1) * C2X_RS + (tp & 1) * C2X_S + 4 * (kk & 3);
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
-    if constexpr (DQZ_TRIM) {
+    {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + 16 * w + kq + off], wr[kk], last[e]);
     }
   }
-  if constexpr (DQZ_TRIM) {
+  {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       last[e] += __shfl_xor(last[e], 16, 64);
@@ -446,7 +446,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
-  if (DQZ_TRIM && kq == 0) {
+  if (kq == 0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) s_red[w * 1792 + (96 + e) * 16 + n] = last[e];
   }

@@ -22,17 +22,8 @@
 
 namespace dqz {
 
-// 1: the conv2 / conv3 input-window loads are all issued before the first
-// LDS store (a scheduling barrier behind them)
-#ifndef DQZ_STAGE_SB
-#define DQZ_STAGE_SB 1
-#endif
-
-// 1: the mostly-empty last MFMA row tile of conv2 / conv3 forward and conv2
-// dX is replaced by VALU dot products of its few live positions
-#ifndef DQZ_TRIM
-#define DQZ_TRIM 1
-#endif
+// The mostly-empty last MFMA row tile of conv2 / conv3 forward and conv2 dX
+// ("trim") is replaced by VALU dot products of its few live positions.
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -43,11 +34,8 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // lanes kq = 0 / 1 (one ds_write_b32 lane group) 16 banks apart instead of on
 // the same banks; a 32-lane read group covers rows 2j, 2j + 1 of one 4-row
 // block, so the position-major reads stay conflict-free.
-#ifndef DQZ_RED_PAD
-#define DQZ_RED_PAD 1
-#endif
-__device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + (DQZ_RED_PAD ? 16 * (row >> 2) : 0) + col; }
-constexpr int red_rows(int rows) { return rows * 16 + (DQZ_RED_PAD ? 16 * ((rows + 3) / 4) : 0); }
+__device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + 16 * (row >> 2) + col; }
+constexpr int red_rows(int rows) { return rows * 16 + 16 * ((rows + 3) / 4); }
 
 struct LayerFwdArgs {
   const float* in;  // [Z][B][...] layer input (NHWC)
@@ -93,7 +81,7 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   // all 13 window loads in flight before the first LDS store (left alone the
   // scheduler issued the 13th only after ten had returned: one more round
   // trip after the hand-off)
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < 13; ++q) {
     const int i = t + 256 * q;
@@ -110,7 +98,7 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   __syncthreads();
   // 81 positions = 5 MFMA row tiles + position 80, which every lane folds
   // from its own weight registers on the VALU (a 6th tile would be 1/16 live)
-  constexpr int MT = DQZ_TRIM ? 5 : 6;
+  constexpr int MT = 5;
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -127,10 +115,10 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     const int off = (kk >> 3) * C2L_S + 4 * (kk & 7);  // kw, ci block
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
-    if constexpr (DQZ_TRIM) last = __fmaf_rn(s_in[blast + off], wr[kk], last);
+    last = __fmaf_rn(s_in[blast + off], wr[kk], last);
   }
   DQZ_STAMP(1, 2);
-  if constexpr (DQZ_TRIM) {
+  {
     last += __shfl_xor(last, 16, 64);
     last += __shfl_xor(last, 32, 64);
   }
@@ -142,7 +130,7 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
-  if (DQZ_TRIM && kq == 0) s_red[w * RW + red_idx(C2M - 1, n)] = last;
+  if (kq == 0) s_red[w * RW + red_idx(C2M - 1, n)] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
@@ -198,7 +186,7 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
   float4 r[NL + 1];
 #pragma unroll
   for (int q = 0; q <= NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q <= NL; ++q) {
     const int i = t + 256 * q;
@@ -293,7 +281,7 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     else
       r[q] = src[min(t + 256 * q, NQ4 - 1)];
   }
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const int i = t + 256 * q;
@@ -309,7 +297,7 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   DQZ_STAMP(2, 1);
   __syncthreads();
   // 49 positions = 3 MFMA row tiles + position 48 on the VALU (see conv2)
-  constexpr int MT = DQZ_TRIM ? 3 : 4;
+  constexpr int MT = 3;
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -327,10 +315,10 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     const int off = (tap / 3) * C3L_RS + (tap % 3) * C3L_S + 4 * (kk & 3);
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_in[base[m] + off], wr[kk], acc[m]);
-    if constexpr (DQZ_TRIM) last = __fmaf_rn(s_in[blast + off], wr[kk], last);
+    last = __fmaf_rn(s_in[blast + off], wr[kk], last);
   }
   DQZ_STAMP(2, 2);
-  if constexpr (DQZ_TRIM) {
+  {
     last += __shfl_xor(last, 16, 64);
     last += __shfl_xor(last, 32, 64);
   }
@@ -342,7 +330,7 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
-  if (DQZ_TRIM && kq == 0) s_red[w * RW + red_idx(C3M - 1, n)] = last;
+  if (kq == 0) s_red[w * RW + red_idx(C3M - 1, n)] = last;
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
@@ -371,15 +359,13 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
 // rows [4 (j >> 2), +6 or +5) of y2 (67 % / 56 %) after its hand-off wait.
 constexpr int C3F_ROWS0 = 4;
 // fwd_conv_kernel runs conv2 / conv3 as 8 jobs per sample when the launch
-// has at most DQZ_FWD8_ZB samples (Z x B): with every block resident from
+// has at most kFwd8MaxSamples samples (Z x B): with every block resident from
 // the start the launch is one latency chain per sample, and halving each
 // job's rows shortens it (the actor's and the MGSC one-transition forward);
 // at the learner's 64 samples the 4-job bodies are faster (fewer, fuller
 // MFMA row tiles and every conv2 block resident from the start).
-#ifndef DQZ_FWD8_ZB
-#define DQZ_FWD8_ZB 16
-#endif
-inline int fwd_conv_jobs(int zb) { return zb <= DQZ_FWD8_ZB ? 8 : 4; }
+constexpr int kFwd8MaxSamples = 16;
+inline int fwd_conv_jobs(int zb) { return zb <= kFwd8MaxSamples ? 8 : 4; }
 __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
@@ -401,7 +387,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
   float4 r[NL];
 #pragma unroll
   for (int q = 0; q < NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
-  if constexpr (DQZ_STAGE_SB) __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
 #pragma unroll
   for (int q = 0; q < NL; ++q) {
     const int i = t + 256 * q;
