@@ -46,6 +46,20 @@ def run(plan):
       graphs[k].replay()
 
 
+from dqn_mgsc_zoo_amd import replicas as replicas_lib  # noqa: E402
+reps_nccl = replicas_lib.Replicas('nccl')  # a world-1 RCCL group, as bench.py forms
+import torch.distributed as dist  # noqa: E402
+gloo = dist.new_group(backend='gloo')
+
+
+def barrier_nccl():
+  dist.barrier()
+
+
+def barrier_gloo():
+  dist.barrier(group=gloo)
+
+
 out = {}
 t = []
 for _ in range(REPS):
@@ -54,11 +68,15 @@ for _ in range(REPS):
   torch.cuda.synchronize()
   t.append(time.perf_counter() - t0)
 out['empty_sync_ms'] = round(1e3 * statistics.median(t), 4)
-for name, plan in plans.items():
+cases = [(name, plan, None) for name, plan in plans.items()]
+cases += [('20+rccl_barrier', [20], barrier_nccl), ('20+gloo_barrier', [20], barrier_gloo)]
+for name, plan, bar in cases:
   host, ev = [], []
   for _ in range(REPS):
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    if bar is not None:
+      bar()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record()
