@@ -244,10 +244,12 @@ def test_fused_uniform_step_matches_sample_then_step(device):
 
 
 @pytest.mark.parametrize('algo,batch,num_actions', [
-    ('dqn', 1, 6), ('dqn', 20, 18), ('double', 48, 4), ('per', 40, 18)])
+    ('dqn', 1, 6), ('dqn', 8, 6), ('double', 5, 6), ('dqn', 20, 18), ('double', 48, 4), ('per', 40, 18)])
 def test_learner_step_odd_shapes(device, algo, batch, num_actions):
   """Batches that are not multiples of the 8-XCD / 16-row / 32-row tilings,
-  and the full 18-action set (head kernel AMAX 32 path)."""
+  the full 18-action set (head kernel AMAX 32 path), and launches of at most
+  16 samples (Z x B: dqn 1 and 8, double 5), whose forward runs conv2 / conv3
+  as 8 jobs per sample (fwd.hpp fwd_conv_jobs)."""
   net, lrn, st, host, online, target, mu, nu = _setup(
       algo, batch, capacity=96, num_frames=260, num_actions=num_actions,
       seed=31 + batch)
@@ -275,7 +277,7 @@ def test_learner_step_odd_shapes(device, algo, batch, num_actions):
 
 
 @pytest.mark.parametrize('algo,batch', [('dqn', 32), ('per', 20), ('double', 64),
-                                        ('dqn', 33)])
+                                        ('dqn', 33), ('dqn', 8)])
 def test_handoff_kernels_bit_reproducible(device, algo, batch):
   """The in-launch hand-offs (bwd_bc_kernel: conv3 dX -> conv2 dX / conv2 dW,
   conv2 dX -> conv1 dW) sum in fixed orders, whichever workgroup arrives
