@@ -118,25 +118,12 @@ __device__ __forceinline__ void meta_extra_term(const MetaExtra& e, int b, float
 }
 
 static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's 32 x 32 tiles fit the tangent launch's LDS");
-#ifndef DQZ_TAN_FC1_FIRST
-#define DQZ_TAN_FC1_FIRST 1
-#endif
 inline int tangent_fwd_blocks(int B, int MG) { return 3 * 4 * ((B + 7) / 8 * 8) + fc1_fwd_blocks(1, MG); }
 __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
                                                           Fc1FwdArgs f1, MetaExtra ex) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int n = 4 * ((c1.B + 7) / 8 * 8);
   int i = blockIdx.x;
-#if DQZ_TAN_FC1_FIRST
-  // the fc1 range first: its blocks run longest, so the short conv blocks
-  // fill the launch's tail instead of the fc1 blocks ending it
-  const int nf = (HID / 32) * FC1_S * f1.MG;  // fc1_fwd_blocks(1, MG)
-  if (i < nf) {
-    fc1_fwd_block32(f1, smem, i);
-    return;
-  }
-  i -= nf;
-#endif
   if (i < n) {
     const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, c1.B);
     if (sj.valid) conv1_fwd_body<false, 0>(c1, smem, sj);
@@ -156,9 +143,7 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
     if (ex.part && sj.job == 0) meta_extra_term(ex, sj.s, smem);
     return;
   }
-#if !DQZ_TAN_FC1_FIRST
   fc1_fwd_block32(f1, smem, i - n);
-#endif
 }
 
 struct MetaRmsArgs {
