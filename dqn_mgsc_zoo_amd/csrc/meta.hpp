@@ -295,7 +295,6 @@ __device__ __forceinline__ float meta_s(const MetaAdamArgs& a, int i) {
   float4 r[META_DOT_SLOTS / 4];
 #pragma unroll
   for (int k = 0; k < META_DOT_SLOTS / 4; ++k) r[k] = q[k];
-  __builtin_amdgcn_sched_barrier(0);  // all 32 loads in flight before the first add
   float acc = 0.f;
 #pragma unroll
   for (int k = 0; k < META_DOT_SLOTS / 4; ++k) {
@@ -309,83 +308,47 @@ __device__ __forceinline__ float meta_s(const MetaAdamArgs& a, int i) {
   return acc;
 }
 
-// Adam step of entry i (g formed from s_i and the batch total).
-__device__ __forceinline__ float meta_adam_entry(const MetaAdamArgs& a, int i, float si, float tot, float pi,
-                                                 float mi, float vi, float xi, int posi, float c1, float c2,
-                                                 const LogitRun& r, double& dS, int* s_far) {
-  const float g = si - pi * tot;
-  const float m = (1.f - a.b1) * g + a.b1 * mi;
-  const float v = (1.f - a.b2) * (g * g) + a.b2 * vi;
-  const float mh = m / c1;
-  const float vh = v / c2;
-  a.m[i] = m;
-  a.v[i] = v;
-  a.dlogits[i] = g;
-  const float nx = xi + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
-  a.logits[posi] = nx;
-  if (r.valid) {
-    dS += run_term(nx, r.c) - run_term(xi, r.c);
-    if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) *s_far = 1;
-    a.dirty[posi / SM_CHUNK] = 1;
-  }
-  return nx;
-}
-
 __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __shared__ float sbuf[META_THREADS / 64];
+  float st = 0.f;
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += meta_s(a, i);
+  const float tot = block_sum_f32(st, sbuf);
+  float lp = 0.f;
+  for (int j = threadIdx.x; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+  lp = block_sum_f32(lp, sbuf);
+  const int32_t cnt = *a.count + 1;
+  const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
   __shared__ double dbuf[META_THREADS / 64];
   __shared__ int s_far;
-  const int t = threadIdx.x;
-  if (t == 0) s_far = 0;
-  double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
+  if (threadIdx.x == 0) s_far = 0;
   LogitRun r{0.0, 0.f, 0};
-  float lp = 0.f;
-  int32_t cnt;
-  if (a.M <= META_THREADS) {
-    // one entry per thread: every operand (the entry's p, m, v, x, pos, the
-    // loss partials, the step count, the running sum) is issued with the
-    // s_i partials, ahead of the first reduction, so the launch pays one
-    // memory round trip instead of four (same arithmetic, same bits)
-    const bool on = t < a.M;
-    float pi = 0.f, mi = 0.f, vi = 0.f, xi = 0.f;
-    int posi = 0;
-    if (on) {
-      pi = a.p[t];
-      mi = a.m[t];
-      vi = a.v[t];
-      xi = a.x[t];
-      posi = a.pos[t];
+  if (a.run) r = *a.run;
+  __syncthreads();
+  double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
+  for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
+    const float g = (a.dot_part ? a.s_out[i] : a.s[i]) - a.p[i] * tot;
+    const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
+    const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
+    const float mh = m / c1;
+    const float vh = v / c2;
+    a.m[i] = m;
+    a.v[i] = v;
+    a.dlogits[i] = g;
+    const float nx = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+    a.logits[a.pos[i]] = nx;
+    if (r.valid) {
+      dS += run_term(nx, r.c) - run_term(a.x[i], r.c);
+      if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
+      a.dirty[a.pos[i] / SM_CHUNK] = 1;
     }
-    for (int j = t; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
-    cnt = *a.count + 1;
-    if (a.run) r = *a.run;
-    const float si = on ? meta_s(a, t) : 0.f;
-    const float tot = block_sum_f32(si, sbuf);
-    lp = block_sum_f32(lp, sbuf);
-    const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
-    if (on) meta_adam_entry(a, t, si, tot, pi, mi, vi, xi, posi, c1, c2, r, dS, &s_far);
-  } else {
-    float st = 0.f;
-    for (int i = t; i < a.M; i += META_THREADS) st += meta_s(a, i);
-    const float tot = block_sum_f32(st, sbuf);
-    for (int j = t; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
-    lp = block_sum_f32(lp, sbuf);
-    cnt = *a.count + 1;
-    const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
-    if (a.run) r = *a.run;
-    // thread i handles entry i in both loops, so it reads back its own s_out store
-    for (int i = t; i < a.M; i += META_THREADS)
-      meta_adam_entry(a, i, a.dot_part ? a.s_out[i] : a.s[i], tot, a.p[i], a.m[i], a.v[i], a.x[i], a.pos[i], c1,
-                      c2, r, dS, &s_far);
   }
   // the buffer's running log-sum-exp follows the M writes (what
   // dqz_logits_write does for them) and their chunks are flagged, so the next
   // add / sample needs no scan; a tripped guard re-seeds here (rare)
   if (a.run && r.valid) {
     __shared__ int s_reseed;
-    __syncthreads();  // s_far
     dS = block_sum_f64(dS, dbuf);  // fixed order: deterministic
-    if (t == 0) {
+    if (threadIdx.x == 0) {
       const double before = r.S;
       r.S += dS;
       s_reseed = s_far || !run_ok(before, r.S, -INFINITY, r.c);
@@ -395,10 +358,10 @@ __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
     if (s_reseed) {
       block_rescan(a.logits, a.n_logits, a.run);
       const int nb = (int)((a.n_logits + SM_CHUNK - 1) / SM_CHUNK);
-      for (int k = t; k < nb; k += META_THREADS) a.dirty[k] = 1;
+      for (int k = threadIdx.x; k < nb; k += META_THREADS) a.dirty[k] = 1;
     }
   }
-  if (t == 0) {
+  if (threadIdx.x == 0) {
     *a.count = cnt;
     *a.loss = lp;
   }
