@@ -180,21 +180,14 @@ __global__ __launch_bounds__(256) void hvp_t4_kernel(HvpArgs a) {
   const int t = threadIdx.x, c = blockIdx.x;
   const float *W = a.th + a.off[6], *Wd = a.tw + a.off[6];
   float2 z = make_float2(0.f, 0.f);
-  float2 w[HVP_T4_KC], wd[HVP_T4_KC];
-  float y[HVP_T4_KC], ty[HVP_T4_KC];
 #pragma unroll
   for (int j = 0; j < HVP_T4_KC; ++j) {
     const int k = c * HVP_T4_KC + j;
-    w[j] = *reinterpret_cast<const float2*>(W + (int64_t)k * HID + 2 * t);
-    wd[j] = *reinterpret_cast<const float2*>(Wd + (int64_t)k * HID + 2 * t);
-    y[j] = a.y3[k];
-    ty[j] = a.ty3[k];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // every row's loads in flight before the first product
-#pragma unroll
-  for (int j = 0; j < HVP_T4_KC; ++j) {
-    z.x += y[j] * wd[j].x + ty[j] * w[j].x;
-    z.y += y[j] * wd[j].y + ty[j] * w[j].y;
+    const float2 w = *reinterpret_cast<const float2*>(W + (int64_t)k * HID + 2 * t);
+    const float2 wd = *reinterpret_cast<const float2*>(Wd + (int64_t)k * HID + 2 * t);
+    const float y = a.y3[k], ty = a.ty3[k];
+    z.x += y * wd.x + ty * w.x;
+    z.y += y * wd.y + ty * w.y;
   }
   *reinterpret_cast<float2*>(a.part + (int64_t)c * HID + 2 * t) = z;
   if (c == 0) {
@@ -232,28 +225,21 @@ __global__ __launch_bounds__(256) void hvp_b2_kernel(HvpArgs a) {
   __shared__ float s_r[16][17];
   const int t = threadIdx.x, pix = blockIdx.x, g = blockIdx.y;
   const int ih = pix / C2O, iw = pix % C2O, cs = t & 15, cl = t >> 4, ci = 16 * g + cl;
-  // every tap's operands are loaded (clamped to a live tap) before the first
-  // product, then the live taps are summed in (kh, kw) order as before
-  float4 w[C3K * C3K], wd[C3K * C3K], d[C3K * C3K], dd[C3K * C3K];
-#pragma unroll
-  for (int tp = 0; tp < C3K * C3K; ++tp) {
-    const int kh = tp / C3K, kw = tp % C3K;
-    const int oh = min(max(ih - kh, 0), C3O - 1), ow = min(max(iw - kw, 0), C3O - 1);
-    const int src = (oh * C3O + ow) * C3CO + 4 * cs;
-    const int64_t wi = ((kh * C3K + kw) * C3CI + ci) * C3CO + 4 * cs;
-    w[tp] = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
-    wd[tp] = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
-    d[tp] = *reinterpret_cast<const float4*>(a.d3 + src);
-    dd[tp] = *reinterpret_cast<const float4*>(a.td3 + src);
-  }
-  __builtin_amdgcn_sched_barrier(0);
   float z = 0.f;
-#pragma unroll
-  for (int tp = 0; tp < C3K * C3K; ++tp) {
-    const int oh = ih - tp / C3K, ow = iw - tp % C3K;
-    if (oh >= 0 && oh < C3O && ow >= 0 && ow < C3O)
-      z += ((d[tp].x * wd[tp].x + dd[tp].x * w[tp].x) + (d[tp].y * wd[tp].y + dd[tp].y * w[tp].y)) +
-           ((d[tp].z * wd[tp].z + dd[tp].z * w[tp].z) + (d[tp].w * wd[tp].w + dd[tp].w * w[tp].w));
+  for (int kh = 0; kh < C3K; ++kh) {
+    const int oh = ih - kh;
+    if (oh < 0 || oh >= C3O) continue;
+    for (int kw = 0; kw < C3K; ++kw) {
+      const int ow = iw - kw;
+      if (ow < 0 || ow >= C3O) continue;
+      const int src = (oh * C3O + ow) * C3CO + 4 * cs;
+      const int64_t wi = ((kh * C3K + kw) * C3CI + ci) * C3CO + 4 * cs;
+      const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
+      const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
+      const float4 d = *reinterpret_cast<const float4*>(a.d3 + src);
+      const float4 dd = *reinterpret_cast<const float4*>(a.td3 + src);
+      z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) + ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
+    }
   }
   s_r[cl][cs] = z;
   __syncthreads();
@@ -273,33 +259,25 @@ __global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
   __shared__ float s_r[C2CI][9];
   const int t = threadIdx.x, pix = blockIdx.x;
   const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
-  // the (at most) 2 x 2 live taps: every operand loaded (clamped) before the
-  // first product, then the live taps summed in (kh, kw, h) order as before
-  float4 w[4][2], wd[4][2], d[4][2], dd[4][2];
-#pragma unroll
-  for (int tp = 0; tp < 4; ++tp) {
-    const int kh = (ih & 1) + C2S * (tp >> 1), kw = (iw & 1) + C2S * (tp & 1);
-    const int oh = min(max(ih - kh, 0) / C2S, C2O - 1), ow = min(max(iw - kw, 0) / C2S, C2O - 1);
-    const int src = (oh * C2O + ow) * C2CO + 8 * cs;
-    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      w[tp][h] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
-      wd[tp][h] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
-      d[tp][h] = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
-      dd[tp][h] = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
   float z = 0.f;
+  for (int kh = (ih & 1); kh < C2K; kh += C2S) {
+    const int oh = (ih - kh) / C2S;
+    if (ih < kh || oh >= C2O) continue;
+    for (int kw = (iw & 1); kw < C2K; kw += C2S) {
+      const int ow = (iw - kw) / C2S;
+      if (iw < kw || ow >= C2O) continue;
+      const int src = (oh * C2O + ow) * C2CO + 8 * cs;
+      const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
 #pragma unroll
-  for (int tp = 0; tp < 4; ++tp) {
-    const int kh = (ih & 1) + C2S * (tp >> 1), kw = (iw & 1) + C2S * (tp & 1);
-    if (ih < kh || (ih - kh) / C2S >= C2O || iw < kw || (iw - kw) / C2S >= C2O) continue;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      z += ((d[tp][h].x * wd[tp][h].x + dd[tp][h].x * w[tp][h].x) + (d[tp][h].y * wd[tp][h].y + dd[tp][h].y * w[tp][h].y)) +
-           ((d[tp][h].z * wd[tp][h].z + dd[tp][h].z * w[tp][h].z) + (d[tp][h].w * wd[tp][h].w + dd[tp][h].w * w[tp][h].w));
+      for (int h = 0; h < 2; ++h) {
+        const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
+        const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
+        const float4 d = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
+        const float4 dd = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
+        z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) +
+             ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
+      }
+    }
   }
   s_r[ci][cs] = z;
   __syncthreads();
