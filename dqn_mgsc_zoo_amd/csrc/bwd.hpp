@@ -350,14 +350,8 @@ struct Conv2BwdArgs {
 // polls the sample's counter, and every dy2 load is an sc1 (L1-bypassing)
 // buffer load.  PUB: dy1 is handed on to the conv1 dW jobs of the same launch
 // (sc1 stores + arrival on sync1).
-// H position parts: the job computes parity-grid positions [q0, q0 + 100 / H),
-// q0 = part * 100 / H (H = 2: 3 MFMA row tiles + 2 VALU positions instead of
-// 6 + 4, so the dX chain's MFMA phase is half as long per job).
-template <bool WAIT, bool PUB = false, int H = 1>
-__device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh,
-                                             int part = 0) {
-  constexpr int NQ = 100 / H, MT = NQ / 16, NV = NQ - 16 * MT;  // 100: 6 + 4, 50: 3 + 2
-  const int q0 = part * NQ;
+template <bool WAIT, bool PUB = false>
+__device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   float wr[16];  // wr[4 t + j] = W2[kh(t)][kw(t)][16 hh + n][16 w + 4 j + kq]
@@ -375,11 +369,10 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   // relu'(y1) operands of the epilogue, loaded early: thread t owns output
   // positions q = t / 4 and q + 64 (< 100), channels 16 hh + 4 (t & 3) .. +3
-  constexpr int NK = (NQ + 63) / 64;
-  float4 ym4[NK];
+  float4 ym4[2];
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int q = q0 + min((t >> 2) + 64 * k, NQ - 1), ah = q / 10, cw = q % 10;
+  for (int k = 0; k < 2; ++k) {
+    const int q = min((t >> 2) + 64 * k, 99), ah = q / 10, cw = q % 10;
     ym4[k] = *reinterpret_cast<const float4*>(a.y1 + ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO +
                                               16 * hh + 4 * (t & 3));
   }
@@ -415,19 +408,18 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   __syncthreads();
   DQZ_STAMP(7, 1);
-  // NQ pixels = MT MFMA row tiles + the last NV pixels on the VALU (fwd.hpp's trim)
+  // 100 pixels = 6 MFMA row tiles + pixels 96..99 on the VALU (fwd.hpp's trim)
+  constexpr int MT = 6;
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int p = q0 + min(16 * m + n, NQ - 1);  // p = 10 a + c
+    const int p = min(16 * m + n, 99);  // p = 10 a + c
     base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + 16 * w + kq;
   }
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float last[NV];  // pixels q0 + 16 MT .. + NV - 1, this lane's k rows
-#pragma unroll
-  for (int e = 0; e < NV; ++e) last[e] = 0.f;
+  float last[4] = {0.f, 0.f, 0.f, 0.f};  // pixels 96..99 (a = 9, c = 6..9), this lane's k rows
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     const int tp = kk >> 2;  // (u', v') = (tp >> 1, tp & 1)
@@ -436,44 +428,40 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
     {
 #pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        const int p = q0 + 16 * MT + e;
-        last[e] = __fmaf_rn(s_win[(p / 10) * C2X_RS + (p % 10) * C2X_S + 16 * w + kq + off], wr[kk], last[e]);
-      }
+      for (int e = 0; e < 4; ++e)
+        last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + 16 * w + kq + off], wr[kk], last[e]);
     }
   }
   {
 #pragma unroll
-    for (int e = 0; e < NV; ++e) {
+    for (int e = 0; e < 4; ++e) {
       last[e] += __shfl_xor(last[e], 16, 64);
       last[e] += __shfl_xor(last[e], 32, 64);
     }
   }
   __syncthreads();
   DQZ_STAMP(7, 2);
-  constexpr int RW = 16 * (16 * MT + 16);  // a wave's rows (the VALU rows included), [4][RW / 16][16]
-  float* s_red = s_win;
+  float* s_red = s_win;  // [4][112][16]
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   if (kq == 0) {
 #pragma unroll
-    for (int e = 0; e < NV; ++e) s_red[w * RW + (16 * MT + e) * 16 + n] = last[e];
+    for (int e = 0; e < 4; ++e) s_red[w * 1792 + (96 + e) * 16 + n] = last[e];
   }
   __syncthreads();
   // 4 channels per lane: one 16-byte (write-through when PUB) store each
   // (a 4-byte write-through store costs ~6x the 16-byte one per byte)
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int ql = (t >> 2) + 64 * k;
-    if (ql < NQ) {
-      const int q = q0 + ql;
-      const int i = 16 * ql + 4 * (t & 3), ah = q / 10, cw = q % 10;
+  for (int k = 0; k < 2; ++k) {
+    const int q = (t >> 2) + 64 * k;
+    if (q < 100) {
+      const int i = 16 * q + 4 * (t & 3), ah = q / 10, cw = q % 10;
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = (s_red[i + e] + s_red[RW + i + e]) + (s_red[2 * RW + i + e] + s_red[3 * RW + i + e]);
+        v[e] = (s_red[i + e] + s_red[1792 + i + e]) + (s_red[3584 + i + e] + s_red[5376 + i + e]);
       v[0] = ym4[k].x > 0.f ? v[0] : 0.f;
       v[1] = ym4[k].y > 0.f ? v[1] : 0.f;
       v[2] = ym4[k].z > 0.f ? v[2] : 0.f;
@@ -739,14 +727,6 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   DQZ_STAMP(11, 3);
 }
 
-// conv2 dX jobs per sample in bwd_bc_kernel: 8 = (parity ph, pw) x channel
-// half; 16 also splits the parity grid's 100 positions in two.
-#ifndef DQZ_C2X_JOBS
-#define DQZ_C2X_JOBS 16
-#endif
-constexpr int C2X_JOBS = DQZ_C2X_JOBS;
-static_assert(C2X_JOBS == 8 || C2X_JOBS == 16, "conv2 dX jobs per sample");
-
 // ---- backward launches ----------------------------------------------------
 // fc1_dx_kernel (fc1 dX), then bwd_bc_kernel: the critical-path dX job chain
 // and the independent dW job sets share one launch, so the latency-bound dX
@@ -831,16 +811,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= NF;
-  if (i < C2X_JOBS * B8) {
-    const SampleJob sj = xcd_sample_job_at(i, C2X_JOBS, c2.B);
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
     DQZ_STAMP(7, 0);
-    conv2_bwd_dx<true, true, C2X_JOBS / 8>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, (sj.job >> 2) & 1,
-                                           sj.job >> 3);
+    conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
     return;
   }
-  i -= C2X_JOBS * B8;
+  i -= 8 * B8;
   if (i < 4 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
     if (!sj.valid) return;

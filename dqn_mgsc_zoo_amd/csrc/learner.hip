@@ -401,8 +401,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  // dy2: 8 conv3 dX producers; consumers: the C2X_JOBS conv2 dX and 8 conv2 dW jobs
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, C2X_JOBS + 8, L->spin_max};
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16, L->spin_max};
   Conv2BwdArgs c2b;
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -419,7 +418,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, C2X_JOBS, 8,
+  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8,
                        L->spin_max};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
@@ -429,7 +428,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + C2X_JOBS * B8 + 4 * B8 + 8 * B8 + 8 * B8;
+  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
   DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
