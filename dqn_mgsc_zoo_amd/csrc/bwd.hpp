@@ -727,10 +727,6 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
   DQZ_STAMP(11, 3);
 }
 
-#ifndef DQZ_BWD_C2X_EARLY
-#define DQZ_BWD_C2X_EARLY 1
-#endif
-
 // ---- backward launches ----------------------------------------------------
 // fc1_dx_kernel (fc1 dX), then bwd_bc_kernel: the critical-path dX job chain
 // and the independent dW job sets share one launch, so the latency-bound dX
@@ -810,36 +806,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  // DQZ_BWD_C2X_EARLY: the conv2 dX range ahead of the fc1 dW range, so every
-  // conv2 dX job is resident (polling) when its sample's dy2 lands instead of
-  // waiting for a slot behind the fc1 dW blocks
-  if (DQZ_BWD_C2X_EARLY) {
-    if (i < 8 * B8) {
-      const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
-      if (!sj.valid) return;
-      DQZ_STAMP(7, 0);
-      conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-      DQZ_STAMP(7, 3);
-      return;
-    }
-    i -= 8 * B8;
-  }
   if (i < NF) {
     fc1_dw_body(f1, smem, i);
     return;
   }
   i -= NF;
-  if (!DQZ_BWD_C2X_EARLY) {
-    if (i < 8 * B8) {
-      const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
-      if (!sj.valid) return;
-      DQZ_STAMP(7, 0);
-      conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-      DQZ_STAMP(7, 3);
-      return;
-    }
-    i -= 8 * B8;
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
+    if (!sj.valid) return;
+    DQZ_STAMP(7, 0);
+    conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
+    DQZ_STAMP(7, 3);
+    return;
   }
+  i -= 8 * B8;
   if (i < 4 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
     if (!sj.valid) return;
