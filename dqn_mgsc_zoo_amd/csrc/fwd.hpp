@@ -54,6 +54,9 @@ struct LayerFwdArgs {
 // A read for position p = 9 oh + ow: 2*oh*RS + 2*ow*S = 2p (mod 32).
 constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
 
+#ifndef DQZ_C2F_ST16
+#define DQZ_C2F_ST16 1
+#endif
 // WAIT: y1 of this sample comes from conv1 blocks of the same launch (poll,
 // then sc1 window loads).  PUB: y2 stores are sc1 and the block arrives.
 template <bool WAIT, bool PUB>
@@ -64,6 +67,9 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   const int n = lane & 15, kq = lane >> 4;
   const float* W = a.nz.p[z] + a.w_off;  // [512][64], k = kh*128 + kw*32 + ci
   const float bv = a.nz.p[z][a.b_off + 16 * nq + (t & 15)];  // epilogue bias, loaded early
+  // PUB epilogue: the bias of this lane's 4 channels 4 (t & 3) .. + 3
+  const float4 bias4 = PUB ? *reinterpret_cast<const float4*>(a.nz.p[z] + a.b_off + 16 * nq + 4 * (t & 3))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
   float wr[32];
 #pragma unroll
   for (int kk = 0; kk < 32; ++kk) wr[kk] = W[(w * 128 + 4 * kk + kq) * C2CO + 16 * nq + n];
@@ -137,18 +143,37 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   const bool dot = a.dot.part != nullptr;
   const float* dyp = a.dot.dy + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   float dacc = 0.f;
-  for (int i = t; i < C2M * 16; i += 256) {
-    const int k = red_idx(i >> 4, i & 15);
-    const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
-    if constexpr (PUB)
-      __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    else if (dot)
-      dacc += v * dyp[(i >> 4) * C2CO + (i & 15)];
-    else
-      out[(i >> 4) * C2CO + (i & 15)] = linear ? v : relu(v);
+  if constexpr (PUB && DQZ_C2F_ST16) {
+    // y2 handed to conv3: 4 channels per lane, one 16-byte write-through store
+    // each (324 per block instead of 1,296 4-byte ones, which the guide prices
+    // at ~6x per byte; same values)
+    for (int i = t; i < C2M * 4; i += 256) {
+      const int p = i >> 2, c4 = 4 * (i & 3);
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = red_idx(p, c4 + e);
+        const float bb = e == 0 ? bias4.x : e == 1 ? bias4.y : e == 2 ? bias4.z : bias4.w;
+        const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bb;
+        o[e] = linear ? v : relu(v);
+      }
+      store_sc1_f4(out, (C2M * C2CO - 16 * nq) * 4, 4 * (p * C2CO + c4), f32x4{o[0], o[1], o[2], o[3]});
+    }
+    a.pub.arrive(sj.s);
+  } else {
+    for (int i = t; i < C2M * 16; i += 256) {
+      const int k = red_idx(i >> 4, i & 15);
+      const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
+      if constexpr (PUB)
+        __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else if (dot)
+        dacc += v * dyp[(i >> 4) * C2CO + (i & 15)];
+      else
+        out[(i >> 4) * C2CO + (i & 15)] = linear ? v : relu(v);
+    }
+    if constexpr (PUB) a.pub.arrive(sj.s);
   }
-  if constexpr (PUB) a.pub.arrive(sj.s);
   if (!PUB && dot) {
     __syncthreads();
     const float r = block_sum256(dacc, s_in);
