@@ -477,16 +477,25 @@ struct CsumLevel1 {
   int blk;        // the chunk the query's u falls in
   double before;  // the normalised-cumsum mass before it
   double tot;     // total of all chunk sums
+  double u;       // the query
 };
 
-// Wave-uniform result on every lane of the calling wave (a whole wave).
-__device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csum, int nblocks, double u) {
+// Wave-uniform result on every lane of the calling wave (a whole wave).  The
+// query u comes from `uf`, called after the chunk sums' loads are issued, so
+// u's own loads (the step counter, a caller's uniform) are in flight with
+// them instead of ahead of them.
+template <class UF>
+__device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csum, int nblocks, UF uf) {
   const int l = threadIdx.x & 63;
   const int seg = (nblocks + 63) / 64;
   const int b0 = min(l * seg, nblocks), b1 = min(b0 + seg, nblocks);
   double mb[CS_SEG];
 #pragma unroll
-  for (int j = 0; j < CS_SEG; ++j) mb[j] = b0 + j < b1 ? csum[b0 + j] : 0.0;
+  for (int j = 0; j < CS_SEG; ++j) mb[j] = csum[min(b0 + j, nblocks - 1)];
+  const double u = uf();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < CS_SEG; ++j) mb[j] = b0 + j < b1 ? mb[j] : 0.0;
   double mine = 0.0;
 #pragma unroll
   for (int j = 0; j < CS_SEG; ++j)
@@ -528,6 +537,7 @@ __device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csu
   const unsigned long long m = __ballot(hit >= 0);
   CsumLevel1 r;
   r.tot = tot;
+  r.u = u;
   if (m) {  // the lowest crossing lane holds the earliest chunk
     const int src = __ffsll((long long)m) - 1;
     r.blk = __shfl(hit, src, 64);
@@ -546,26 +556,29 @@ __device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csu
 // lanes) the lane (16 terms each) and the slot from the chunk's re-formed
 // terms, whose scan total is csum[chunk].  At most one lane sees the
 // crossing, so it stores the slot directly.
+template <class UF>
 __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, const LogitRun* run,
-                                                       const double* __restrict__ csum, int nblocks, double u) {
+                                                       const double* __restrict__ csum, int nblocks, UF uf) {
   __shared__ double s_wave[SM_THREADS / 64];
   __shared__ double s_before, s_tot;
   __shared__ int s_blk;
   __shared__ int64_t s_idx;
   const int t = threadIdx.x;
   const float c = run->c;
+  __shared__ double s_u;
   if (t < 64) {
-    const CsumLevel1 r = csum_level1(csum, nblocks, u);
+    const CsumLevel1 r = csum_level1(csum, nblocks, uf);
     if (t == 0) {
       s_blk = r.blk;
       s_before = r.before;
       s_tot = r.tot;
       s_idx = -1;
+      s_u = r.u;
     }
   }
   __syncthreads();
   const int blk = s_blk;
-  const double tot = s_tot, before = s_before;
+  const double tot = s_tot, before = s_before, u = s_u;
   float xv[SM_PER_LANE];
   load_chunk_lane(x, n, blk, xv);
   double p[SM_PER_LANE];
@@ -619,7 +632,7 @@ __global__ __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __
   __shared__ double s_tot;
   const LogitRun r = *run;
   if (threadIdx.x < 64) {
-    const CsumLevel1 l1 = csum_level1(csum, nblocks, 2.0);  // u = 2: only the total is used
+    const CsumLevel1 l1 = csum_level1(csum, nblocks, [] { return 2.0; });  // u = 2: only the total is used
     if (threadIdx.x == 0) s_tot = l1.tot;
   }
   __syncthreads();
@@ -660,8 +673,9 @@ struct SoftmaxDraw {
 };
 
 __device__ __forceinline__ int32_t softmax_draw_slot(const SoftmaxDraw& d, int b) {
-  const double u = d.uniforms ? d.uniforms[b] : philox_uniform(d.seed, *d.counter, b);
-  return (int32_t)softmax_choice_body(d.x, d.n, d.run, d.csum, d.nblocks, u);
+  return (int32_t)softmax_choice_body(d.x, d.n, d.run, d.csum, d.nblocks, [&] {
+    return d.uniforms ? d.uniforms[b] : philox_uniform(d.seed, *d.counter, b);
+  });
 }
 
 // Learned-logit batch draw (replay_circular.py:205-217, 540-545:
@@ -680,15 +694,10 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
     int32_t* __restrict__ out_slots, int64_t* __restrict__ out_idx) {
   int* done = sync.words + SampleSync::kStride;
   const int q = blockIdx.x;
-  uint64_t ctr = 0;
-  double u;
-  if (uniforms) {
-    u = uniforms[q];
-  } else {
-    ctr = *counter;
-    u = philox_uniform(seed, ctr, q);
-  }
-  const int64_t idx = softmax_choice_body(x, n, run, csum, nblocks, u);
+  const uint64_t ctr = uniforms ? 0 : *counter;
+  const int64_t idx = softmax_choice_body(x, n, run, csum, nblocks, [&] {
+    return uniforms ? uniforms[q] : philox_uniform(seed, ctr, q);
+  });
   if (threadIdx.x == 0) {
     if (out_slots) out_slots[q] = (int32_t)idx;
     if (out_idx) out_idx[q] = idx;
@@ -1014,12 +1023,41 @@ constexpr int PS_TOP_NODES = 2 << PS_TOPD;  // LDS doubles of the staged top
 
 // Stages tree nodes 1 .. 2^(dtop + 1) - 1 into s_top[1 ..] (whole block) and
 // returns dtop.
-__device__ __forceinline__ int per_stage_top(const PerSampleArgs& a, double* s_top) {
-  const int dtop = min(a.levels, PS_TOPD);
-  const int ntop = (2 << dtop) - 1;
-  for (int q = threadIdx.x; q < ntop; q += blockDim.x) s_top[1 + q] = a.tree[1 + q];
+// The top is staged in two halves so a caller can issue other loads between
+// them: per_top_load issues every load of the thread (a guarded loop left to
+// the compiler loaded, waited and stored one node per thread at a time: eight
+// dependent round trips per 256-thread block), per_top_store writes them.
+constexpr int PS_TOP_R = (PS_TOP_NODES + 255) / 256;  // nodes per thread of a 256-thread block
+struct PerTop {
+  double v[PS_TOP_R];
+  int dtop, ntop;
+};
+__device__ __forceinline__ PerTop per_top_load(const PerSampleArgs& a) {
+  PerTop t;
+  t.dtop = min(a.levels, PS_TOPD);
+  t.ntop = (2 << t.dtop) - 1;
+  const int nb = blockDim.x;
+#pragma unroll
+  for (int r = 0; r < PS_TOP_R; ++r) t.v[r] = a.tree[1 + min((int)threadIdx.x + r * nb, t.ntop - 1)];
+  return t;
+}
+__device__ __forceinline__ int per_top_store(const PerSampleArgs& a, const PerTop& t, double* s_top) {
+  const int nb = blockDim.x;
+#pragma unroll
+  for (int r = 0; r < PS_TOP_R; ++r) {
+    const int q = threadIdx.x + r * nb;
+    if (q < t.ntop) s_top[1 + q] = t.v[r];
+  }
+  for (int q = threadIdx.x + PS_TOP_R * nb; q < t.ntop; q += nb) s_top[1 + q] = a.tree[1 + q];  // blocks under 256 threads
   __syncthreads();
-  return dtop;
+  return t.dtop;
+}
+// Stages tree nodes 1 .. 2^(dtop + 1) - 1 into s_top[1 ..] (whole block) and
+// returns dtop.
+__device__ __forceinline__ int per_stage_top(const PerSampleArgs& a, double* s_top) {
+  const PerTop t = per_top_load(a);
+  __builtin_amdgcn_sched_barrier(0);
+  return per_top_store(a, t, s_top);
 }
 
 // Draw i of PrioritizedDistribution.sample (replay.py:680-716) by one
@@ -1170,10 +1208,12 @@ struct PerDrawOut {
 __device__ __forceinline__ PerDrawOut per_draw_slot(const PerSampleArgs& a, int b, double* lds, bool publish) {
   __shared__ int32_t s_slot;
   double prob = 0.0;
-  // the draw's inputs (the counter or the injected values: block-uniform
-  // loads) are issued before the tree top is staged and land under it
+  // the tree top's loads and the draw's inputs (the counter or the injected
+  // values: block-uniform loads) are all in flight before the first wait
+  const PerTop top = per_top_load(a);
   const PerDrawInput raw = per_draw_load(a, b);
-  const int dtop = per_stage_top(a, lds);
+  __builtin_amdgcn_sched_barrier(0);
+  const int dtop = per_top_store(a, top, lds);
   if (threadIdx.x < 32) {
     const PerDrawInput in = a.inj_u ? raw : per_draw_input(a, b, (uint64_t)raw.uni);
     const PerPick pk = per_pick(a, threadIdx.x, lds, dtop, in);
