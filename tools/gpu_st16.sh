@@ -13,3 +13,6 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 set -e
 bash tools/abv.sh 3 $L/libdqz.so $L/libdqz_st4.so > $OUT/abv.txt 2>&1
 DQZ_TRACE_PREBUILT=1 timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_step.txt 2>&1
+# the sampler load batching (PER tree top, learned-logit chunk sums): configs 4 and 3
+timeout -k 10 300 python bench.py --algo per --cpu-seconds 0 > $OUT/bench_per.json 2> $OUT/bench_per.err
+timeout -k 10 300 python bench.py --algo mgsc --cpu-seconds 0 > $OUT/bench_mgsc.json 2> $OUT/bench_mgsc.err
