@@ -111,8 +111,18 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
   constexpr int QPC = C1_PLANE / 16;  // 126 16-byte pieces per channel
   if (src.states) {
     const uint4* g = reinterpret_cast<const uint4*>(src.states + ((int64_t)b * FH + row0) * FW * FC);
-    for (int i = threadIdx.x; i < C1_PLANE * FC / 16; i += blockDim.x) {
-      const uint4 v = g[i];  // 4 pixels x 4 channels
+    // both 16-byte pieces of a thread in flight before the first LDS store (a
+    // guarded loop loaded, waited and stored them one at a time)
+    constexpr int NS = C1_PLANE * FC / 16, RS = (NS + 255) / 256;  // 504, 2
+    uint4 vs[RS];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) vs[r] = g[min((int)threadIdx.x + 256 * r, NS - 1)];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      const int i = threadIdx.x + 256 * r;
+      if (i >= NS) break;
+      const uint4 v = vs[r];  // 4 pixels x 4 channels
       const unsigned w[4] = {v.x, v.y, v.z, v.w};
       const int p = 4 * i;
 #pragma unroll
