@@ -16,3 +16,4 @@ DQZ_TRACE_PREBUILT=1 timeout -k 10 200 python -u tools/trace_step.py > $OUT/trac
 # the sampler load batching (PER tree top, learned-logit chunk sums): configs 4 and 3
 timeout -k 10 300 python bench.py --algo per --cpu-seconds 0 > $OUT/bench_per.json 2> $OUT/bench_per.err
 timeout -k 10 300 python bench.py --algo mgsc --cpu-seconds 0 > $OUT/bench_mgsc.json 2> $OUT/bench_mgsc.err
+timeout -k 10 300 python bench.py --algo agent --steps 2000 --warmup 50 > $OUT/bench_agent.json 2> $OUT/bench_agent.err
