@@ -54,9 +54,6 @@ struct LayerFwdArgs {
 // A read for position p = 9 oh + ow: 2*oh*RS + 2*ow*S = 2p (mod 32).
 constexpr int C2L_S = 33, C2L_RS = 665, C2L_WIN = 20 * C2L_RS;  // 13300 floats
 
-#ifndef DQZ_C2F_ST16
-#define DQZ_C2F_ST16 1
-#endif
 // WAIT: y1 of this sample comes from conv1 blocks of the same launch (poll,
 // then sc1 window loads).  PUB: y2 stores are sc1 and the block arrives.
 template <bool WAIT, bool PUB>
@@ -143,7 +140,7 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
   const bool dot = a.dot.part != nullptr;
   const float* dyp = a.dot.dy + ((int64_t)z * a.B + b) * (C2M * C2CO) + 16 * nq;
   float dacc = 0.f;
-  if constexpr (PUB && DQZ_C2F_ST16) {
+  if constexpr (PUB) {
     // y2 handed to conv3: 4 channels per lane, one 16-byte write-through store
     // each (324 per block instead of 1,296 4-byte ones, which the guide prices
     // at ~6x per byte; same values)
@@ -164,15 +161,11 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     for (int i = t; i < C2M * 16; i += 256) {
       const int k = red_idx(i >> 4, i & 15);
       const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bv;
-      if constexpr (PUB)
-        __hip_atomic_store(out + (i >> 4) * C2CO + (i & 15), linear ? v : relu(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      else if (dot)
+      if (dot)
         dacc += v * dyp[(i >> 4) * C2CO + (i & 15)];
       else
         out[(i >> 4) * C2CO + (i & 15)] = linear ? v : relu(v);
     }
-    if constexpr (PUB) a.pub.arrive(sj.s);
   }
   if (!PUB && dot) {
     __syncthreads();
