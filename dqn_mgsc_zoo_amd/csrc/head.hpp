@@ -88,8 +88,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   DQZ_STAMP(4, 0);
   __shared__ float s_red[8][3 * AMAX];
   __shared__ float s_q[3][AMAX];
-  __shared__ float s_g;
-  __shared__ int s_a;
+  __shared__ float s_rec[5];  // {a_tm1 bits, r, d, w, p} of sample b
   const int n = threadIdx.x, lane = n & 63, wave = n >> 6;
   const int A = h.A, B = h.B, Z = h.Z, S = h.S;
   // Every global load is issued up front: the batch record chain
@@ -194,6 +193,12 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     if (h.weights) w = h.weights[b];
     if (h.per_wb) w = wper;
     if (h.meta_p && !h.meta_logits) pm = h.meta_p[b];
+    // broadcast for the TD below, which every thread forms (no extra barrier)
+    s_rec[0] = __int_as_float(a_tm1);
+    s_rec[1] = r;
+    s_rec[2] = d;
+    s_rec[3] = w;
+    s_rec[4] = pm;
   }
   DQZ_STAMP(4, 1);
   float hz[ZMAX];
@@ -246,7 +251,15 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   if (!h.fwd_only) {
     __syncthreads();
     DQZ_STAMP(15, 2);  // q values in LDS
-    if (n == 0) {
+    {
+      // every thread forms the TD error and its cotangent from the same LDS
+      // values with the same operations (same bits in every thread), so the
+      // dz1 row below needs no second barrier; thread 0 stores the outputs
+      a_tm1 = __float_as_int(s_rec[0]);
+      r = s_rec[1];
+      d = s_rec[2];
+      w = s_rec[3];
+      pm = s_rec[4];
       float q0[AMAX], q1[AMAX], q2[AMAX];  // every LDS read issued before the first use
 #pragma unroll
       for (int a = 0; a < AMAX; ++a) {
@@ -286,20 +299,19 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
         g = w * td / (float)B;  // d mean(l2(td) * w) / d td
         g = fminf(fmaxf(g, -h.bound), h.bound);
       }
-      s_g = -g;
-      s_a = a_tm1;
-      h.td[b] = td;
-      h.loss_part[b] = 0.5f * td * td * w;
-      h.gq[b] = -g;
-      h.ga[b] = a_tm1;
-    }
-    __syncthreads();
-    float wv = w2v[0][0];
+      if (n == 0) {
+        h.td[b] = td;
+        h.loss_part[b] = 0.5f * td * td * w;
+        h.gq[b] = -g;
+        h.ga[b] = a_tm1;
+      }
+      float wv = w2v[0][0];
 #pragma unroll
-    for (int a = 1; a < AMAX; ++a) wv = a == s_a ? w2v[0][a] : wv;
-    DQZ_STAMP(4, 2);
-    const float dz = hz[0] > 0.f ? s_g * wv : 0.f;
-    h.dz1[(int64_t)b * HID + n] = dz;
+      for (int a = 1; a < AMAX; ++a) wv = a == a_tm1 ? w2v[0][a] : wv;
+      DQZ_STAMP(4, 2);
+      const float dz = hz[0] > 0.f ? -g * wv : 0.f;
+      h.dz1[(int64_t)b * HID + n] = dz;
+    }
   } else if (h.act_out) {  // actor: eps-greedy draw b of call act_ctr
     __syncthreads();
     if (n == 0) {
