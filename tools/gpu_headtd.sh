@@ -1,9 +1,9 @@
 #!/bin/bash
-# Head A/B: every thread forms the TD error (one barrier fewer) against the
-# thread-0 TD + broadcast (libdqz_oldhead.so, the previous head.hpp built with
-# the current build id).  GPU suite on the default library first.
+# Head A/B (usage: gpu_headtd.sh [out tag]): the head at the working tree against
+# libdqz_oldhead.so (the committed head.hpp built with the working tree's
+# build id).  GPU suite on the default library first.
 set -o pipefail
-OUT=gpurun_out/headtd
+OUT=gpurun_out/${1:-headtd}
 mkdir -p $OUT
 L=dqn_mgsc_zoo_amd
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1
