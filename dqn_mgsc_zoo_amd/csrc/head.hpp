@@ -237,7 +237,13 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
         for (int u = 0; u < 4; ++u) a4[u] += row[(i + u) << lgT];
       }
       float v = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      // butterfly over the T lanes: DPP within 16-lane rows (quad xor 1,
+      // xor 2, half-row and row mirrors), one ds_bpermute across rows for T = 32
+      v += dpp_f<0xB1>(v);
+      v += dpp_f<0x4E>(v);
+      v += dpp_f<0x141>(v);
+      v += dpp_f<0x140>(v);
+      if (T == 32) v += __shfl_xor(v, 16, 64);
       qv = v + b2v;
       if (jj == 0) s_q[zq][aq] = qv;
     }
