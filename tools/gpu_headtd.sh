@@ -1,7 +1,10 @@
 #!/bin/bash
-# Head A/B (usage: gpu_headtd.sh [out tag]): the head at the working tree against
-# libdqz_oldhead.so (the committed head.hpp built with the working tree's
-# build id).  GPU suite on the default library first.
+# Working tree against committed sources (usage: gpu_headtd.sh [out tag]):
+# libdqz.so is the working tree, libdqz_oldhead.so the committed version of
+# the edited files built beforehand with the working tree's build id.  GPU
+# suite on the default library first, then three interleaved bench rounds,
+# a step trace and the config 4 / 3 lines.  (Used for the head TD, head
+# wave-partial, head DPP and fc1 dX 8-wave A/Bs of round 4.)
 set -o pipefail
 OUT=gpurun_out/${1:-headtd}
 mkdir -p $OUT
