@@ -72,6 +72,29 @@ __device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double e
   return dqz_action{act, v};
 }
 
+// Maximum of a wave's non-negative doubles (the PER importance weights), in
+// every lane: the DPP row scan of wave_sum with max (lanes whose DPP source is
+// outside the row read 0, the identity here), then readlane 63.  Max is exact
+// in any order, so the result equals a shuffle butterfly's bit for bit.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_max_nonneg(double m) {
+  m = fmax(m, dpp_d<0x111>(m));
+  m = fmax(m, dpp_d<0x112>(m));
+  m = fmax(m, dpp_d<0x114>(m));
+  m = fmax(m, dpp_d<0x118>(m));
+  m = fmax(m, dpp_d<0x142, 0xa>(m));
+  m = fmax(m, dpp_d<0x143, 0xc>(m));
+  const long long b = __builtin_bit_cast(long long, m);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
 // One workgroup (512 threads = hidden units) per sample b:
 //   h1 = relu(b1 + sum_s partial), q = h1 @ W2 + b2 for every copy z,
 //   TD error (rlax 0.1.2 q_learning / double_q_learning as called at
@@ -145,8 +168,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   if (h.per_wb && wave == 0) {  // the batch's IS weights (the fused PER draw)
     double m = 0.0;
     for (int j = lane; j < B; j += 64) m = fmax(m, h.per_wb[j]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    m = wave_max_nonneg(m);
     if (lane == 0) {
       const double wb = h.per_wb[b];
       wper = (float)(h.per_normalize ? wb / m : wb);
