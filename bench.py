@@ -44,6 +44,11 @@ if ROOT not in sys.path:
 
 METRIC = ('learner grad-steps/sec at batch=32, 84×84×4 uint8, '
           '1/2/4/8 MI355X')
+# --algo agent (config 1): learner steps/s of the whole agent loop (acting,
+# preprocessing and replay adds inside the timed region) -- not the headline
+# learner-only quantity, so it carries a metric name of its own
+AGENT_METRIC = ('agent-loop learner steps/sec (act + preprocess + add + learn), '
+                'batch=32, 84×84×4 uint8, MI355X')
 BATCH = 32
 META_BATCH = 100  # the meta-update timed apart at M = 100
 NUM_ACTIONS = 6  # Pong minimal action set (gym_atari.py:52-54)
@@ -464,6 +469,18 @@ def selftest_cpu(args, g, rem):
   elapsed_max = reps.max_over_ranks(elapsed)
   per_rank = reps.gather_stats([counters['steps'] - warm, elapsed,
                                 counters['syncs'], counters['gathers']])
+  # device identities: stand-ins here (DQZ_SELFTEST_DEVICE overrides the
+  # per-rank default, so a test can make two ranks collide)
+  stand_in = os.environ.get('DQZ_SELFTEST_DEVICE', 'stand-in-%d' % reps.rank)
+  devices = reps.gather_objects(
+      dict(replicas_lib.device_identity(reps.local_rank, stand_in=stand_in),
+           fill_s=0.0))
+  errors = replicas_lib.check_devices(devices, args.gpus)
+  if errors:
+    if reps.rank == 0:
+      print('bench.py: %s' % '; '.join(errors), file=sys.stderr)
+    reps.close()
+    return 4
   if reps.rank == 0:
     print(json.dumps({
         'metric': METRIC + ' [CPU orchestration self-test]',
@@ -474,6 +491,7 @@ def selftest_cpu(args, g, rem):
         'per_rank_steps': [int(v) for v in per_rank[:, 0]],
         'per_rank_target_syncs': [int(v) for v in per_rank[:, 2]],
         'per_rank_stats_gathers': [int(v) for v in per_rank[:, 3]],
+        'devices': devices,
         'rccl': {'backend': reps.backend, 'world': reps.world,
                  'last_in_loop_gather': {
                      'steps_done': [int(v) for v in last['stats'][:, 0]],
@@ -737,6 +755,17 @@ def run_gpu(args, g, rem):
   lrn.fetch_outputs()
   per_rank = reps.gather_stats([steps / elapsed, elapsed, float(steps),
                                 float(lrn.loss[0].item())], device=dev)
+  # which device each rank ran on, and its replay fill time: a line from N
+  # ranks is only valid with N distinct devices (SCALE runs, config 5)
+  devices = reps.gather_objects(
+      dict(replicas_lib.device_identity(local_rank), fill_s=round(wl.fill_s, 2)))
+  dev_errors = replicas_lib.check_devices(devices, args.gpus)
+  if dev_errors:
+    if rank == 0:
+      print('bench.py: %s: the line is invalid' % '; '.join(dev_errors),
+            file=sys.stderr)
+    reps.close()
+    return 4
 
   # Per-phase device time (HIP events on the launch stream) for the roofline.
   phases = lrn.profile(store, slots, weights=wl.weights, iters=args.profile_iters)
@@ -789,7 +818,7 @@ def run_gpu(args, g, rem):
   per_gpu = steps / elapsed
   step_tflops = STEP_FLOP[algo] * per_gpu / 1e12
   step_gbs = STEP_BYTES[algo] * per_gpu / 1e9
-  rccl = {'backend': reps.backend, 'world': world,
+  rccl = {'backend': reps.backend, 'world': world, 'devices': devices,
           'in_loop_gathers': len(pending), 'stats_every': args.stats_every,
           'final_gather': {'steps_per_s': [round(float(x), 2) for x in per_rank[:, 0]],
                            'steps': [int(x) for x in per_rank[:, 2]],
@@ -962,13 +991,22 @@ def run_agent(args):
   elapsed_max = reps.max_over_ranks(elapsed, device=dev)
   per_rank = reps.gather_stats([args.steps / elapsed, frames / elapsed,
                                 float(frames)], device=dev)
+  devices = reps.gather_objects(
+      dict(replicas_lib.device_identity(dev.index), fill_s=round(fill_s, 2)))
+  dev_errors = replicas_lib.check_devices(devices, args.gpus)
+  if dev_errors:
+    if rank == 0:
+      print('bench.py: %s: the line is invalid' % '; '.join(dev_errors),
+            file=sys.stderr)
+    reps.close()
+    return 4
   finite = bool(torch.isfinite(agent.learner.online).all().item())
   if rank != 0:
     reps.close()
     return 0 if (status == 0 and ok and finite) else 3
   world = reps.world
   out = {
-      'metric': METRIC,
+      'metric': AGENT_METRIC,
       'value': round(world * args.steps / elapsed_max, 2),
       'unit': 'steps/s',
       'n_gpus': world,

@@ -299,17 +299,6 @@ __device__ __forceinline__ void conv1_fwd_body(const Conv1FwdArgs& a, float* sme
   }
   DQZ_STAMP(0, 3);
 }
-__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1FwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const SampleJob sj = xcd_sample_job(C1_BLOCKS, a.Z * a.B);
-  if (!sj.valid) return;
-  switch (a.src.fused) {  // the stand-alone conv1 launch (profile / debug layouts)
-    case 1: conv1_fwd_body<false, 1>(a, smem, sj); break;
-    case 2: conv1_fwd_body<false, 2>(a, smem, sj); break;
-    case 3: conv1_fwd_body<false, 3>(a, smem, sj); break;
-    default: conv1_fwd_body<false, 0>(a, smem, sj); break;
-  }
-}
 
 struct Conv1DwArgs {
   Conv1Src src;

@@ -264,12 +264,6 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
   DQZ_STAMP(1, 3);
 }
 
-__global__ __launch_bounds__(256) void conv2_fwd_kernel(LayerFwdArgs a) {
-  __shared__ float s_in[C2L_WIN];
-  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
-  if (!sj.valid) return;
-  conv2_fwd_body<false, false>(a, s_in, sj);
-}
 
 // ---- conv3: 9x9x64 -> 7x7x64, 3x3 stride 1 ---------------------------------
 // Wave w owns input channels [16w, 16w + 16) of every tap.  Bank of the A read
@@ -464,12 +458,6 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
   DQZ_STAMP(2, 3);
 }
 
-__global__ __launch_bounds__(256) void conv3_fwd_kernel(LayerFwdArgs a) {
-  __shared__ float s_in[C3L_WIN];
-  const SampleJob sj = xcd_sample_job(4, a.Z * a.B);
-  if (!sj.valid) return;
-  conv3_fwd_body<false>(a, s_in, sj);
-}
 
 // ---- conv1 -> conv2 -> conv3 forward in one launch ------------------------
 // Grid, in dispatch order, over the Z x B samples s = z B + b:

@@ -176,6 +176,12 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     }
   }
   if (h.meta_logits) {
+    // one thread per meta-batch logit: thread n holds pos[n], and the block
+    // of sample b writes x_out[b] / p_out[b] through thread n == b, so the
+    // meta batch must fit the block (launch_meta keeps M <= MAXB with one
+    // chunk).  This path sums in another order than meta_softmax_kernel (the
+    // K > 1 chunks): p agrees with it within f32 rounding, not bit for bit.
+    static_assert(MAXB <= HID, "the head's one-chunk meta softmax needs M <= the block's threads");
     // p = exp(x - (c + log sum exp(x - c))), c = max x, over the M meta-batch
     // logits (replay_circular.py:79-86 as meta_softmax_kernel forms it; the
     // block reductions run in a fixed order)

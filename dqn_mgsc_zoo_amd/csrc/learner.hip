@@ -68,8 +68,6 @@ static int g_attr_done = 0;
 
 static int init_kernel_attrs() {
   if (g_attr_done) return DQZ_OK;
-  DQZ_HIP(hipFuncSetAttribute((const void*)conv1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kConv1FwdSmem));
   const void* fwd_kernels[] = {(const void*)fwd_conv_kernel<0>, (const void*)fwd_conv_kernel<1>,
                                (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>,
                                (const void*)tangent_fwd_kernel};
@@ -188,13 +186,13 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
     }                                                                       \
   } while (0)
 
-// conv1..fc1 forward of Z network copies (phases 0-3).
-// fused_conv: conv1 -> conv2 -> conv3 as one hand-off launch (fwd_conv_kernel),
-// used by the learner step (since conv1 runs on bf16 MFMA: 15,590 -> 16,050
-// steps/s; with the f32-MFMA conv1 it had measured 1.5 % slower) and the actor.
+// conv1..fc1 forward of Z network copies (phases 0-3): conv1 -> conv2 ->
+// conv3 as one hand-off launch (fwd_conv_kernel; since conv1 runs on bf16
+// MFMA: 15,590 -> 16,050 steps/s against three launches, which round 4
+// removed), then the split-K fc1.  Used by the learner step and the actor.
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
-                        PhaseEvents pe, bool fused_conv) {
-  Conv1FwdArgs c1;
+                        PhaseEvents pe) {
+  Conv1FwdArgs c1{};
   c1.src = src;
   c1.nz = nz;
   c1.w_off = L->off[0];
@@ -204,7 +202,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c1.linear = 0;
   c1.out = L->y1;
 
-  LayerFwdArgs c2;
+  LayerFwdArgs c2{};
   c2.in = L->y1;
   c2.nz = nz;
   c2.w_off = L->off[2];
@@ -219,38 +217,29 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c3.w_off = L->off[4];
   c3.b_off = L->off[5];
   c3.out = L->y3;
-  if (fused_conv) {
-    // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample.  The
-    // word layout follows the learner's configured batch, not this call's n
-    // (the actor's forward has n = 1): Z * n <= 3 * cfg.batch samples, and
-    // every launch shares the one error word dqz_learner_sync_status reads.
-    const int Bc = L->cfg.batch;
-    int* hw = L->sync + 2 * Bc * Handoff::kStride;
-    int* err = L->sync + 16 * Bc * Handoff::kStride;
-    const int jobs = fwd_conv_jobs(Z * B);
-    c2.jobs = c3.jobs = jobs;
-    c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, jobs};
-    c2.wait = c1.pub;
-    c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
-    c3.wait = c2.pub;
-    const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
-    DQZ_PHASE(0, switch (src.fused) {
-      case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
-      case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
-      case 3: hipLaunchKernelGGL(fwd_conv_kernel<3>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
-      default: hipLaunchKernelGGL(fwd_conv_kernel<0>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
-    } DQZ_HIP(hipGetLastError()));
-    if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
-  } else {
-    DQZ_PHASE(0, hipLaunchKernelGGL(conv1_fwd_kernel, xcd_grid(C1_BLOCKS, Z * B), dim3(256), kConv1FwdSmem, st, c1);
-              DQZ_HIP(hipGetLastError()));
-    DQZ_PHASE(1, hipLaunchKernelGGL(conv2_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c2);
-              DQZ_HIP(hipGetLastError()));
-    DQZ_PHASE(2, hipLaunchKernelGGL(conv3_fwd_kernel, xcd_grid(4, Z * B), dim3(256), 0, st, c3);
-              DQZ_HIP(hipGetLastError()));
-  }
+  // y1 / y2 hand-offs: 4 producer and 4 consumer blocks per sample.  The
+  // word layout follows the learner's configured batch, not this call's n
+  // (the actor's forward has n = 1): Z * n <= 3 * cfg.batch samples, and
+  // every launch shares the one error word dqz_learner_sync_status reads.
+  const int Bc = L->cfg.batch;
+  int* hw = L->sync + 2 * Bc * Handoff::kStride;
+  int* err = L->sync + 16 * Bc * Handoff::kStride;
+  const int jobs = fwd_conv_jobs(Z * B);
+  c2.jobs = c3.jobs = jobs;
+  c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, jobs};
+  c2.wait = c1.pub;
+  c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
+  c3.wait = c2.pub;
+  const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
+  DQZ_PHASE(0, switch (src.fused) {
+    case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+    case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+    case 3: hipLaunchKernelGGL(fwd_conv_kernel<3>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+    default: hipLaunchKernelGGL(fwd_conv_kernel<0>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
+  } DQZ_HIP(hipGetLastError()));
+  if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
 
-  Fc1FwdArgs f1;
+  Fc1FwdArgs f1{};
   f1.in = L->y3;
   f1.nz = nz;
   f1.w_off = L->off[6];
@@ -298,7 +287,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   if (L->cfg.algo == DQZ_ALGO_PER && !is_weights && !pd) return fail(DQZ_ERR_INVALID, "PER step needs is_weights");
   hipStream_t st = (hipStream_t)stream;
   const int B = L->cfg.batch, Z = L->Z, A = L->cfg.num_actions;
-  NetZ nz;
+  NetZ nz{};
   nz.p[0] = P->online;
   nz.p[1] = P->target;
   nz.p[2] = P->online;
@@ -323,9 +312,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
       fsrc.fused = 2;
       fsrc.sm = *sm;
     }
-    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe, true)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, fsrc, st, pe)) return rc;
   } else {
-    if (int rc = forward_impl(L, nz, Z, B, src, st, pe, true)) return rc;
+    if (int rc = forward_impl(L, nz, Z, B, src, st, pe)) return rc;
   }
 
   // an MGSC meta stage applied in the gradient epilogues (Rms), or plain
@@ -372,7 +361,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
 
   // Backward: fc1 dX, then the merged launch that pairs the dX chain with the
   // independent dW job sets (bwd.hpp).
-  Fc1BwdArgs fb;
+  Fc1BwdArgs fb{};
   fb.dz1 = L->dz1;
   fb.y3 = L->y3;
   fb.th = P->online;
@@ -390,7 +379,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
             DQZ_HIP(hipGetLastError()));
 
-  Conv3BwdArgs c3b;
+  Conv3BwdArgs c3b{};
   c3b.dy3 = L->dy3;
   c3b.y2 = L->y2;
   c3b.w3 = P->online + L->off[4];
@@ -402,7 +391,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
   c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16, L->spin_max};
-  Conv2BwdArgs c2b;
+  Conv2BwdArgs c2b{};
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
   c2b.w2 = P->online + L->off[2];
@@ -411,7 +400,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c2b.part = L->p2;
   c2b.B = B;
   c2b.sync = c3b.sync;
-  Conv1DwArgs c1dw;
+  Conv1DwArgs c1dw{};
   c1dw.src = src;
   c1dw.src.rec = nullptr;
   c1dw.which = 0;
@@ -434,7 +423,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
             DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
-  UpdArgs u;
+  UpdArgs u{};
   u.th = P->online;
   u.mu = P->mu;
   u.nu = P->nu;
@@ -555,10 +544,10 @@ int dqz_learner_outputs(dqz_learner* L, float* q_tm1, float* td, float* loss, vo
 
 static int forward_q(dqz_learner* L, const float* params, const Conv1Src& src, int which, int n, float* q_out,
                      hipStream_t st) {
-  NetZ nz;
+  NetZ nz{};
   nz.p[0] = nz.p[1] = nz.p[2] = params;
   nz.which[0] = nz.which[1] = nz.which[2] = which;
-  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile, true)) return rc;
+  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile)) return rc;
   HeadArgs h = make_head(L, nz, 1, n);
   h.fwd_only = 1;
   h.q = q_out;
@@ -620,11 +609,11 @@ int dqz_act(dqz_learner* L, const float* params, const uint8_t* states, int n, d
   if (int rc = device_view(out, &dout, "out")) return rc;
   if (reinterpret_cast<uintptr_t>(dstates) % 16) return fail(DQZ_ERR_INVALID, "states must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
-  NetZ nz;
+  NetZ nz{};
   nz.p[0] = nz.p[1] = nz.p[2] = params;
   nz.which[0] = nz.which[1] = nz.which[2] = 0;
   Conv1Src src{nullptr, nullptr, nullptr, static_cast<const uint8_t*>(dstates), 0, UniformDraw{}};
-  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile, true)) return rc;
+  if (int rc = forward_impl(L, nz, 1, n, src, st, kNoProfile)) return rc;
   HeadArgs h = make_head(L, nz, 1, n);
   h.fwd_only = 1;
   h.q = L->q;
@@ -1248,7 +1237,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     }
   }
 
-  MetaRmsArgs ra;
+  MetaRmsArgs ra{};
   ra.lr = H->cfg.learning_rate;
   ra.decay = H->cfg.decay;
   ra.c1 = (float)(1.0 - (double)H->cfg.decay);
@@ -1296,7 +1285,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
                            nullptr, nullptr, nullptr, &epi))
       return rc;
     const int nparts1 = 4 * (FLAT / 16) + (int)update_blocks(L1->sz, A, L1->shared_bias ? 1 : A);
-    HvpArgs hv;
+    HvpArgs hv{};
     hv.frames = S1->frames;
     hv.fidx = S1->fidx;
     hv.slot = online_slot;
@@ -1350,7 +1339,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   // Tangent forward over the stored online activations: V * y + vb per layer,
   // chunk by chunk (K > 1: the chunk's forward / backward is recomputed first
   // so L holds its activations and p-weighted backward signals).
-  NetZ nv;
+  NetZ nv{};
   nv.p[0] = nv.p[1] = nv.p[2] = v;
   nv.which[0] = nv.which[1] = nv.which[2] = 0;
   for (int k = 0; k < K; ++k) {
@@ -1358,7 +1347,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     if (K > 1) {
       if (int rc = step_impl(L, P, S, ks, nullptr, stream, kNoProfile, H->Gs, H->p + (int64_t)k * C)) return rc;
     }
-    Conv1FwdArgs c1;
+    Conv1FwdArgs c1{};
     c1.src = Conv1Src{S->frames, S->fidx, ks, nullptr, 0, UniformDraw{}};
     c1.nz = nv;
     c1.w_off = L->off[0];
@@ -1367,7 +1356,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     c1.Z = 1;
     c1.linear = 1;
     c1.out = H->zv1;
-    LayerFwdArgs c2;
+    LayerFwdArgs c2{};
     c2.in = L->y1;
     c2.nz = nv;
     c2.w_off = L->off[2];
@@ -1381,7 +1370,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     c3.w_off = L->off[4];
     c3.b_off = L->off[5];
     c3.out = H->zv3;
-    Fc1FwdArgs f1;
+    Fc1FwdArgs f1{};
     f1.in = L->y3;
     f1.nz = nv;
     f1.w_off = L->off[6];
@@ -1402,7 +1391,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     DQZ_HIP(hipGetLastError());
     if (K == 1) break;
 
-    MetaDotArgs md;
+    MetaDotArgs md{};
     md.dy1 = L->dy1;
     md.dy2 = L->dy2;
     md.dy3 = L->dy3;
@@ -1426,7 +1415,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     DQZ_HIP(hipGetLastError());
   }
 
-  MetaAdamArgs ad;
+  MetaAdamArgs ad{};
   ad.x = H->x;
   ad.p = H->p;
   ad.s = H->s;
@@ -1491,7 +1480,7 @@ extern "C" int dqz_debug_trace(unsigned long long* host_out, int clear) {
 // Atari observation preprocessing (processors.py:488-497)
 
 struct dqz_frame_plan {
-  FramePlan p;
+  FramePlan p{};
   void* block;
 };
 

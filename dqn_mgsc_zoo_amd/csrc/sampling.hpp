@@ -694,9 +694,14 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
     int32_t* __restrict__ out_slots, int64_t* __restrict__ out_idx) {
   int* done = sync.words + SampleSync::kStride;
   const int q = blockIdx.x;
-  const uint64_t ctr = uniforms ? 0 : *counter;
-  const int64_t idx = softmax_choice_body(x, n, run, csum, nblocks, [&] {
-    return uniforms ? uniforms[q] : philox_uniform(seed, ctr, q);
+  // the counter is loaded inside the draw (as softmax_draw_slot does), so
+  // csum_level1 issues the chunk-sum loads first; wave 0, thread 0 included,
+  // runs the lambda, and thread 0 keeps the value for the final increment
+  uint64_t ctr = 0;
+  const int64_t idx = softmax_choice_body(x, n, run, csum, nblocks, [&]() -> double {
+    if (uniforms) return uniforms[q];
+    ctr = *counter;
+    return philox_uniform(seed, ctr, q);
   });
   if (threadIdx.x == 0) {
     if (out_slots) out_slots[q] = (int32_t)idx;

@@ -22,6 +22,42 @@ import torch
 STORE_FILE_ENV = 'DQZ_STORE_FILE'
 
 
+def device_identity(local_rank, stand_in=None):
+  """What a rank's device is: name, PCI location and UUID.
+
+  `stand_in` (a string) replaces the hardware query in the CPU self-test,
+  where there is no device to ask.
+  """
+  if stand_in is not None:
+    return {'name': 'cpu stand-in', 'pci': stand_in, 'uuid': stand_in}
+  p = torch.cuda.get_device_properties(local_rank)
+  pci = '%04x:%02x:%02x' % (int(p.pci_domain_id), int(p.pci_bus_id),
+                            int(p.pci_device_id))
+  return {'name': p.name, 'pci': pci, 'uuid': str(p.uuid)}
+
+
+def check_devices(identities, expected_world):
+  """Errors of an N-rank run's device set: every rank on its own device.
+
+  identities: one device_identity() per rank, in rank order.  Returns a list
+  of messages (empty when the world is the expected size and no two ranks
+  share a PCI location or a UUID).
+  """
+  errors = []
+  if len(identities) != expected_world:
+    errors.append('world %d != --gpus %d' % (len(identities), expected_world))
+  for key in ('pci', 'uuid'):
+    seen = {}
+    for r, ident in enumerate(identities):
+      v = ident.get(key)
+      if v in seen:
+        errors.append('ranks %d and %d report the same device (%s %s)'
+                      % (seen[v], r, key, v))
+      else:
+        seen[v] = r
+  return errors
+
+
 class Replicas:
   """Rank bookkeeping + the two reporting collectives."""
 
@@ -83,6 +119,14 @@ class Replicas:
     out = [torch.zeros_like(v) for _ in range(self.world)]
     self.dist.all_gather(out, v)
     return torch.stack(out).cpu().numpy()
+
+  def gather_objects(self, obj):
+    """All-gather a picklable python object from every rank -> list."""
+    if self.dist is None:
+      return [obj]
+    out = [None] * self.world
+    self.dist.all_gather_object(out, obj)
+    return out
 
   def close(self):
     if self.dist is not None and self.dist.is_initialized():

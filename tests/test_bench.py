@@ -95,6 +95,27 @@ def test_gpus2_spawns_two_ranks_gloo():
   assert out['rccl']['backend'] == 'gloo' and out['rccl']['world'] == 2
   assert out['rccl']['last_in_loop_gather']['steps_done'] == [25, 25]
   assert len(out['rccl']['last_in_loop_gather']['value']) == 2
+  # each rank's device identity (stand-ins on CPU), all distinct
+  assert [d['pci'] for d in out['devices']] == ['stand-in-0', 'stand-in-1']
+
+
+def test_gpus2_same_device_fails():
+  """Two ranks reporting one device make the line invalid (exit 4)."""
+  p = _run_bench(['--gpus', '2', '--steps', '4', '--warmup', '0',
+                  '--selftest-cpu'], env={'DQZ_SELFTEST_DEVICE': 'dup'})
+  assert p.returncode == 4, p.stderr[-2000:]
+  assert 'report the same device' in p.stderr
+  assert not [l for l in p.stdout.splitlines() if l.startswith('{')]
+
+
+def test_check_devices():
+  from dqn_mgsc_zoo_amd import replicas  # pylint: disable=g-import-not-at-top
+  ids = [{'pci': '0000:%02x:00' % i, 'uuid': 'u%d' % i} for i in range(4)]
+  assert replicas.check_devices(ids, 4) == []
+  assert replicas.check_devices(ids, 8) == ['world 4 != --gpus 8']
+  ids[3] = dict(ids[1])
+  errs = replicas.check_devices(ids, 4)
+  assert len(errs) == 2 and all('ranks 1 and 3' in e for e in errs)
 
 
 def test_gpus1_forms_a_process_group():
