@@ -777,6 +777,13 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // leading workgroups: wave 0 of the first runs per_write_back_wave beside the
 // whole backward (the TD errors are final since the head), the other seven
 // exit at once (the sample ranges keep their XCD alignment).
+// Timing-only experiment switches (never set in a product build; the
+// numerics of a build with them are wrong): DQZ_EXP_SKIP bit 0 skips the fc1
+// dW range, bit 1 conv3 dW, bit 2 conv2 dW, bit 3 conv1 dW (skipped
+// consumers still pass their hand-off waits, so the words stay balanced).
+#ifndef DQZ_EXP_SKIP
+#define DQZ_EXP_SKIP 0
+#endif
 template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
@@ -807,6 +814,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
   i -= 8 * B8;
   if (i < NF) {
+    if (DQZ_EXP_SKIP & 1) return;
     fc1_dw_body(f1, smem, i);
     return;
   }
@@ -823,6 +831,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   if (i < 4 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
     if (!sj.valid) return;
+    if (DQZ_EXP_SKIP & 2) return;
     DQZ_STAMP(12, 0);
     conv3_bwd_dw(c3, smem, sj.s, sj.job);
     DQZ_STAMP(12, 3);
@@ -835,12 +844,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c1.B);
     if (!sj.valid) return;
+    if (DQZ_EXP_SKIP & 8) {
+      c1.sync1.wait(sj.s);
+      return;
+    }
     conv1_dw_half(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
     return;
   }
   i -= 8 * B8;
   const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
   if (!sj.valid) return;
+  if (DQZ_EXP_SKIP & 4) {
+    c2.sync.wait(sj.s);
+    return;
+  }
   DQZ_STAMP(13, 0);
   conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
   DQZ_STAMP(13, 3);

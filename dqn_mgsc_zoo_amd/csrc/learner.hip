@@ -1077,6 +1077,14 @@ int dqz_target_copy(float* target, const float* online, int64_t total, void* str
 // ---------------------------------------------------------------------------
 // MGSC meta-update (meta.hpp)
 
+// The meta-update's tangent conv part as dot products with the per-sample
+// gradient slabs (tangent_slab_kernel, default) or as the linear conv forward
+// with dot-product epilogues (tangent_fwd_kernel, -DDQZ_META_SLAB=0 for A/B).
+#ifndef DQZ_META_SLAB
+#define DQZ_META_SLAB 1
+#endif
+constexpr bool kMetaSlabDots = DQZ_META_SLAB != 0;
+
 struct dqz_meta {
   dqz_meta_config cfg;
   // Meta batches larger than the learner's MAXB run in K chunks of C samples
@@ -1384,6 +1392,24 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
       c3.dot = TangentDot{L->dy3, H->dotp, 8};
       f1.dot = TangentDot{L->dz1, H->dotp, 12};
       ex = MetaExtra{L->dz1, L->h1, L->gq, L->ga, v, L->off[7], L->off[8], L->off[9], A, H->dotp};
+    }
+    if (K == 1 && kMetaSlabDots) {
+      // the conv layers' dot products from the batch backward's per-sample
+      // gradient slabs, beside the fc1 tangent range (meta.hpp SlabDotArgs)
+      SlabDotArgs sd{};
+      sd.p1 = L->p1;
+      sd.p2 = L->p2;
+      sd.p3 = L->p3;
+      sd.v = v;
+      sd.off1 = L->off[0];
+      sd.off2 = L->off[2];
+      sd.off3 = L->off[4];
+      sd.part = H->dotp;
+      sd.M = C;
+      hipLaunchKernelGGL(tangent_slab_kernel, dim3((unsigned)tangent_slab_blocks(C, f1.MG)), dim3(256), 0, st, sd,
+                         f1, ex);
+      DQZ_HIP(hipGetLastError());
+      break;
     }
     // the four layers' tangent outputs are independent: one launch
     hipLaunchKernelGGL(tangent_fwd_kernel, dim3((unsigned)tangent_fwd_blocks(C, f1.MG)), dim3(256), kConv1FwdSmem,

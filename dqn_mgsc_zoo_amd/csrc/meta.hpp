@@ -146,6 +146,90 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
   fc1_fwd_block32(f1, smem, i - n);
 }
 
+// ---- the tangent's conv part from the per-sample gradient slabs -----------
+// The B = M backward already leaves, per sample b, the p-weighted gradient of
+// every conv layer as a dW partial slab (slab_b = p_b g_b: conv1 [4 row
+// blocks][257][32], conv2 [513][64], conv3 [577][64], bias rows last, rows in
+// the parameter layout, each layer's w and b leaves contiguous).  The conv
+// ranges of tangent_fwd_kernel compute sum over positions of
+// <dz_l, V_l y_{l-1} + vb_l>, which is <v_l, p_b g_l^b>: the same number as the
+// dot product of v with those slabs.  So the tangent launch keeps only its fc1
+// range (and the fc1-bias / fc2 terms) and the conv layers become 12 dot
+// products per sample over 411 KB of slabs (MALL-resident, written one launch
+// earlier) instead of a linear conv forward of the meta batch (1.1 GMAC at
+// M = 100).  Slots as before: conv1 row block rb -> rb, conv2 / conv3 row
+// quarter q -> 4 + q / 8 + q.
+struct SlabDotArgs {
+  const float* p1;  // [M][4][257][32]
+  const float* p2;  // [M][513][64]
+  const float* p3;  // [M][577][64]
+  const float* v;   // tangent (param layout)
+  int64_t off1, off2, off3;  // v offsets of the conv1 / conv2 / conv3 w leaves (b follows w)
+  float* part;      // [M][META_DOT_SLOTS]
+  int M;
+};
+constexpr int SLAB_DOT_JOBS = 12;
+
+__device__ __forceinline__ void slab_dot_body(const SlabDotArgs& a, int b, int j, float* s_tmp) {
+  constexpr int N1 = (C1KK + 1) * C1CO / 4, N2 = (C2KK + 1) * C2CO / 4, N3 = (C3KK + 1) * C3CO / 4;  // float4s
+  const float4* src;
+  const float4* vv;
+  int n;
+  if (j < 4) {
+    src = reinterpret_cast<const float4*>(a.p1) + ((int64_t)b * C1_BLOCKS + j) * N1;
+    vv = reinterpret_cast<const float4*>(a.v + a.off1);
+    n = N1;
+  } else if (j < 8) {
+    const int q0 = (j - 4) * N2 / 4, q1 = (j - 3) * N2 / 4;
+    src = reinterpret_cast<const float4*>(a.p2) + (int64_t)b * N2 + q0;
+    vv = reinterpret_cast<const float4*>(a.v + a.off2) + q0;
+    n = q1 - q0;
+  } else {
+    const int q0 = (j - 8) * N3 / 4, q1 = (j - 7) * N3 / 4;
+    src = reinterpret_cast<const float4*>(a.p3) + (int64_t)b * N3 + q0;
+    vv = reinterpret_cast<const float4*>(a.v + a.off3) + q0;
+    n = q1 - q0;
+  }
+  constexpr int R = (N3 / 4 + 255) / 256;  // 10 float4 pairs per thread at most
+  static_assert(N1 <= 256 * R && N2 / 4 + 1 <= 256 * R && N3 / 4 + 1 <= 256 * R, "slab part per block");
+  float4 x[R], y[R];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {  // every load in flight before the first product
+    const int i = min(t + 256 * r, n - 1);
+    x[r] = src[i];
+    y[r] = vv[i];
+  }
+  float d = 0.f;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (t + 256 * r < n) d += (x[r].x * y[r].x + x[r].y * y[r].y) + (x[r].z * y[r].z + x[r].w * y[r].w);
+  d = block_sum256(d, s_tmp);
+  if (t == 0) a.part[(int64_t)b * META_DOT_SLOTS + j] = d;
+}
+
+// The tangent launch with one meta chunk: [fc1 tiles] [12 slab dots per
+// sample], the fc1-bias / fc2 term (slot META_EXTRA_SLOT) by each sample's
+// first slab-dot block.  Static LDS (fc1's four 32 x 32 tiles, 16.9 KB):
+// every block of the grid is resident at once.
+inline int tangent_slab_blocks(int M, int MG) { return fc1_fwd_blocks(1, MG) + SLAB_DOT_JOBS * M; }
+__global__ __launch_bounds__(256) void tangent_slab_kernel(SlabDotArgs sd, Fc1FwdArgs f1, MetaExtra ex) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * FC1_32RW];
+  const int nf = (HID / 32) * FC1_S * f1.MG;  // fc1_fwd_blocks(1, MG)
+  int i = blockIdx.x;
+  if (i < nf) {
+    fc1_fwd_block32(f1, smem, i);
+    return;
+  }
+  i -= nf;
+  const int b = i / SLAB_DOT_JOBS, j = i % SLAB_DOT_JOBS;
+  slab_dot_body(sd, b, j, smem);
+  if (j == 0) {
+    __syncthreads();
+    meta_extra_term(ex, b, smem);
+  }
+}
+
 struct MetaRmsArgs {
   float lr, decay, c1, eps;
   int64_t n4;  // total / 4 (float4 granules)

@@ -452,3 +452,142 @@ def test_config4_fused_step_per_draw_1m(device, store):
   np.testing.assert_allclose(tree.storage[1:], host.sum_tree.storage[1:],
                              rtol=1e-15, atol=0)
   assert max_seen.item() == max(1.0, pr.max())
+
+
+def _rel_norm_err(got, want):
+  worst = 0.0
+  for m in want:
+    for n in want[m]:
+      w = np.asarray(want[m][n], np.float64)
+      d = np.linalg.norm(np.asarray(got[m][n], np.float64) - w)
+      worst = max(worst, d / max(np.linalg.norm(w), 1e-30))
+  return worst
+
+
+def _check_step_unfiltered(lrn, ref, online, target, what):
+  """The bars of test_learner_gpu.test_learner_step_on_unfiltered_batches:
+  q / td / loss elementwise (a ReLU kink moves gradient entries, not the
+  forward), the gradient (mu after one step from zero is (1 - decay) g) and
+  the parameter update within a relative Frobenius norm per leaf."""
+  q, td, loss = lrn.fetch_outputs()
+  torch.cuda.synchronize()
+  np.testing.assert_allclose(q.cpu().numpy(), ref['q_tm1'], atol=Q_ATOL)
+  np.testing.assert_allclose(td.cpu().numpy(), ref['td'], atol=Q_ATOL)
+  np.testing.assert_allclose(loss.cpu().numpy()[0], ref['loss'], rtol=1e-4,
+                             atol=1e-7)
+  g_err = _rel_norm_err(lrn.params_tree('mu'), ref['mu'])
+  after = lrn.params_tree('online')
+  delta_got = {m: {n: after[m][n] - online[m][n] for n in online[m]}
+               for m in online}
+  delta_want = {m: {n: ref['params'][m][n] - online[m][n] for n in online[m]}
+                for m in online}
+  u_err = _rel_norm_err(delta_got, delta_want)
+  print('%s: gradient rel err %.2e, update rel err %.2e' % (what, g_err, u_err))
+  assert g_err <= 1e-5, g_err
+  assert u_err <= 1e-3, u_err
+  _compare_tree(lrn.params_tree('target'), target, 0.0, what='target')
+  assert lrn.sync_status() == 0
+
+
+def test_unfiltered_batches_1m(device, store):
+  """one batch per config 2 / 3 / 4 at C = 1M taken as
+  the sampler's stream gives it — no kink-free advance — through the fused
+  one-call steps the bench times (dqz_learner_step_uniform /
+  _step_logits / _step_per_draw).  Index work stays bit-exact; q / td at
+  1e-4, the gradient and update at the relative-norm bars of the small-store
+  unfiltered test (dqn/agent.py:85-107, prioritized/agent.py:86-113)."""
+  from dqn_mgsc_zoo_amd import _native
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  net = networks.dqn_atari_network(A)
+
+  # config 2: the first Philox batch of the stream
+  online = net.init(31)
+  target = helpers.perturbed_tree(online, 32)
+  lrn = learner_lib.Learner(net, B, algo='dqn', device=device)
+  lrn.set_params(online, target)
+  seed = 4321
+  counter = torch.zeros((1,), dtype=torch.int64, device=device)
+  preview = torch.empty((B,), dtype=torch.int32, device=device)
+  learner_lib.sample_uniform(0, CAP, CAP, B, seed, counter.clone(), preview)
+  out = torch.empty((B,), dtype=torch.int32, device=device)
+  lrn.step_uniform(store, 0, CAP, CAP, seed, counter, out)
+  torch.cuda.synchronize()
+  slots = out.cpu().numpy()
+  np.testing.assert_array_equal(slots, preview.cpu().numpy())
+  batch = _host_batch(store, slots)
+  z = learner_ref.zeros_like_tree(online)
+  s_tm1, a, r, d, s_t = batch
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t)
+  print('config 2 margin %.2e' % learner_ref.relu_margin(online, s_tm1))
+  _check_step_unfiltered(lrn, ref, online, target, 'config 2')
+
+  # config 3: the learned-logit draw of the Generator's first uniforms
+  rng = np.random.default_rng(33)
+  logits = rng.standard_normal(CAP).astype(np.float32)
+  dev = rc._DeviceLogits(CAP, device, max_queries=512)  # pylint: disable=protected-access
+  dev.load(logits)
+  online = net.init(34)
+  target = helpers.perturbed_tree(online, 35)
+  lrn = learner_lib.Learner(net, B, algo='dqn', device=device)
+  lrn.set_params(online, target)
+  u = np.random.default_rng(36).random(B)
+  want = dev.sample_abs(u).cpu().numpy()
+  lrn.step_logits(store, dev, out,
+                  uniforms=torch.as_tensor(u, dtype=torch.float64, device=device))
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(out.cpu().numpy(), want)
+  s_tm1, a, r, d, s_t = _host_batch(store, want)
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t)
+  print('config 3 margin %.2e' % learner_ref.relu_margin(online, s_tm1))
+  _check_step_unfiltered(lrn, ref, online, target, 'config 3')
+
+  # config 4: the PER draw for RandomState(0), double-Q net with IS weights
+  alpha, usp, beta = 0.6, 1e-3, 0.4
+  host = replay_lib.PrioritizedDistribution(
+      alpha, usp, np.random.RandomState(0), min_capacity=CAP, max_capacity=CAP)
+  ids = np.arange(CAP)
+  host._assign_indices(ids)  # pylint: disable=protected-access
+  index = host.index_of(ids)
+  leaves = np.zeros(CAP)
+  leaves[index] = replay_lib._power(rng.uniform(0.01, 2.0, CAP), alpha)  # pylint: disable=protected-access
+  host.sum_tree.set_all(leaves)
+  host.note_priorities(leaves)
+  dist = copy.deepcopy(host)
+  dist.to_device(device)
+  tree = dist.sum_tree
+  tree.index_to_slot[torch.as_tensor(index, device=device)] = torch.as_tensor(
+      ids.astype(np.int32), device=device)
+  want_ids, want_probs = host.sample(B)
+  dist._random_state = np.random.RandomState(0)  # pylint: disable=protected-access
+  uniform_idx, uu = dist.draw(B)
+  dnet = networks.double_dqn_atari_network(A)
+  online = dnet.init(37)
+  target = helpers.perturbed_tree(online, 38)
+  lrn = learner_lib.Learner(dnet, B, algo='per', device=device)
+  lrn.set_params(online, target)
+  inj_i = torch.from_numpy(uniform_idx).to(device)
+  inj_u = torch.from_numpy(uu).to(device)
+  idx = torch.empty((B,), dtype=torch.int32, device=device)
+  slots = torch.empty((B,), dtype=torch.int32, device=device)
+  w = torch.empty((B,), dtype=torch.float32, device=device)
+  probs = torch.empty((B,), dtype=torch.float64, device=device)
+  max_seen = torch.ones((1,), dtype=torch.float64, device=device)
+  p = _native.ptr
+  draw = _native.DqzPerDraw(
+      p(tree.tree).value, tree.capacity, 0, CAP, CAP, usp, beta, 1, 0, None,
+      p(inj_i).value, p(inj_u).value, p(tree.index_to_slot).value, alpha,
+      p(max_seen).value, p(idx).value, p(slots).value, p(probs).value,
+      p(w).value)
+  lrn.step_per_draw(store, draw)
+  torch.cuda.synchronize()
+  assert slots.cpu().numpy().tolist() == want_ids.tolist()
+  assert probs.cpu().numpy().tolist() == want_probs.tolist()
+  s_tm1, a, r, d, s_t = _host_batch(store, want_ids)
+  z = learner_ref.zeros_like_tree(online)
+  ref = learner_ref.learner_step(online, target, z, z, s_tm1, a, r, d, s_t,
+                                 algo='per', weights=w.cpu().numpy())
+  print('config 4 margin %.2e' % learner_ref.relu_margin(online, s_tm1))
+  _check_step_unfiltered(lrn, ref, online, target, 'config 4')

@@ -13,7 +13,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')
+LIB = os.environ.get('DQZ_TRACE_LIB') or os.path.join(ROOT, 'dqn_mgsc_zoo_amd', 'libdqz_trace.so')  # prebuilt variants
 sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 if os.environ.get('DQZ_TRACE_PREBUILT') != '1':  # 1: libdqz_trace.so was built beforehand (off the GPU box)
