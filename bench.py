@@ -964,6 +964,14 @@ def run_agent(args):
     orig_learn()
 
   agent._learn = learn  # pylint: disable=protected-access
+  counts['target_syncs'] = 0
+  orig_sync = agent._learner.sync_target  # pylint: disable=protected-access
+
+  def sync_target():
+    counts['target_syncs'] += 1
+    orig_sync()
+
+  agent._learner.sync_target = sync_target  # pylint: disable=protected-access
   env = synthetic.SyntheticAtari(episode_len=27_000, seed=1 + rank,
                                  num_actions=NUM_ACTIONS)
   loop = parts.run_loop(agent, env, max_steps_per_episode=108_000)
@@ -978,6 +986,7 @@ def run_agent(args):
   _barrier(reps)
   torch.cuda.synchronize(dev)
   start = counts['learn']
+  syncs0 = counts['target_syncs']
   frames = 0
   t0 = time.perf_counter()
   while counts['learn'] - start < args.steps:
@@ -1023,9 +1032,12 @@ def run_agent(args):
                              'raw frames through processors.atari (device '
                              'observation math), TransitionReplay(capacity=%d, '
                              'RandomState), batch=32, learn_period=16, '
-                             'min_replay_capacity_fraction=%g, A=%d' % (
-                                 args.capacity, args.min_replay_fraction,
-                                 NUM_ACTIONS),
+                             'min_replay_capacity_fraction=%g, '
+                             'target_network_update_period=40000 frames, '
+                             'A=%d' % (args.capacity, args.min_replay_fraction,
+                                       NUM_ACTIONS),
+                 'target_update_period_frames': 40_000,
+                 'min_replay_capacity_fraction': args.min_replay_fraction,
                  'global_batch': BATCH * world, 'replay_capacity': args.capacity,
                  'parallelism': 'independent-seed replicas x%d' % world},
       'frames': frames,
@@ -1039,6 +1051,7 @@ def run_agent(args):
       'replay_size': replay.size,
       'replay_valid': bool(ok),
       'fill_frames': fill_frames,
+      'target_syncs_timed': counts['target_syncs'] - syncs0,
       'fill_s': round(fill_s, 2),
       'handoff_status': int(status) & 1,
       'params_finite': finite,

@@ -784,6 +784,11 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 #ifndef DQZ_EXP_SKIP
 #define DQZ_EXP_SKIP 0
 #endif
+// A/B: the fc1 dW range last in the grid (after conv2 dW) instead of second
+#ifndef DQZ_BWD_FC1_LAST
+#define DQZ_BWD_FC1_LAST 0
+#endif
+constexpr bool kBwdFc1Last = DQZ_BWD_FC1_LAST != 0;
 template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
@@ -813,12 +818,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  if (i < NF) {
-    if (DQZ_EXP_SKIP & 1) return;
-    fc1_dw_body(f1, smem, i);
-    return;
+  if (!kBwdFc1Last) {
+    if (i < NF) {
+      if (DQZ_EXP_SKIP & 1) return;
+      fc1_dw_body(f1, smem, i);
+      return;
+    }
+    i -= NF;
   }
-  i -= NF;
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
@@ -852,6 +859,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
+  if (kBwdFc1Last && i >= 8 * B8) {
+    i -= 8 * B8;
+    if (DQZ_EXP_SKIP & 1) return;
+    fc1_dw_body(f1, smem, i);
+    return;
+  }
   const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
   if (!sj.valid) return;
   if (DQZ_EXP_SKIP & 4) {

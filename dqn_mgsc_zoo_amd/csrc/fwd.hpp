@@ -35,6 +35,24 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // the same banks; a 32-lane read group covers rows 2j, 2j + 1 of one 4-row
 // block, so the position-major reads stay conflict-free.
 __device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + 16 * (row >> 2) + col; }
+
+// Epilogues that read four channels of a reduction row per lane
+// (ds_read_b128): a 64-lane wave covers 16 rows, and the LDS serves it in
+// four 16-lane groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, ... (four
+// rows each).  With row = lane / 4, two rows of a group share a bank quad in
+// the padded layout (row start 16 (row + row / 4) mod 64 dwords): 2-way
+// conflicts in every group.  This order gives each group four rows whose
+// starts are 0, 16, 32, 48 mod 64: lane quad q of the wave's 16 takes row
+// 16 (i / 64) + kEpiPerm[q].  Every row of [0, 16 ceil(rows / 16)) is visited
+// once, so loops run i over that range and skip rows past the end.
+#ifndef DQZ_EPI_PERM
+#define DQZ_EPI_PERM 1
+#endif
+__device__ __forceinline__ int epi_row(int i) {
+  if (!DQZ_EPI_PERM) return i >> 2;
+  return ((i >> 6) << 4) + (int)((0xFBAE9DC873261540ull >> (4 * ((i >> 2) & 15))) & 15);
+}
+constexpr int epi_range(int rows) { return (rows + 15) / 16 * 64; }
 constexpr int red_rows(int rows) { return rows * 16 + 16 * ((rows + 3) / 4); }
 
 struct LayerFwdArgs {
@@ -144,8 +162,9 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
     // y2 handed to conv3: 4 channels per lane, one 16-byte write-through store
     // each (324 per block instead of 1,296 4-byte ones, which the guide prices
     // at ~6x per byte; same values)
-    for (int i = t; i < C2M * 4; i += 256) {
-      const int p = i >> 2, c4 = 4 * (i & 3);
+    for (int i = t; i < epi_range(C2M); i += 256) {
+      const int p = epi_row(i), c4 = 4 * (i & 3);
+      if (p >= C2M) continue;
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -248,8 +267,9 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
   float* out = a.out + ((int64_t)z * a.B + b) * (C2M * C2CO) + oh0 * C2O * C2CO + 16 * nq;
   const int out_bytes = (C2M * C2CO - oh0 * C2O * C2CO - 16 * nq) * 4;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
-  for (int i = t; i < npos * 4; i += 256) {
-    const int p = i >> 2, c4 = 4 * (i & 3);
+  for (int i = t; i < epi_range(npos); i += 256) {
+    const int p = epi_row(i), c4 = 4 * (i & 3);
+    if (p >= npos) continue;
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -443,8 +463,9 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + oh0 * C3O * C3CO + 16 * nq;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
-  for (int i = t; i < npos * 4; i += 256) {
-    const int p = i >> 2, c4 = 4 * (i & 3);
+  for (int i = t; i < epi_range(npos); i += 256) {
+    const int p = epi_row(i), c4 = 4 * (i & 3);
+    if (p >= npos) continue;
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -529,6 +550,16 @@ struct Fc1FwdArgs {
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
+// fc1 forward's load order: every W1 load issued before the y3 loads (round
+// 3's order; round 4's interleaved order made the kernel 0.2-0.3 us slower,
+// fc1 4.90-4.96 -> 4.69-4.75 us back to back and 16,171 -> 16,248 steps/s,
+// three interleaved rounds, profiles/r05/c2).  0 keeps the interleaved order.
+#ifndef DQZ_FC1_LOADS_W_FIRST
+#define DQZ_FC1_LOADS_W_FIRST 1
+#endif
+// DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
+// of partial stores); the learner's fc1_fwd32_kernel compiles without it.
+template <bool DOT>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
@@ -543,12 +574,21 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
   float4 av[G];
+#if DQZ_FC1_LOADS_W_FIRST
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
+#pragma unroll
+  for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
+#else
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   }
+#endif
   f32x16 acc = {};
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -569,7 +609,7 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
     const int k = q * 33 + c4 + e;
     v[e] = (s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k]);
   }
-  if (a.dot.part) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
+  if (DOT) {  // this split's share of <V_fc1 y3, dz1> for row q: 8 lanes x 4 columns
     float d = 0.f;
     if (live) {
       const float4 dz = *reinterpret_cast<const float4*>(a.dot.dy + (int64_t)(32 * mg + q) * HID + 32 * nt + c4);
@@ -592,7 +632,7 @@ inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 __global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_32RW];
-  fc1_fwd_block32(a, s_red, blockIdx.x);
+  fc1_fwd_block32<false>(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 

@@ -1084,6 +1084,12 @@ int dqz_target_copy(float* target, const float* online, int64_t total, void* str
 #define DQZ_META_SLAB 1
 #endif
 constexpr bool kMetaSlabDots = DQZ_META_SLAB != 0;
+// Meta Adam fused with the chunk re-sums of the logits it writes
+// (meta_adam_chunks_kernel, default) or the two launches (-DDQZ_META_ADAM_CHUNKS=0).
+#ifndef DQZ_META_ADAM_CHUNKS
+#define DQZ_META_ADAM_CHUNKS 1
+#endif
+constexpr bool kMetaAdamChunks = DQZ_META_ADAM_CHUNKS != 0;
 
 struct dqz_meta {
   dqz_meta_config cfg;
@@ -1105,6 +1111,7 @@ struct dqz_meta {
   float *GQ, *HQ, *s1_part, *hpart;
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
   float* dotp;  // [C][META_DOT_SLOTS] the tangent launch's dot-product partials (one chunk)
+  int* arrive;  // meta_adam_chunks_kernel's re-seed arrival counter (zero between launches)
   int nparts2;
   void* block;
 };
@@ -1151,13 +1158,13 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
                            so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID,
-                           (int64_t)C * META_DOT_SLOTS};
+                           (int64_t)C * META_DOT_SLOTS, 64};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
                     &H->ty1, &H->ty2, &H->ty3, &H->td4, &H->td3, &H->td2, &H->td1, &H->s1, &H->hpart,
-                    &H->dotp};
+                    &H->dotp, reinterpret_cast<float**>(&H->arrive)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
@@ -1467,6 +1474,13 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.run = keep ? logit_buf->run : nullptr;
   ad.dirty = keep ? logit_buf->dirty : nullptr;
   ad.n_logits = keep ? logit_buf->capacity : 0;
+  if (keep && K == 1 && M <= META_THREADS && kMetaAdamChunks) {
+    // Adam and the re-sums of the chunks it writes in one launch
+    MetaAdamChunks ck{logit_buf->csum, logit_buf->nblocks, H->arrive};
+    hipLaunchKernelGGL(meta_adam_chunks_kernel, dim3(logit_buf->nblocks), dim3(META_THREADS), 0, st, ad, ck);
+    DQZ_HIP(hipGetLastError());
+    return DQZ_OK;
+  }
   hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
   DQZ_HIP(hipGetLastError());
   if (keep) return chunk_sums(logit_buf, logits, true, st);

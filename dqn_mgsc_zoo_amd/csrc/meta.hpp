@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void tangent_fwd_kernel(Conv1FwdArgs c1, Layer
     if (ex.part && sj.job == 0) meta_extra_term(ex, sj.s, smem);
     return;
   }
-  fc1_fwd_block32(f1, smem, i - n);
+  if (f1.dot.part) fc1_fwd_block32<true>(f1, smem, i - n); else fc1_fwd_block32<false>(f1, smem, i - n);
 }
 
 // ---- the tangent's conv part from the per-sample gradient slabs -----------
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void tangent_slab_kernel(SlabDotArgs sd, Fc1Fw
   const int nf = (HID / 32) * FC1_S * f1.MG;  // fc1_fwd_blocks(1, MG)
   int i = blockIdx.x;
   if (i < nf) {
-    fc1_fwd_block32(f1, smem, i);
+    fc1_fwd_block32<true>(f1, smem, i);
     return;
   }
   i -= nf;
@@ -392,47 +392,95 @@ __device__ __forceinline__ float meta_s(const MetaAdamArgs& a, int i) {
   return acc;
 }
 
+// Sum of the tangent launch's dot-product partials of one entry (slots
+// 0 .. META_EXTRA_SLOT in order), from its row loaded as float4s.
+__device__ __forceinline__ float meta_s_row(const float4 (&r)[META_DOT_SLOTS / 4]) {
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < META_DOT_SLOTS / 4; ++k) {
+    acc += r[k].x;
+    if (4 * k + 1 <= META_EXTRA_SLOT) acc += r[k].y;
+    if (4 * k + 2 <= META_EXTRA_SLOT) acc += r[k].z;
+    if (4 * k + 3 <= META_EXTRA_SLOT) acc += r[k].w;
+    if (4 * k + 4 > META_EXTRA_SLOT) break;
+  }
+  return acc;
+}
+
+// Every global load the block needs for its first META_THREADS entries and
+// the first META_ADAM_LP x META_THREADS loss partials is issued before the
+// first reduction (the loops over the partials had issued one load per
+// dependent iteration); entries and partials past those take the loops.
+constexpr int META_ADAM_LP = 16;
 __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __shared__ float sbuf[META_THREADS / 64];
-  float st = 0.f;
-  for (int i = threadIdx.x; i < a.M; i += META_THREADS) st += meta_s(a, i);
+  const int t = threadIdx.x;
+  const bool own = t < a.M;
+  const int i0 = own ? t : 0;
+  float4 dr[META_DOT_SLOTS / 4];
+  float s0 = 0.f;
+  if (a.dot_part) {
+    const float4* q = reinterpret_cast<const float4*>(a.dot_part + (int64_t)i0 * META_DOT_SLOTS);
+#pragma unroll
+    for (int k = 0; k < META_DOT_SLOTS / 4; ++k) dr[k] = q[k];
+  } else {
+    s0 = a.s[i0];
+  }
+  float lpv[META_ADAM_LP];
+#pragma unroll
+  for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
+  const float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
+  const int32_t pos0 = a.pos[i0];
+  const int32_t cnt = *a.count + 1;
+  LogitRun r{0.0, 0.f, 0};
+  if (a.run) r = *a.run;
+  __builtin_amdgcn_sched_barrier(0);
+  if (a.dot_part) {
+    s0 = meta_s_row(dr);
+    if (own) a.s_out[t] = s0;
+  }
+  float st = own ? s0 : 0.f;
+  for (int i = t + META_THREADS; i < a.M; i += META_THREADS) st += meta_s(a, i);
   const float tot = block_sum_f32(st, sbuf);
   float lp = 0.f;
-  for (int j = threadIdx.x; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+#pragma unroll
+  for (int k = 0; k < META_ADAM_LP; ++k)
+    if (t + k * META_THREADS < a.nparts) lp += lpv[k];
+  for (int j = t + META_ADAM_LP * META_THREADS; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
   lp = block_sum_f32(lp, sbuf);
-  const int32_t cnt = *a.count + 1;
   const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
   __shared__ double dbuf[META_THREADS / 64];
   __shared__ int s_far;
-  if (threadIdx.x == 0) s_far = 0;
-  LogitRun r{0.0, 0.f, 0};
-  if (a.run) r = *a.run;
+  if (t == 0) s_far = 0;
   __syncthreads();
   double dS = 0.0;  // running-sum change of this thread's writes (positions are distinct)
-  for (int i = threadIdx.x; i < a.M; i += META_THREADS) {
-    const float g = (a.dot_part ? a.s_out[i] : a.s[i]) - a.p[i] * tot;
-    const float m = (1.f - a.b1) * g + a.b1 * a.m[i];
-    const float v = (1.f - a.b2) * (g * g) + a.b2 * a.v[i];
+  auto entry = [&](int i, float si, float xi, float pi, float mi, float vi, int32_t posi) {
+    const float g = si - pi * tot;
+    const float m = (1.f - a.b1) * g + a.b1 * mi;
+    const float v = (1.f - a.b2) * (g * g) + a.b2 * vi;
     const float mh = m / c1;
     const float vh = v / c2;
     a.m[i] = m;
     a.v[i] = v;
     a.dlogits[i] = g;
-    const float nx = a.x[i] + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
-    a.logits[a.pos[i]] = nx;
+    const float nx = xi + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+    a.logits[posi] = nx;
     if (r.valid) {
-      dS += run_term(nx, r.c) - run_term(a.x[i], r.c);
+      dS += run_term(nx, r.c) - run_term(xi, r.c);
       if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
-      a.dirty[a.pos[i] / SM_CHUNK] = 1;
+      a.dirty[posi / SM_CHUNK] = 1;
     }
-  }
+  };
+  if (own) entry(t, s0, x0, p0, m0, v0, pos0);
+  for (int i = t + META_THREADS; i < a.M; i += META_THREADS)
+    entry(i, a.dot_part ? a.s_out[i] : a.s[i], a.x[i], a.p[i], a.m[i], a.v[i], a.pos[i]);
   // the buffer's running log-sum-exp follows the M writes (what
   // dqz_logits_write does for them) and their chunks are flagged, so the next
   // add / sample needs no scan; a tripped guard re-seeds here (rare)
   if (a.run && r.valid) {
     __shared__ int s_reseed;
     dS = block_sum_f64(dS, dbuf);  // fixed order: deterministic
-    if (threadIdx.x == 0) {
+    if (t == 0) {
       const double before = r.S;
       r.S += dS;
       s_reseed = s_far || !run_ok(before, r.S, -INFINITY, r.c);
@@ -442,15 +490,231 @@ __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
     if (s_reseed) {
       block_rescan(a.logits, a.n_logits, a.run);
       const int nb = (int)((a.n_logits + SM_CHUNK - 1) / SM_CHUNK);
-      for (int k = threadIdx.x; k < nb; k += META_THREADS) a.dirty[k] = 1;
+      for (int k = t; k < nb; k += META_THREADS) a.dirty[k] = 1;
     }
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     *a.count = cnt;
     *a.loss = lp;
   }
 }
 
 __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a) { meta_adam_body(a); }
+
+// ---- meta Adam + the written chunks' sums in one launch -------------------
+// (one meta chunk, M <= META_THREADS, a logit buffer whose running state the
+// host vouches for).  The separate form ran meta_adam_kernel (one block) and
+// then chunk_sums_kernel over the flagged chunks: two launches and a boundary
+// for <= M chunk re-sums.  Here the grid is one block per logit chunk; a block
+// whose chunk holds none of the M positions exits at once (the leader, the
+// block of pos[0]'s chunk, never does).  Every remaining block forms the
+// whole Adam step in the same fixed order (so all of them agree on tot, the
+// new logits, dS and the re-seed decision bit for bit), stores the logits of
+// its own chunk and re-sums that chunk from an LDS copy patched with them;
+// the leader alone stores m, v, dlogits, s, the count, the loss and the
+// running state.  Dirty flags stay clear: every writer re-sums what it
+// writes.  A tripped guard (rare) is handled by the last of the active
+// blocks to arrive, after every block's logit stores drained write-through:
+// re-scan of the buffer and every chunk sum, with L2-bypassing loads.
+// 4-byte write-through (sc1) store of element e (the fused Adam's rare
+// re-seed path only: 4-byte sc1 stores cost ~6x the 16-byte ones per byte).
+__device__ __forceinline__ void store_sc1_f1(float* base, int bytes, int e, float v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, e * 4, 0, 16);
+}
+
+struct MetaAdamChunks {
+  double* csum;  // [nblocks]
+  int nblocks;
+  int* arrive;   // re-seed arrival counter (zero between launches)
+};
+
+__device__ __forceinline__ float rescan_sc1(const float* x, int64_t n, LogitRun* run, double* dbuf, float* fbuf) {
+  const int bytes = (int)(n * 4);
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) m = fmaxf(m, load_sc1_f1(x, bytes, (int)j));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) fbuf[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(fbuf[0], fbuf[1]), fmaxf(fbuf[2], fbuf[3]));
+  const float c = m == -INFINITY ? 0.f : m;
+  double sum = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += SM_THREADS) sum += run_term(load_sc1_f1(x, bytes, (int)j), c);
+  sum = block_sum_f64(sum, dbuf);
+  if (threadIdx.x == 0) *run = LogitRun{sum, c, 1};
+  __syncthreads();
+  return c;
+}
+
+__device__ __forceinline__ double chunk_sum_sc1(const float* x, int64_t n, int k, float c, double* s_wave) {
+  const int bytes = (int)(n * 4);
+  const int64_t base = (int64_t)k * SM_CHUNK + threadIdx.x * SM_PER_LANE;
+  float xv[SM_PER_LANE];
+  if (base + SM_PER_LANE <= n) {
+#pragma unroll
+    for (int q = 0; q < SM_PER_LANE / 4; ++q) {
+      const float4 f = load_sc1_f4(reinterpret_cast<const float4*>(x), bytes, (int)(base / 4) + q);
+      xv[4 * q] = f.x;
+      xv[4 * q + 1] = f.y;
+      xv[4 * q + 2] = f.z;
+      xv[4 * q + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < SM_PER_LANE; ++i) xv[i] = base + i < n ? load_sc1_f1(x, bytes, (int)(base + i)) : -INFINITY;
+  }
+  double lane = 0.0;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], c);
+  double tot;
+  (void)block_scan_excl_f64(lane, s_wave, &tot);
+  return tot;
+}
+
+__global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdamArgs a, MetaAdamChunks ck) {
+  static_assert(META_THREADS == SM_THREADS, "one thread per meta entry and per chunk lane");
+  __shared__ float s_chunk[SM_CHUNK];
+  __shared__ float sbuf[META_THREADS / 64];
+  __shared__ double dbuf[META_THREADS / 64];
+  __shared__ int s_act, s_far, s_reseed, s_last;
+  const int k = blockIdx.x, t = threadIdx.x;
+  const bool own = t < a.M;
+  const int i0 = own ? t : 0;
+  const int32_t pos0 = a.pos[i0];
+  const int lead = a.pos[0] / SM_CHUNK;
+  if (t == 0) {
+    s_act = 0;
+    s_far = 0;
+  }
+  __syncthreads();
+  const bool mine = own && pos0 / SM_CHUNK == k;
+  if (mine) s_act = 1;
+  __syncthreads();
+  const bool leader = k == lead;
+  if (!s_act) return;  // (the leader's chunk holds pos[0])
+  // this chunk's logits (before the writes) into LDS, under the Adam loads
+  float4 cv[SM_PER_LANE / 4];
+  {
+    const int64_t base = (int64_t)k * SM_CHUNK + t * SM_PER_LANE;
+#pragma unroll
+    for (int q = 0; q < SM_PER_LANE / 4; ++q) {
+      if (base + 4 * q + 3 < a.n_logits) {
+        cv[q] = *reinterpret_cast<const float4*>(a.logits + base + 4 * q);
+      } else {
+        float e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = base + 4 * q + u < a.n_logits ? a.logits[base + 4 * q + u] : -INFINITY;
+        cv[q] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  }
+  float4 dr[META_DOT_SLOTS / 4];
+  {
+    const float4* q = reinterpret_cast<const float4*>(a.dot_part + (int64_t)i0 * META_DOT_SLOTS);
+#pragma unroll
+    for (int u = 0; u < META_DOT_SLOTS / 4; ++u) dr[u] = q[u];
+  }
+  float lpv[META_ADAM_LP];
+  if (leader) {
+#pragma unroll
+    for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
+  }
+  const float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
+  const int32_t cnt = *a.count + 1;
+  LogitRun r = *a.run;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < SM_PER_LANE / 4; ++q) *reinterpret_cast<float4*>(s_chunk + t * SM_PER_LANE + 4 * q) = cv[q];
+  const float s0 = meta_s_row(dr);
+  const float tot = block_sum_f32(own ? s0 : 0.f, sbuf);
+  float lp = 0.f;
+  if (leader) {
+#pragma unroll
+    for (int u = 0; u < META_ADAM_LP; ++u)
+      if (t + u * META_THREADS < a.nparts) lp += lpv[u];
+    for (int j = t + META_ADAM_LP * META_THREADS; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+    lp = block_sum_f32(lp, sbuf);
+  }
+  const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
+  double dS = 0.0;
+  float nx = 0.f;
+  if (own) {  // meta_adam_body's arithmetic, in the same order
+    const float g = s0 - p0 * tot;
+    const float m = (1.f - a.b1) * g + a.b1 * m0;
+    const float v = (1.f - a.b2) * (g * g) + a.b2 * v0;
+    const float mh = m / c1;
+    const float vh = v / c2;
+    nx = x0 + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
+    if (leader) {
+      a.m[t] = m;
+      a.v[t] = v;
+      a.dlogits[t] = g;
+      a.s_out[t] = s0;
+    }
+    if (r.valid) {
+      dS = run_term(nx, r.c) - run_term(x0, r.c);
+      if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
+    }
+    if (mine) s_chunk[pos0 - k * SM_CHUNK] = nx;
+  }
+  if (!r.valid) {  // (the host vouches for the state, so not expected) as meta_adam_body: writes only
+    if (mine) a.logits[pos0] = nx;
+    if (leader && t == 0) {
+      *a.count = cnt;
+      *a.loss = lp;
+    }
+    return;
+  }
+  dS = block_sum_f64(dS, dbuf);  // fixed order: the same in every block (also a barrier for s_chunk / s_far)
+  if (t == 0) s_reseed = s_far || !run_ok(r.S, r.S + dS, -INFINITY, r.c);
+  __syncthreads();
+  const bool reseed = s_reseed;
+  if (!reseed) {
+    if (mine) a.logits[pos0] = nx;
+    float xv[SM_PER_LANE];
+#pragma unroll
+    for (int i = 0; i < SM_PER_LANE; ++i) xv[i] = s_chunk[t * SM_PER_LANE + i];
+    double lane = 0.0;
+#pragma unroll
+    for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], r.c);
+    double ctot;
+    (void)block_scan_excl_f64(lane, dbuf, &ctot);
+    if (t == 0) {
+      ck.csum[k] = ctot;
+      if (leader) {
+        r.S += dS;
+        *a.run = r;
+        *a.count = cnt;
+        *a.loss = lp;
+      }
+    }
+    return;
+  }
+  // re-seed (rare): logits out write-through, the last active block re-scans
+  if (mine) store_sc1_f1(a.logits, (int)(a.n_logits * 4), (int)pos0, nx);
+  if (leader && t == 0) {
+    *a.count = cnt;
+    *a.loss = lp;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // active blocks: the distinct chunks of pos[0 .. M)
+  int first = 0;
+  if (own) {
+    first = 1;
+    for (int j = 0; j < t; ++j)
+      if (a.pos[j] / SM_CHUNK == pos0 / SM_CHUNK) first = 0;
+  }
+  const int nact = (int)block_sum_f32((float)first, sbuf);
+  if (t == 0) s_last = __hip_atomic_fetch_add(ck.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nact - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (t == 0) __hip_atomic_store(ck.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float c = rescan_sc1(a.logits, a.n_logits, a.run, dbuf, sbuf);
+  for (int kk = 0; kk < ck.nblocks; ++kk) {
+    const double sk = chunk_sum_sc1(a.logits, a.n_logits, kk, c, dbuf);
+    if (t == 0) ck.csum[kk] = sk;
+  }
+}
 
 }  // namespace dqz

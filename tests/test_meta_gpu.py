@@ -190,3 +190,78 @@ def test_second_order_meta_update_matches_oracle(device, bound, meta_batch):
   np.testing.assert_allclose(dlogits, ref['dlogits'], atol=2e-5 * scale)
   # and the second-order answer is not the first-order one
   assert np.abs(ref['dlogits'] - first['dlogits']).max() > 0.05 * scale
+
+
+@pytest.mark.parametrize('meta_lr', [2.5e-4, 200.0])
+def test_meta_update_keeps_logit_buffer_state(device, meta_lr):
+  """The meta-update on a logit buffer whose running state is known
+  (meta_adam_chunks_kernel: Adam and the re-sums of the chunks it writes in
+  one launch).  The written logits match the oracle's Adam step, the others
+  are untouched, the running log-sum-exp equals a fresh fp64 scan and every
+  chunk sum equals its canonical restatement bit for bit.  meta_lr = 200
+  moves some logits ~200 above the running shift c: the guard trips and the
+  last active block re-scans the buffer and re-sums every chunk
+  (replay_circular.py:166-217 semantics are those of the plain write)."""
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  a, m, cap_logits = 6, 100, 50_000  # 13 chunks, the last one partial
+  net = networks.dqn_atari_network(a)
+  online = net.init(71)
+  target = helpers.perturbed_tree(online, 72)
+  mu, nu = _rand_opt_state(online, 73)
+  lrn = learner_lib.Learner(net, 32, algo='dqn')
+  lrn.set_params(online, target)
+  lrn.set_opt_state(mu, nu)
+  meta = learner_lib.MetaLearner(lrn, m, learner_lib.adam(meta_lr))
+  rng = np.random.default_rng(74)
+  st, host = _store(256, 640, a, 75, device)
+  slots = rng.choice(256, m, replace=False).astype(np.int32)
+  logits = rng.standard_normal(cap_logits).astype(np.float32)
+  # positions clustered in a few chunks, some chunks untouched
+  pos = np.concatenate([rng.choice(np.arange(4096, 8192), 60, replace=False),
+                        rng.choice(np.arange(40_000, cap_logits), 40, replace=False)]).astype(np.int32)
+  rng.shuffle(pos)
+  dev = rc._DeviceLogits(cap_logits, device, max_queries=32)  # pylint: disable=protected-access
+  dev.load(logits)
+  dev.sample_abs(rng.random(32))  # a draw re-seeds: the running state is known
+  assert dev.run_state()['known'] == 1
+  ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot = replay_lib.Transition(ot_tm1, 1, 1.0, 0.99, ot_t)
+  mb = dict(s_tm1=helpers.stacks_from(host['frames'], host['fidx'], slots, 0),
+            a_tm1=host['action'][slots], r_t=host['reward'][slots],
+            discount_t=host['discount'][slots],
+            s_t=helpers.stacks_from(host['frames'], host['fidx'], slots, 1))
+  ref = learner_ref.meta_update(
+      _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
+      dict(s_tm1=ot_tm1, a_tm1=1, r_t=1.0, discount_t=0.99, s_t=ot_t),
+      np.zeros(m), np.zeros(m), 0, meta_lr=meta_lr)
+  meta.set_online_transition(ot)
+  pos_d = torch.from_numpy(pos).to(device)
+  meta.update(st, torch.from_numpy(slots).to(device), dev.logits, pos_d,
+              logit_buffer=dev)
+  probs, dlogits, _, loss = [t.cpu().numpy() for t in meta.fetch_outputs()]
+  np.testing.assert_allclose(probs, ref['probs'], rtol=1e-5)
+  np.testing.assert_allclose(loss[0], ref['loss'], rtol=2e-5)
+  scale = np.abs(ref['dlogits']).max()
+  np.testing.assert_allclose(dlogits, ref['dlogits'], atol=2e-5 * scale)
+  after = dev.logits.cpu().numpy()
+  np.testing.assert_allclose(after[pos], ref['new_logits'], atol=1e-6 * max(1.0, meta_lr))
+  keep = np.ones(cap_logits, bool)
+  keep[pos] = False
+  np.testing.assert_array_equal(after[keep], logits[keep])
+  run = dev.run_state()
+  assert run['valid'] == 1 and run['known'] == 1
+  a64 = after.astype(np.float64)
+  want_lse = a64.max() + np.log(np.exp(a64 - a64.max()).sum())
+  assert abs(run['c'] + np.log(run['S']) - want_lse) < 1e-9 * max(1.0, abs(want_lse))
+  if meta_lr > 1.0:
+    assert after.max() > logits.max() + 80.0  # the guard's case was hit
+    assert run['c'] == after.max()  # re-seeded about the new maximum
+  t_dev, csum, _ = dev.terms()
+  np.testing.assert_array_equal(csum.cpu().numpy(),
+                                helpers.canonical_chunk_sums(t_dev.cpu().numpy()))
+  # and the buffer samples from the new state (no re-seed needed first)
+  assert dev.sample_abs(rng.random(32)).cpu().numpy().max() < cap_logits

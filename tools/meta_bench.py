@@ -42,6 +42,10 @@ def main():
   lrn.set_params(net.init(seed=3))
   lbuf = rc._DeviceLogits(cap, dev, max_queries=B)  # pylint: disable=protected-access
   lbuf.load(rng.standard_normal(cap).astype(np.float32))
+  # one draw re-seeds the running log-sum-exp, as the agent loop's samples
+  # and adds keep it: the meta-update then maintains it and re-sums the
+  # chunks it writes (the path config 3's agent takes)
+  lbuf.sample_abs(rng.random(B))
   ot = replay_lib.Transition(rng.integers(0, 256, (84, 84, 4), dtype=np.uint8), 2, 1.0, 0.99,
                              rng.integers(0, 256, (84, 84, 4), dtype=np.uint8))
   out = {'capacity': cap, 'num_actions': A, 'steps': args.steps}
