@@ -201,7 +201,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
     const int i = t + 256 * q;
     if (i < NW4) {
       const int pix = i >> 4;
-      float* d = s_win + (pix / 11) * C3X_RS + (pix % 11) * C3X_S + (i & 15) * 4;
+      float* d = s_win + (pix / 11) * C3X_RS + (pix % 11) * C3X_S + win64_ch((i & 15) * 4);
       d[0] = r[q].x;
       d[1] = r[q].y;
       d[2] = r[q].z;
@@ -214,7 +214,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
     const int p = min(48 * mh + 16 * m + n, C2M - 1);
-    base[m] = (p / C2O) * C3X_RS + (p % C2O) * C3X_S + 16 * w + kq;
+    base[m] = (p / C2O) * C3X_RS + (p % C2O) * C3X_S + win64_ch(16 * w) + kq;
   }
   f32x4 acc[3];
 #pragma unroll
@@ -399,7 +399,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     const int i = t + 256 * q;
     if (i < NW4) {
       const int pix = i >> 4;
-      float* d = s_win + (pix / 11) * C2X_RS + (pix % 11) * C2X_S + (i & 15) * 4;
+      float* d = s_win + (pix / 11) * C2X_RS + (pix % 11) * C2X_S + win64_ch((i & 15) * 4);
       d[0] = r[q].x;
       d[1] = r[q].y;
       d[2] = r[q].z;
@@ -414,7 +414,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, 99);  // p = 10 a + c
-    base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + 16 * w + kq;
+    base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + win64_ch(16 * w) + kq;
   }
   f32x4 acc[MT];
 #pragma unroll
@@ -429,7 +429,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + 16 * w + kq + off], wr[kk], last[e]);
+        last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + win64_ch(16 * w) + kq + off], wr[kk], last[e]);
     }
   }
   {

@@ -319,7 +319,7 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
     const int i = t + 256 * q;
     if (i < NQ4) {
       const int pix = i >> 4, ci = (i & 15) * 4;
-      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + ci;
+      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + win64_ch(ci);
       d[0] = r[q].x;
       d[1] = r[q].y;
       d[2] = r[q].z;
@@ -334,13 +334,13 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, C3M - 1);
-    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + 16 * w + kq;
+    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + win64_ch(16 * w) + kq;
   }
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   float last = 0.f;  // position 48 (oh = ow = 6), this lane's k rows
-  const int blast = (C3O - 1) * C3L_RS + (C3O - 1) * C3L_S + 16 * w + kq;
+  const int blast = (C3O - 1) * C3L_RS + (C3O - 1) * C3L_S + win64_ch(16 * w) + kq;
 #pragma unroll
   for (int kk = 0; kk < 36; ++kk) {
     const int tap = kk >> 2;
@@ -425,7 +425,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
     const int i = t + 256 * q;
     if (i < nq4) {
       const int pix = i >> 4, ci = (i & 15) * 4;
-      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + ci;
+      float* d = s_in + (pix / C2O) * C3L_RS + (pix % C2O) * C3L_S + win64_ch(ci);
       d[0] = r[q].x;
       d[1] = r[q].y;
       d[2] = r[q].z;
@@ -439,7 +439,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int p = min(16 * m + n, npos - 1);
-    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + 16 * w + kq;
+    base[m] = (p / C3O) * C3L_RS + (p % C3O) * C3L_S + win64_ch(16 * w) + kq;
   }
   f32x4 acc[MT];
 #pragma unroll

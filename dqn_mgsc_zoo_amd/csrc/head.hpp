@@ -448,6 +448,46 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stri
                      ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
 }
 
+// The same sum with every load issued before the first addition, for S <=
+// 8 R G slabs: R rounds of eight clamped loads, summed in sum_split2's order
+// (a[u] over the rounds, then the fixed tree), so the bits are the same.  The
+// loop form above issues one round of eight loads per dependent step and a
+// ninth round for its tail (conv1's 4 B = 128 slabs took three serial round
+// trips at B = 32; conv2 / conv3's 32 slabs one).
+template <int R>
+__device__ __forceinline__ float2 sum_split2_r(const float* p, int S, int64_t stride, int64_t j, int g) {
+  constexpr int G = UPD_GROUPS;
+  float2 v[R][8];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[r][u] = *reinterpret_cast<const float2*>(p + (int64_t)min(g + (8 * r + u) * G, S - 1) * stride + j);
+  __builtin_amdgcn_sched_barrier(0);
+  float2 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (g + (8 * r + u) * G < S) {
+        a[u].x += v[r][u].x;
+        a[u].y += v[r][u].y;
+      }
+  return make_float2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
+                     ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
+}
+#ifndef DQZ_UPD_BATCH
+#define DQZ_UPD_BATCH 1
+#endif
+__device__ __forceinline__ float2 sum_slabs(const float* p, int S, int64_t stride, int64_t j, int g) {
+  if (!DQZ_UPD_BATCH) return sum_split2(p, S, stride, j, g);
+  if (S <= 8 * UPD_GROUPS) return sum_split2_r<1>(p, S, stride, j, g);
+  if (S <= 16 * UPD_GROUPS) return sum_split2_r<2>(p, S, stride, j, g);
+  return sum_split2(p, S, stride, j, g);
+}
+
 // One gradient element of the small head leaves (fc1/b, fc2/w, fc2/b): this
 // thread's share (samples grp, grp + G, ...) and its destination offset.
 // Eight samples' operands are loaded per round (unconditional, clamped to the
@@ -580,11 +620,11 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     g.x = small_grad(u, e, grp, unused);
     g.y = small_grad(u, e + 1, grp, unused);
   } else if (e < c1) {
-    g = sum_split2(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
+    g = sum_slabs(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
   } else if (e < c2) {
-    g = sum_split2(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
+    g = sum_slabs(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
   } else if (e < c3) {
-    g = sum_split2(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
+    g = sum_slabs(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
   }
   s_part[grp][pl] = g;
   if (blk == 0 && threadIdx.x < 64) {
