@@ -755,6 +755,86 @@ __device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, i
   DQZ_STAMP(5, 3);
 }
 
+// ---- B = 1: the head and fc1 dX in one launch (head_dx1_kernel) ----------
+// With one sample (the MGSC meta-update's pass at theta') dz1 is 2 KB, so the
+// fc1 dX blocks can wait for it inside the head's launch: block 0 runs the
+// head (dz1 stored write-through, one arrival), blocks 1.. each own 32 W1
+// rows (two 256-thread halves of 16 rows), load them before the wait, then
+// read dz1 with sc1 loads and form dy3 = relu'(y3) (W1 dz1) as VALU dot
+// products (a one-row GEMV: 16 lanes per row, 32 columns per lane, in
+// column order, then a 16-lane sum).  They also write the dX-ordered W3 / W2
+// copies, as fc1_dx_kernel does.  Saves the head -> fc1 dX boundary and the
+// fc1 dX load phase (they overlap the head).
+constexpr int FC1X1_ROWS = 32;
+constexpr int FC1X1_BLOCKS = FLAT / FC1X1_ROWS;  // 98
+__device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, int row0, int t, const Handoff& hw) {
+  const int r = row0 + (t >> 4), c0 = 32 * (t & 15);
+  const float* W1 = a.th + a.w_off;
+  float4 wv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)r * HID + c0 + 4 * j);
+  const float ym = a.y3[r];  // relu'(y3) of the one sample
+  // W3 / W2 dX copies: element g of the 69,632 by thread g of the fc1 dX range
+  const int g = (row0 / 16) * 256 + t;
+  float v3 = 0.f, v2 = 0.f;
+  if (a.w3p) {
+    if (g < W3P_N) v3 = a.w3[w3p_src(g)];
+    if (g < W2P_N) v2 = a.w2[w2p_src(g)];
+  }
+  hw.wait(0);
+  if (threadIdx.x < HID / 4)
+    reinterpret_cast<float4*>(s_dz)[threadIdx.x] = load_sc1_f4(reinterpret_cast<const float4*>(a.dz1), HID * 4, threadIdx.x);
+  __syncthreads();
+  float d = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float4 z = *reinterpret_cast<const float4*>(s_dz + c0 + 4 * j);
+    d = __fmaf_rn(wv[j].x, z.x, d);
+    d = __fmaf_rn(wv[j].y, z.y, d);
+    d = __fmaf_rn(wv[j].z, z.z, d);
+    d = __fmaf_rn(wv[j].w, z.w, d);
+  }
+  // sum over the row's 16 lanes (one DPP row): quad xor 1, xor 2, half-row and row mirrors
+  d += dpp_f<0xB1>(d);
+  d += dpp_f<0x4E>(d);
+  d += dpp_f<0x141>(d);
+  d += dpp_f<0x140>(d);
+  if ((t & 15) == 0) a.dy3[r] = ym > 0.f ? d : 0.f;
+  if (a.w3p) {
+    if (g < W3P_N) a.w3p[g] = v3;
+    if (g < W2P_N) a.w2p[g] = v2;
+  }
+}
+
+template <int AMAX, int SMAX, int ZMAX>
+__global__ __launch_bounds__(512) void head_dx1_kernel(HeadArgs h, Fc1BwdArgs f) {
+  __shared__ __attribute__((aligned(16))) float s_dz[HID];
+  if (blockIdx.x == 0) {
+    head_body<AMAX, SMAX, ZMAX>(h, 0);
+    return;
+  }
+  const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
+  fc1_dx1_rows(f, s_dz, FC1X1_ROWS * (blockIdx.x - 1) + 16 * half, t, h.dz1_pub);
+}
+
+// head_dx1_kernel's launch: the head_kernel template choice (launch_head)
+inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStream_t st) {
+  if (h.S > 7 || h.Z < 1 || h.Z > 3 || h.B != 1) return hipErrorInvalidValue;
+  const dim3 grid(1 + FC1X1_BLOCKS), block(512);
+  if (h.A <= 8) {
+    if (h.Z <= 2)
+      hipLaunchKernelGGL((head_dx1_kernel<8, 7, 2>), grid, block, 0, st, h, f);
+    else
+      hipLaunchKernelGGL((head_dx1_kernel<8, 7, 3>), grid, block, 0, st, h, f);
+  } else {
+    if (h.Z <= 2)
+      hipLaunchKernelGGL((head_dx1_kernel<MAXA, 7, 2>), grid, block, 0, st, h, f);
+    else
+      hipLaunchKernelGGL((head_dx1_kernel<MAXA, 7, 3>), grid, block, 0, st, h, f);
+  }
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
   fc1_dx_block(a, smem, blockIdx.x);

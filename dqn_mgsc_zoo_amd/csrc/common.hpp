@@ -335,6 +335,14 @@ __device__ __forceinline__ void store_sc1_f4(float* base, int bytes, int off, f3
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
 }
 
+// 4-byte write-through (sc1) store of element e (small hand-offs and the
+// fused meta Adam's rare re-seed path: 4-byte sc1 stores cost ~6x the
+// 16-byte ones per byte).
+__device__ __forceinline__ void store_sc1_f1(float* base, int bytes, int e, float v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, e * 4, 0, 16);
+}
+
 // Uniform replay draw of the device sampler (replay.py:119-125 distribution):
 // draw i of step `ctr` -> live slot (base + floor(u * size)) mod capacity,
 // u from Philox(counter = (ctr, i), key = seed).

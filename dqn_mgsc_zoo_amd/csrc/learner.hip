@@ -64,6 +64,13 @@ struct dqz_learner {
   void* block;
 };
 
+// B = 1 learner steps run the head and fc1 dX as one launch (head_dx1_kernel);
+// -DDQZ_HEAD_DX1=0 keeps the two launches (A/B).
+#ifndef DQZ_HEAD_DX1
+#define DQZ_HEAD_DX1 1
+#endif
+constexpr bool kHeadDx1 = DQZ_HEAD_DX1 != 0;
+
 static int g_attr_done = 0;
 
 static int init_kernel_attrs() {
@@ -375,9 +382,18 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w2 = P->online + L->off[2];
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
-  DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
-  DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
-            DQZ_HIP(hipGetLastError()));
+  if (B == 1 && !pe.on() && kHeadDx1) {
+    // one sample (the MGSC pass at theta', the HVP's unit-cotangent pass):
+    // the head and fc1 dX in one launch, dz1 handed over in-launch
+    h.dz1_wt = 1;
+    h.dz1_pub = Handoff{L->sync + (16 * B + 1) * Handoff::kStride, L->sync + (16 * B + 2) * Handoff::kStride,
+                        L->sync + 16 * B * Handoff::kStride, 1, FC1X1_BLOCKS, L->spin_max};
+    DQZ_HIP(launch_head_dx1(h, fb, st));
+  } else {
+    DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
+    DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
+              DQZ_HIP(hipGetLastError()));
+  }
 
   Conv3BwdArgs c3b{};
   c3b.dy3 = L->dy3;
@@ -450,7 +466,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.rms = rms;
   u.rms.sq_off = 4 * (FLAT / 16);  // meta_rms2 partials: the fc1 dW blocks' first, then the update's
   const unsigned nblk = update_blocks(L->sz, A, u.nb2);
-  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
+  DQZ_PHASE(9, if (update_rmax(u.S1) <= 2) hipLaunchKernelGGL(update_kernel<2>, dim3(nblk), dim3(256), 0, st, u);
+            else hipLaunchKernelGGL(update_kernel<7>, dim3(nblk), dim3(256), 0, st, u);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }

@@ -516,12 +516,6 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
 // writes.  A tripped guard (rare) is handled by the last of the active
 // blocks to arrive, after every block's logit stores drained write-through:
 // re-scan of the buffer and every chunk sum, with L2-bypassing loads.
-// 4-byte write-through (sc1) store of element e (the fused Adam's rare
-// re-seed path only: 4-byte sc1 stores cost ~6x the 16-byte ones per byte).
-__device__ __forceinline__ void store_sc1_f1(float* base, int bytes, int e, float v) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, e * 4, 0, 16);
-}
 
 struct MetaAdamChunks {
   double* csum;  // [nblocks]
