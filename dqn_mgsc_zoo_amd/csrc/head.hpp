@@ -489,21 +489,15 @@ __device__ __forceinline__ float2 sum_split2_r(const float* p, int S, int64_t st
 #ifndef DQZ_UPD_BATCH
 #define DQZ_UPD_BATCH 1
 #endif
-// RMAX: the widest batch the kernel instance compiles (its registers scale
-// with it): 2 for the learner's B <= 32 (conv1's 4 B slabs <= 128), 7 for the
-// M = 100 meta batch (conv1's 400 slabs).
-template <int RMAX>
+// (Wider forms, up to 56 loads per lane for the M = 100 meta batch's 400
+// conv1 slabs, cost that kernel 0.5 us: 162 VGPRs left its 1,276 blocks no
+// longer all resident; profiles/r05/c7.)
 __device__ __forceinline__ float2 sum_slabs(const float* p, int S, int64_t stride, int64_t j, int g) {
   if (!DQZ_UPD_BATCH) return sum_split2(p, S, stride, j, g);
   if (S <= 8 * UPD_GROUPS) return sum_split2_r<1>(p, S, stride, j, g);
   if (S <= 16 * UPD_GROUPS) return sum_split2_r<2>(p, S, stride, j, g);
-  if constexpr (RMAX >= 7) {
-    if (S <= 32 * UPD_GROUPS) return sum_split2_r<4>(p, S, stride, j, g);
-    if (S <= 56 * UPD_GROUPS) return sum_split2_r<7>(p, S, stride, j, g);
-  }
   return sum_split2(p, S, stride, j, g);
 }
-inline int update_rmax(int S1) { return S1 <= 16 * UPD_GROUPS ? 2 : 7; }
 
 // One gradient element of the small head leaves (fc1/b, fc2/w, fc2/b): this
 // thread's share (samples grp, grp + G, ...) and its destination offset.
@@ -574,7 +568,6 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 // LDS.  Grid: the small head leaves first (their blocks run the longest
 // per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
 // RMSProp operands are loaded at entry, under the reduction's latency.
-template <int RMAX>
 __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[UPD_PAIRS], int blk) {
   DQZ_STAMP(9, 0);
   const int pl = threadIdx.x % UPD_PAIRS, grp = threadIdx.x / UPD_PAIRS;
@@ -638,11 +631,11 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     g.x = small_grad(u, e, grp, unused);
     g.y = small_grad(u, e + 1, grp, unused);
   } else if (e < c1) {
-    g = sum_slabs<RMAX>(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
+    g = sum_slabs(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
   } else if (e < c2) {
-    g = sum_slabs<RMAX>(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
+    g = sum_slabs(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
   } else if (e < c3) {
-    g = sum_slabs<RMAX>(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
+    g = sum_slabs(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
   }
   s_part[grp][pl] = g;
   if (blk == 0 && threadIdx.x < 64) {
@@ -716,10 +709,9 @@ inline unsigned update_blocks(const int64_t sz[10], int A, int nb2) {
   return (unsigned)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS + (nconv + UPD_PARAMS - 1) / UPD_PARAMS);
 }
 
-template <int RMAX>
 __global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
   __shared__ float2 s_part[UPD_GROUPS][UPD_PAIRS];
-  update_body<RMAX>(u, s_part, blockIdx.x);
+  update_body(u, s_part, blockIdx.x);
 }
 
 __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,

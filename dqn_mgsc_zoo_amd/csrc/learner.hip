@@ -466,8 +466,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.rms = rms;
   u.rms.sq_off = 4 * (FLAT / 16);  // meta_rms2 partials: the fc1 dW blocks' first, then the update's
   const unsigned nblk = update_blocks(L->sz, A, u.nb2);
-  DQZ_PHASE(9, if (update_rmax(u.S1) <= 2) hipLaunchKernelGGL(update_kernel<2>, dim3(nblk), dim3(256), 0, st, u);
-            else hipLaunchKernelGGL(update_kernel<7>, dim3(nblk), dim3(256), 0, st, u);
+  DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
