@@ -557,19 +557,26 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 #ifndef DQZ_FC1_LOADS_W_FIRST
 #define DQZ_FC1_LOADS_W_FIRST 1
 #endif
+// Waves per fc1 block (8: each wave owns 56 of the split's 448 k).
+#ifndef DQZ_FC1_WAVES
+#define DQZ_FC1_WAVES 4
+#endif
+constexpr int FC1_NW = DQZ_FC1_WAVES;
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
-template <bool DOT>
+template <bool DOT, int NW = 4>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
+  static_assert(NW == 4 || (NW == 8 && !DOT), "fc1 block shape");
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
   const int z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 31, h = lane >> 5;
-  const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
+  constexpr int KW = FC1_KS / NW;
+  const int k0 = s * FC1_KS + w * KW + 4 * h;
   const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
-  constexpr int G = FC1_KW / 8;                         // 14
+  constexpr int G = KW / 8;                             // 14 (NW 4)
   const int row = min(32 * mg + c, a.B - 1);
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
@@ -600,6 +607,20 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 #pragma unroll
   for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
   __syncthreads();
+  if (NW == 8) {  // 512 threads x 2 outputs: row q = t / 16, columns 2 (t % 16) .. + 1
+    const int q = t >> 4, c2 = 2 * (t & 15);
+    if (32 * mg + q >= a.B) return;
+    float v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int k = q * 33 + c2 + e;
+      v[e] = ((s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k])) +
+             ((s_red[4 * FC1_32RW + k] + s_red[5 * FC1_32RW + k]) + (s_red[6 * FC1_32RW + k] + s_red[7 * FC1_32RW + k]));
+    }
+    *reinterpret_cast<float2*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c2) =
+        make_float2(v[0], v[1]);
+    return;
+  }
   // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
   const int q = t >> 3, c4 = 4 * (t & 7);
   const bool live = 32 * mg + q < a.B;
@@ -629,10 +650,10 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 
 inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
-__global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
+__global__ __launch_bounds__(64 * FC1_NW) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
-  __shared__ float s_red[4 * FC1_32RW];
-  fc1_fwd_block32<false>(a, s_red, blockIdx.x);
+  __shared__ float s_red[FC1_NW * FC1_32RW];
+  fc1_fwd_block32<false, FC1_NW>(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 

@@ -253,7 +253,7 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   f1.B = B;
   f1.MG = (B + 31) / 32;
   f1.part = L->fc1p;
-  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(256), 0, st, f1);
+  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(64 * FC1_NW), 0, st, f1);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
