@@ -398,6 +398,9 @@ constexpr int C3F_ROWS0 = 4;
 // MFMA row tiles and every conv2 block resident from the start).
 constexpr int kFwd8MaxSamples = 16;
 inline int fwd_conv_jobs(int zb) { return zb <= kFwd8MaxSamples ? 8 : 4; }
+// PUB (fwd_fc1_kernel): y3 goes out as 16-byte write-through stores and the
+// fc1 blocks of the same launch wait for the 8 arrivals of each sample.
+template <bool PUB = false>
 __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
@@ -462,6 +465,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
     for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + oh0 * C3O * C3CO + 16 * nq;
+  const int out_bytes = (FLAT - oh0 * C3O * C3CO - 16 * nq) * 4;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < epi_range(npos); i += 256) {
     const int p = epi_row(i), c4 = 4 * (i & 3);
@@ -474,8 +478,12 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
       const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bb;
       o[e] = linear ? v : relu(v);
     }
-    *reinterpret_cast<float4*>(out + p * C3CO + c4) = make_float4(o[0], o[1], o[2], o[3]);
+    if (PUB)
+      store_sc1_f4(out, out_bytes, 4 * (p * C3CO + c4), f32x4{o[0], o[1], o[2], o[3]});
+    else
+      *reinterpret_cast<float4*>(out + p * C3CO + c4) = make_float4(o[0], o[1], o[2], o[3]);
   }
+  if (PUB) a.pub.arrive(sj.s);
   DQZ_STAMP(2, 3);
 }
 
@@ -547,6 +555,7 @@ struct Fc1FwdArgs {
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
+  Handoff wait = {};  // fwd_fc1_kernel: y3 of each sample produced by the same launch's conv3 blocks
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
@@ -564,9 +573,12 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 constexpr int FC1_NW = DQZ_FC1_WAVES;
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
-template <bool DOT, int NW = 4>
+// WAIT (fwd_fc1_kernel, one row group): the W1 loads are issued, then the
+// block waits for y3 of every sample of its copy and reads it with sc1 loads.
+template <bool DOT, int NW = 4, bool WAIT = false>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
   static_assert(NW == 4 || (NW == 8 && !DOT), "fc1 block shape");
+  static_assert(!(WAIT && DOT), "fc1 block form");
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
@@ -581,6 +593,16 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
   float4 av[G];
+  if (WAIT) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
+    for (int q = 0; q < a.B; ++q) a.wait.wait(z * a.B + q);
+    const float4* xz = reinterpret_cast<const float4*>(a.in + (int64_t)z * a.B * FLAT);
+#pragma unroll
+    for (int g = 0; g < G; ++g) av[g] = load_sc1_f4(xz, a.B * FLAT * 4, (row * FLAT + k0 + 8 * g) >> 2);
+  } else {
 #if DQZ_FC1_LOADS_W_FIRST
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -596,6 +618,7 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   }
 #endif
+  }
   f32x16 acc = {};
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -656,5 +679,42 @@ __global__ __launch_bounds__(64 * FC1_NW) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   fc1_fwd_block32<false, FC1_NW>(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
+
+// ---- conv1 -> conv2 -> conv3 -> fc1 forward in one launch -----------------
+// For launches of at most kFwd8MaxSamples samples and one fc1 row group (the
+// MGSC pass at theta', the HVP's unit-cotangent pass, the actor): the grid of
+// fwd_conv_kernel (8-job conv2 / conv3) followed by the fc1 blocks, which
+// issue their W1 loads at dispatch (the whole 6.4 MB per copy streams while
+// the conv chain runs) and wait for the 8 conv3 arrivals of each sample of
+// their copy.  Every block of such a launch is resident from the start (384
+// at Z = 2, two 57.6 KB blocks per CU), the conv3 producers precede their fc1
+// consumers in dispatch order, and the fc1 launch boundary and its load phase
+// leave the chain.
+template <int F>
+__global__ __launch_bounds__(256) void fwd_fc1_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
+                                                      Fc1FwdArgs f1) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int zb = c1.Z * c1.B, n = 4 * ((zb + 7) / 8 * 8);
+  int i = blockIdx.x;
+  if (i < n) {
+    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, zb);
+    if (sj.valid) conv1_fwd_body<true, F>(c1, smem, sj);
+    return;
+  }
+  i -= n;
+  if (i < 2 * n) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, zb);
+    if (sj.valid) conv2_fwd8_body(c2, smem, sj);
+    return;
+  }
+  i -= 2 * n;
+  if (i < 2 * n) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, zb);
+    if (sj.valid) conv3_fwd8_body<true>(c3, smem, sj);
+    return;
+  }
+  fc1_fwd_block32<false, 4, true>(f1, smem, i - 2 * n);
+}
+static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's tiles fit fwd_fc1_kernel's LDS");
 
 }  // namespace dqz
