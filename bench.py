@@ -322,12 +322,13 @@ def _run_ranks(n, argv, store_file, script, store_env):
     env.pop('MASTER_PORT', None)
     procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
   rcs = [None] * n
+  own = []  # exit codes of ranks that failed by themselves (not terminated here)
   while any(rc is None for rc in rcs):
     for i, p in enumerate(procs):
       if rcs[i] is None:
         rcs[i] = p.poll()
-    bad = [rc for rc in rcs if rc not in (None, 0)]
-    if bad:  # one rank failed: the others would wait forever at a collective
+    own = [rc for rc in rcs if rc not in (None, 0)]
+    if own:  # one rank failed: the others would wait forever at a collective
       for i, p in enumerate(procs):
         if rcs[i] is None:
           p.terminate()
@@ -340,12 +341,12 @@ def _run_ranks(n, argv, store_file, script, store_env):
             rcs[i] = p.wait()
       break
     time.sleep(0.05)
-  worst = 0
-  for rc in rcs:
+  # the code of the first rank that failed by itself (a rank this parent
+  # terminated after it reports -SIGTERM, which says nothing of the cause)
+  for rc in own + rcs:
     if rc != 0:
-      worst = rc if rc > 0 else 1
-      break
-  return worst
+      return rc if rc > 0 else 1
+  return 0
 
 
 def parse_args(argv=None):
