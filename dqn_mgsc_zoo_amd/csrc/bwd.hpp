@@ -801,6 +801,7 @@ __device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, i
 constexpr int FC1X1_ROWS = 32;
 constexpr int FC1X1_BLOCKS = FLAT / FC1X1_ROWS;  // 98
 __device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, int row0, int t, const Handoff& hw) {
+  DQZ_STAMP(5, 0);
   const int r = row0 + (t >> 4), c0 = 32 * (t & 15);
   const float* W1 = a.th + a.w_off;
   float4 wv[8];
@@ -815,6 +816,7 @@ __device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, i
     if (g < W2P_N) v2 = a.w2[w2p_src(g)];
   }
   hw.wait(0);
+  DQZ_STAMP(5, 1);
   if (threadIdx.x < HID / 4)
     reinterpret_cast<float4*>(s_dz)[threadIdx.x] = load_sc1_f4(reinterpret_cast<const float4*>(a.dz1), HID * 4, threadIdx.x);
   __syncthreads();
@@ -837,6 +839,7 @@ __device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, i
     if (g < W3P_N) a.w3p[g] = v3;
     if (g < W2P_N) a.w2p[g] = v2;
   }
+  DQZ_STAMP(5, 3);
 }
 
 template <int AMAX, int SMAX, int ZMAX>

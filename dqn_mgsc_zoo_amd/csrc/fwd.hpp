@@ -599,6 +599,7 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 #pragma unroll
       for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
     for (int q = 0; q < a.B; ++q) a.wait.wait(z * a.B + q);
+    DQZ_STAMP(3, 1);
     const float4* xz = reinterpret_cast<const float4*>(a.in + (int64_t)z * a.B * FLAT);
 #pragma unroll
     for (int g = 0; g < G; ++g) av[g] = load_sc1_f4(xz, a.B * FLAT * 4, (row * FLAT + k0 + 8 * g) >> 2);
@@ -713,7 +714,9 @@ __global__ __launch_bounds__(256) void fwd_fc1_kernel(Conv1FwdArgs c1, LayerFwdA
     if (sj.valid) conv3_fwd8_body<true>(c3, smem, sj);
     return;
   }
+  DQZ_STAMP(3, 0);
   fc1_fwd_block32<false, 4, true>(f1, smem, i - 2 * n);
+  DQZ_STAMP(3, 3);
 }
 static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's tiles fit fwd_fc1_kernel's LDS");
 

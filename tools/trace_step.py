@@ -32,12 +32,13 @@ K, NB, NS = 16, 4096, 4
 dev = torch.device('cuda:0')
 cap = int(os.environ.get('CAP', '200000'))
 ALGO = os.environ.get('ALGO', 'dqn')  # dqn | double | per | mgsc: bench.py's workloads
+BATCH = int(os.environ.get('BATCH', '32'))  # dqn: BATCH=1 is the MGSC theta' pass's shape
 if ALGO == 'dqn':
   net = networks.dqn_atari_network(6)
-  lrn = learner_lib.Learner(net, 32, algo='dqn', device=dev)
+  lrn = learner_lib.Learner(net, BATCH, algo='dqn', device=dev)
   lrn.set_params(net.init(0))
   store = synthetic.fill_episodic(cap, 6, seed=0, device=dev)
-  slots = torch.zeros((32,), dtype=torch.int32, device=dev)
+  slots = torch.zeros((BATCH,), dtype=torch.int32, device=dev)
   counter = torch.zeros((1,), dtype=torch.int64, device=dev)
 
   def step():
