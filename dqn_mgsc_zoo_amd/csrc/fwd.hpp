@@ -674,6 +674,73 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 
 inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 
+// fc1 forward of at most FC1_GEMV_MAXB rows (the MGSC pass at theta', the HVP
+// pass, the actor's single state) as VALU dot products: the 32 x 32 MFMA tile
+// would spend 56 v_mfma_f32_32x32x2f32 per wave (1.5 us) on one live row.
+// Same blocks and partial layout as fc1_fwd_block32; thread t owns column
+// t % 32 of the block's 32 and k [56 (t / 32), +56) of its split; the split's
+// y3 rows are staged in LDS, and the 8 k-group sums of each output are added
+// in k-group order.  WAIT: fwd_fc1_kernel's form (y3 handed over in-launch).
+constexpr int FC1_GEMV_MAXB = 4, FC1_GEMV_KG = FC1_KS / 8;  // 56
+constexpr int FC1_GEMV_SMEM = FC1_GEMV_MAXB * FC1_KS + 8 * FC1_GEMV_MAXB * 32;  // floats
+#ifndef DQZ_FC1_GEMV
+#define DQZ_FC1_GEMV 1
+#endif
+constexpr bool kFc1Gemv = DQZ_FC1_GEMV != 0;
+template <bool WAIT>
+__device__ __forceinline__ void fc1_gemv_block(const Fc1FwdArgs& a, float* smem, int i) {
+  const int nt = i % (HID / 32);
+  const int rest = i / (HID / 32);
+  const int s = rest % FC1_S, z = rest / FC1_S;
+  const int t = threadIdx.x, c = t & 31, kg = t >> 5;
+  const int B = a.B;
+  const int k0 = s * FC1_KS + kg * FC1_GEMV_KG;
+  const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
+  float wr[FC1_GEMV_KG];
+#pragma unroll
+  for (int j = 0; j < FC1_GEMV_KG; ++j) wr[j] = W[(int64_t)(k0 + j) * HID];
+  if (WAIT)
+    for (int q = 0; q < B; ++q) a.wait.wait(z * B + q);
+  float* s_x = smem;                                // [B][448]: y3 rows of the split
+  float* s_red = smem + FC1_GEMV_MAXB * FC1_KS;     // [8 k groups][4 rows][32 columns]
+  const float4* xz = reinterpret_cast<const float4*>(a.in + (int64_t)z * B * FLAT);
+  for (int e = t; e < B * (FC1_KS / 4); e += blockDim.x) {
+    const int row = e / (FC1_KS / 4), q4 = e % (FC1_KS / 4);
+    const int src = (row * FLAT + s * FC1_KS) / 4 + q4;
+    const float4 v = WAIT ? load_sc1_f4(xz, B * FLAT * 4, src) : xz[src];
+    *reinterpret_cast<float4*>(s_x + row * FC1_KS + 4 * q4) = v;
+  }
+  __syncthreads();
+  float acc[FC1_GEMV_MAXB];
+#pragma unroll
+  for (int r = 0; r < FC1_GEMV_MAXB; ++r) {
+    acc[r] = 0.f;
+    if (r < B) {
+      const float* x = s_x + r * FC1_KS + kg * FC1_GEMV_KG;
+#pragma unroll
+      for (int j = 0; j < FC1_GEMV_KG; ++j) acc[r] = __fmaf_rn(wr[j], x[j], acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < FC1_GEMV_MAXB; ++r)
+    if (r < B) s_red[(kg * FC1_GEMV_MAXB + r) * 32 + c] = acc[r];
+  __syncthreads();
+  if (t < 32 * B) {
+    const int r = t >> 5;
+    float v = s_red[r * 32 + c];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) v += s_red[(g * FC1_GEMV_MAXB + r) * 32 + c];
+    a.part[(((int64_t)z * FC1_S + s) * B + r) * HID + 32 * nt + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void fc1_gemv_kernel(Fc1FwdArgs a) {
+  DQZ_STAMP(3, 0);
+  __shared__ __attribute__((aligned(16))) float smem[FC1_GEMV_SMEM];
+  fc1_gemv_block<false>(a, smem, blockIdx.x);
+  DQZ_STAMP(3, 3);
+}
+
 __global__ __launch_bounds__(64 * FC1_NW) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[FC1_NW * FC1_32RW];
@@ -715,9 +782,13 @@ __global__ __launch_bounds__(256) void fwd_fc1_kernel(Conv1FwdArgs c1, LayerFwdA
     return;
   }
   DQZ_STAMP(3, 0);
-  fc1_fwd_block32<false, 4, true>(f1, smem, i - 2 * n);
+  if (kFc1Gemv && f1.B <= FC1_GEMV_MAXB)
+    fc1_gemv_block<true>(f1, smem, i - 2 * n);
+  else
+    fc1_fwd_block32<false, 4, true>(f1, smem, i - 2 * n);
   DQZ_STAMP(3, 3);
 }
-static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem, "fc1's tiles fit fwd_fc1_kernel's LDS");
+static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem && FC1_GEMV_SMEM * sizeof(float) <= kConv1FwdSmem,
+              "fc1's tiles fit fwd_fc1_kernel's LDS");
 
 }  // namespace dqz

@@ -278,7 +278,10 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   } DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
 
-  DQZ_PHASE(3, hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(64 * FC1_NW), 0, st, f1);
+  DQZ_PHASE(3, if (kFc1Gemv && B <= FC1_GEMV_MAXB)
+                 hipLaunchKernelGGL(fc1_gemv_kernel, dim3(fc1_fwd_blocks(Z, 1)), dim3(256), 0, st, f1);
+               else
+                 hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(64 * FC1_NW), 0, st, f1);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
