@@ -69,15 +69,6 @@ constexpr int FC1X_SMEM = 32 * FC1X_LD + 4 * 2 * FC1X_RED;  // floats: dz1 chunk
 
 // Samples [c_beg, c_end) of the batch, in chunks of 32 (fc1_dx_block gives a
 // block one chunk).
-// DQZ_FC1DX_DIRECT: the dz1 A fragments loaded straight into registers (each
-// wave reads only its K quarter of the chunk's rows) instead of staged through
-// a 66.5 KB LDS chunk: 10 KB of LDS per block, so every block of the M = 100
-// meta batch's 784 is resident at once.
-#ifndef DQZ_FC1DX_DIRECT
-#define DQZ_FC1DX_DIRECT 0
-#endif
-constexpr bool kFc1dxDirect = DQZ_FC1DX_DIRECT != 0;
-constexpr int FC1X_SMEM_K = kFc1dxDirect ? 4 * 2 * FC1X_RED : FC1X_SMEM;
 __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, int blk, int c_beg, int c_end) {
   DQZ_STAMP(5, 0);
   constexpr int LD = FC1X_LD;
@@ -86,7 +77,7 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
   // 4 rows: the writes of lanes kq = 0 / 1 (and 2 / 3), one ds_write_b32
   // lane group, land 16 banks apart instead of on the same banks; the
   // reduction's reads stay conflict-free (a wave reads rows 4w .. 4w + 3).
-  float(*s_red)[2][FC1X_RED] = reinterpret_cast<float(*)[2][FC1X_RED]>(smem + (kFc1dxDirect ? 0 : 32 * LD));
+  float(*s_red)[2][FC1X_RED] = reinterpret_cast<float(*)[2][FC1X_RED]>(smem + 32 * LD);
   auto red_at = [](int row, int col) { return row * 16 + 16 * (row >> 2) + col; };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -98,31 +89,6 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
     wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
   for (int c = c_beg; c < c_end; c += 32) {
     if (c > c_beg) __syncthreads();  // previous chunk's s_dz / s_red readers are done
-    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    float ym[2];  // relu'(y3) operands of the epilogue
-    if (kFc1dxDirect) {
-      // rows past B clamp to B - 1: an A row only feeds its own output row,
-      // and those rows are not stored
-      float4 av[2][8];
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const float* d = a.dz1 + (int64_t)min(c + 16 * mt + n, a.B - 1) * HID + 128 * w + 4 * kq;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) av[mt][j] = *reinterpret_cast<const float4*>(d + 16 * j);
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xacc[mt] = mfma4(av[mt][j].x, wv[j].x, xacc[mt]);
-          xacc[mt] = mfma4(av[mt][j].y, wv[j].y, xacc[mt]);
-          xacc[mt] = mfma4(av[mt][j].z, wv[j].z, xacc[mt]);
-          xacc[mt] = mfma4(av[mt][j].w, wv[j].w, xacc[mt]);
-        }
-    } else {
     // stage dz1 rows [c, c + 32) (rows past B are zero)
     float4 v[16];
 #pragma unroll
@@ -131,6 +97,7 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
       const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + 4 * (f & 127));
       v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    float ym[2];  // relu'(y3) operands of the epilogue
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
@@ -141,6 +108,7 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
     }
     __syncthreads();
     // rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
+    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const float* d = s_dz + (16 * mt + n) * LD + 128 * w + 4 * kq;
@@ -152,7 +120,6 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
         xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
         xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
       }
-    }
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -872,7 +839,7 @@ inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStr
 }
 
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM_K];
+  __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
   fc1_dx_block(a, smem, blockIdx.x);
 }
 

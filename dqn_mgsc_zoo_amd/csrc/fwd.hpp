@@ -398,9 +398,6 @@ constexpr int C3F_ROWS0 = 4;
 // MFMA row tiles and every conv2 block resident from the start).
 constexpr int kFwd8MaxSamples = 16;
 inline int fwd_conv_jobs(int zb) { return zb <= kFwd8MaxSamples ? 8 : 4; }
-// PUB (fwd_fc1_kernel): y3 goes out as 16-byte write-through stores and the
-// fc1 blocks of the same launch wait for the 8 arrivals of each sample.
-template <bool PUB = false>
 __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
@@ -465,7 +462,6 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
     for (int rr = 0; rr < 4; ++rr) s_red[w * RW + red_idx(16 * m + 4 * kq + rr, n)] = acc[m][rr];
   __syncthreads();
   float* out = a.out + ((int64_t)z * a.B + b) * FLAT + oh0 * C3O * C3CO + 16 * nq;
-  const int out_bytes = (FLAT - oh0 * C3O * C3CO - 16 * nq) * 4;
   const bool linear = a.linear;  // read once (see conv1_fwd_body)
   for (int i = t; i < epi_range(npos); i += 256) {
     const int p = epi_row(i), c4 = 4 * (i & 3);
@@ -478,12 +474,8 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
       const float v = ((s_red[k] + s_red[RW + k]) + (s_red[2 * RW + k] + s_red[3 * RW + k])) + bb;
       o[e] = linear ? v : relu(v);
     }
-    if (PUB)
-      store_sc1_f4(out, out_bytes, 4 * (p * C3CO + c4), f32x4{o[0], o[1], o[2], o[3]});
-    else
-      *reinterpret_cast<float4*>(out + p * C3CO + c4) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(out + p * C3CO + c4) = make_float4(o[0], o[1], o[2], o[3]);
   }
-  if (PUB) a.pub.arrive(sj.s);
   DQZ_STAMP(2, 3);
 }
 
@@ -555,7 +547,6 @@ struct Fc1FwdArgs {
   int B, MG;        // MG = ceil(B / 32) row groups
   float* part;      // [Z][FC1_S][B][512]
   TangentDot dot = {nullptr, nullptr, 0};  // MGSC tangent: per-row dot products with dz1 instead of stores
-  Handoff wait = {};  // fwd_fc1_kernel: y3 of each sample produced by the same launch's conv3 blocks
 };
 
 constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
@@ -566,44 +557,25 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 #ifndef DQZ_FC1_LOADS_W_FIRST
 #define DQZ_FC1_LOADS_W_FIRST 1
 #endif
-// Waves per fc1 block (8: each wave owns 56 of the split's 448 k).
-#ifndef DQZ_FC1_WAVES
-#define DQZ_FC1_WAVES 4
-#endif
-constexpr int FC1_NW = DQZ_FC1_WAVES;
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
-// WAIT (fwd_fc1_kernel, one row group): the W1 loads are issued, then the
-// block waits for y3 of every sample of its copy and reads it with sc1 loads.
-template <bool DOT, int NW = 4, bool WAIT = false>
+// (Round 5: 8 waves per block, 56 k each, measured 4.70 -> 4.86 us and
+// 16,239 -> 16,169 steps/s, profiles/r05/s8; not kept.)
+template <bool DOT>
 __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_red, int i) {
-  static_assert(NW == 4 || (NW == 8 && !DOT), "fc1 block shape");
-  static_assert(!(WAIT && DOT), "fc1 block form");
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
   const int s = rest % FC1_S, zm = rest / FC1_S;
   const int z = zm / a.MG, mg = zm % a.MG;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 31, h = lane >> 5;
-  constexpr int KW = FC1_KS / NW;
-  const int k0 = s * FC1_KS + w * KW + 4 * h;
+  const int k0 = s * FC1_KS + w * FC1_KW + 4 * h;
   const float* W = a.nz.p[z] + a.w_off + 32 * nt + c;  // [3136][512]
-  constexpr int G = KW / 8;                             // 14 (NW 4)
+  constexpr int G = FC1_KW / 8;                         // 14
   const int row = min(32 * mg + c, a.B - 1);
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
   float4 av[G];
-  if (WAIT) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
-    for (int q = 0; q < a.B; ++q) a.wait.wait(z * a.B + q);
-    DQZ_STAMP(3, 1);
-    const float4* xz = reinterpret_cast<const float4*>(a.in + (int64_t)z * a.B * FLAT);
-#pragma unroll
-    for (int g = 0; g < G; ++g) av[g] = load_sc1_f4(xz, a.B * FLAT * 4, (row * FLAT + k0 + 8 * g) >> 2);
-  } else {
 #if DQZ_FC1_LOADS_W_FIRST
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -619,7 +591,6 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
   }
 #endif
-  }
   f32x16 acc = {};
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -631,20 +602,6 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
 #pragma unroll
   for (int r = 0; r < 16; ++r) s_red[w * FC1_32RW + ((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = acc[r];
   __syncthreads();
-  if (NW == 8) {  // 512 threads x 2 outputs: row q = t / 16, columns 2 (t % 16) .. + 1
-    const int q = t >> 4, c2 = 2 * (t & 15);
-    if (32 * mg + q >= a.B) return;
-    float v[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int k = q * 33 + c2 + e;
-      v[e] = ((s_red[k] + s_red[FC1_32RW + k]) + (s_red[2 * FC1_32RW + k] + s_red[3 * FC1_32RW + k])) +
-             ((s_red[4 * FC1_32RW + k] + s_red[5 * FC1_32RW + k]) + (s_red[6 * FC1_32RW + k] + s_red[7 * FC1_32RW + k]));
-    }
-    *reinterpret_cast<float2*>(a.part + (((int64_t)z * FC1_S + s) * a.B + 32 * mg + q) * HID + 32 * nt + c2) =
-        make_float2(v[0], v[1]);
-    return;
-  }
   // 256 threads x 4 outputs: row q = t / 8 (0..31), columns 4 (t % 8) .. + 3
   const int q = t >> 3, c4 = 4 * (t & 7);
   const bool live = 32 * mg + q < a.B;
@@ -680,14 +637,10 @@ inline int fc1_fwd_blocks(int Z, int MG) { return (HID / 32) * FC1_S * Z * MG; }
 // Same blocks and partial layout as fc1_fwd_block32; thread t owns column
 // t % 32 of the block's 32 and k [56 (t / 32), +56) of its split; the split's
 // y3 rows are staged in LDS, and the 8 k-group sums of each output are added
-// in k-group order.  WAIT: fwd_fc1_kernel's form (y3 handed over in-launch).
+// in k-group order.  (Round 5: fc1 at B = 1 4.37 -> 2.73 us span; the MGSC
+// first-order meta-update 195-197 -> 193 us, profiles/r05/s9.)
 constexpr int FC1_GEMV_MAXB = 4, FC1_GEMV_KG = FC1_KS / 8;  // 56
 constexpr int FC1_GEMV_SMEM = FC1_GEMV_MAXB * FC1_KS + 8 * FC1_GEMV_MAXB * 32;  // floats
-#ifndef DQZ_FC1_GEMV
-#define DQZ_FC1_GEMV 1
-#endif
-constexpr bool kFc1Gemv = DQZ_FC1_GEMV != 0;
-template <bool WAIT>
 __device__ __forceinline__ void fc1_gemv_block(const Fc1FwdArgs& a, float* smem, int i) {
   const int nt = i % (HID / 32);
   const int rest = i / (HID / 32);
@@ -699,16 +652,13 @@ __device__ __forceinline__ void fc1_gemv_block(const Fc1FwdArgs& a, float* smem,
   float wr[FC1_GEMV_KG];
 #pragma unroll
   for (int j = 0; j < FC1_GEMV_KG; ++j) wr[j] = W[(int64_t)(k0 + j) * HID];
-  if (WAIT)
-    for (int q = 0; q < B; ++q) a.wait.wait(z * B + q);
   float* s_x = smem;                                // [B][448]: y3 rows of the split
   float* s_red = smem + FC1_GEMV_MAXB * FC1_KS;     // [8 k groups][4 rows][32 columns]
   const float4* xz = reinterpret_cast<const float4*>(a.in + (int64_t)z * B * FLAT);
   for (int e = t; e < B * (FC1_KS / 4); e += blockDim.x) {
     const int row = e / (FC1_KS / 4), q4 = e % (FC1_KS / 4);
     const int src = (row * FLAT + s * FC1_KS) / 4 + q4;
-    const float4 v = WAIT ? load_sc1_f4(xz, B * FLAT * 4, src) : xz[src];
-    *reinterpret_cast<float4*>(s_x + row * FC1_KS + 4 * q4) = v;
+    *reinterpret_cast<float4*>(s_x + row * FC1_KS + 4 * q4) = xz[src];
   }
   __syncthreads();
   float acc[FC1_GEMV_MAXB];
@@ -737,58 +687,15 @@ __device__ __forceinline__ void fc1_gemv_block(const Fc1FwdArgs& a, float* smem,
 __global__ __launch_bounds__(256) void fc1_gemv_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ __attribute__((aligned(16))) float smem[FC1_GEMV_SMEM];
-  fc1_gemv_block<false>(a, smem, blockIdx.x);
+  fc1_gemv_block(a, smem, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 
-__global__ __launch_bounds__(64 * FC1_NW) void fc1_fwd32_kernel(Fc1FwdArgs a) {
+__global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
-  __shared__ float s_red[FC1_NW * FC1_32RW];
-  fc1_fwd_block32<false, FC1_NW>(a, s_red, blockIdx.x);
+  __shared__ float s_red[4 * FC1_32RW];
+  fc1_fwd_block32<false>(a, s_red, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
-
-// ---- conv1 -> conv2 -> conv3 -> fc1 forward in one launch -----------------
-// For launches of at most kFwd8MaxSamples samples and one fc1 row group (the
-// MGSC pass at theta', the HVP's unit-cotangent pass, the actor): the grid of
-// fwd_conv_kernel (8-job conv2 / conv3) followed by the fc1 blocks, which
-// issue their W1 loads at dispatch (the whole 6.4 MB per copy streams while
-// the conv chain runs) and wait for the 8 conv3 arrivals of each sample of
-// their copy.  Every block of such a launch is resident from the start (384
-// at Z = 2, two 57.6 KB blocks per CU), the conv3 producers precede their fc1
-// consumers in dispatch order, and the fc1 launch boundary and its load phase
-// leave the chain.
-template <int F>
-__global__ __launch_bounds__(256) void fwd_fc1_kernel(Conv1FwdArgs c1, LayerFwdArgs c2, LayerFwdArgs c3,
-                                                      Fc1FwdArgs f1) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int zb = c1.Z * c1.B, n = 4 * ((zb + 7) / 8 * 8);
-  int i = blockIdx.x;
-  if (i < n) {
-    const SampleJob sj = xcd_sample_job_at(i, C1_BLOCKS, zb);
-    if (sj.valid) conv1_fwd_body<true, F>(c1, smem, sj);
-    return;
-  }
-  i -= n;
-  if (i < 2 * n) {
-    const SampleJob sj = xcd_sample_job_at(i, 8, zb);
-    if (sj.valid) conv2_fwd8_body(c2, smem, sj);
-    return;
-  }
-  i -= 2 * n;
-  if (i < 2 * n) {
-    const SampleJob sj = xcd_sample_job_at(i, 8, zb);
-    if (sj.valid) conv3_fwd8_body<true>(c3, smem, sj);
-    return;
-  }
-  DQZ_STAMP(3, 0);
-  if (kFc1Gemv && f1.B <= FC1_GEMV_MAXB)
-    fc1_gemv_block<true>(f1, smem, i - 2 * n);
-  else
-    fc1_fwd_block32<false, 4, true>(f1, smem, i - 2 * n);
-  DQZ_STAMP(3, 3);
-}
-static_assert(4 * FC1_32RW * sizeof(float) <= kConv1FwdSmem && FC1_GEMV_SMEM * sizeof(float) <= kConv1FwdSmem,
-              "fc1's tiles fit fwd_fc1_kernel's LDS");
 
 }  // namespace dqz

@@ -60,7 +60,7 @@ struct dqz_learner {
   double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err,
-                  // dz1 cnt/ack (B = 1), fwd y3 cnt/ack [3B] each (fwd_fc1_kernel)
+                  // dz1 cnt/ack (B = 1, head_dx1_kernel)
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
@@ -78,8 +78,6 @@ static int init_kernel_attrs() {
   if (g_attr_done) return DQZ_OK;
   const void* fwd_kernels[] = {(const void*)fwd_conv_kernel<0>, (const void*)fwd_conv_kernel<1>,
                                (const void*)fwd_conv_kernel<2>, (const void*)fwd_conv_kernel<3>,
-                               (const void*)fwd_fc1_kernel<0>,  (const void*)fwd_fc1_kernel<1>,
-                               (const void*)fwd_fc1_kernel<2>,  (const void*)fwd_fc1_kernel<3>,
                                (const void*)tangent_fwd_kernel};
   for (const void* k : fwd_kernels)
     DQZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kConv1FwdSmem));
@@ -126,7 +124,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (22 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
                            2 * (int64_t)B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
@@ -200,12 +198,10 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
 // conv3 as one hand-off launch (fwd_conv_kernel; since conv1 runs on bf16
 // MFMA: 15,590 -> 16,050 steps/s against three launches, which round 4
 // removed), then the split-K fc1.  Used by the learner step and the actor.
-// Launches of at most 16 samples run fc1 in the same launch (fwd_fc1_kernel,
-// DQZ_FWD_FC1; 0 keeps the two launches).
-#ifndef DQZ_FWD_FC1
-#define DQZ_FWD_FC1 1
-#endif
-constexpr bool kFwdFc1 = DQZ_FWD_FC1 != 0;
+// (Round 5: fc1 inside the forward launch for launches of at most 16
+// samples, its W1 loads issued at dispatch and y3 handed over per sample,
+// measured slower at B = 1: the W1 stream stretched the conv chain by 0.9-1.6
+// us, profiles/r05/s8, s9; removed.)
 static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv1Src& src, hipStream_t st,
                         PhaseEvents pe) {
   Conv1FwdArgs c1{};
@@ -247,29 +243,6 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
   c3.wait = c2.pub;
   const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
-  Fc1FwdArgs f1{};
-  f1.in = L->y3;
-  f1.nz = nz;
-  f1.w_off = L->off[6];
-  f1.B = B;
-  f1.MG = (B + 31) / 32;
-  f1.part = L->fc1p;
-  if (kFwdFc1 && jobs == 8 && f1.MG == 1 && !pe.on()) {
-    // small launches: fc1 in the same launch (fwd_fc1_kernel), y3 handed
-    // over per sample to the fc1 blocks of its copy
-    int* yw = L->sync + (16 * Bc + 3) * Handoff::kStride;
-    c3.pub = Handoff{yw, yw + 3 * Bc * Handoff::kStride, err, jobs, fc1_fwd_blocks(1, 1)};
-    f1.wait = c3.pub;
-    const dim3 g2(grid.x + fc1_fwd_blocks(Z, 1));
-    switch (src.fused) {
-      case 1: hipLaunchKernelGGL(fwd_fc1_kernel<1>, g2, dim3(256), kConv1FwdSmem, st, c1, c2, c3, f1); break;
-      case 2: hipLaunchKernelGGL(fwd_fc1_kernel<2>, g2, dim3(256), kConv1FwdSmem, st, c1, c2, c3, f1); break;
-      case 3: hipLaunchKernelGGL(fwd_fc1_kernel<3>, g2, dim3(256), kConv1FwdSmem, st, c1, c2, c3, f1); break;
-      default: hipLaunchKernelGGL(fwd_fc1_kernel<0>, g2, dim3(256), kConv1FwdSmem, st, c1, c2, c3, f1); break;
-    }
-    DQZ_HIP(hipGetLastError());
-    return DQZ_OK;
-  }
   DQZ_PHASE(0, switch (src.fused) {
     case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
     case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
@@ -278,10 +251,17 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   } DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[1] = pe.ms[2] = 0.f;
 
-  DQZ_PHASE(3, if (kFc1Gemv && B <= FC1_GEMV_MAXB)
+  Fc1FwdArgs f1{};
+  f1.in = L->y3;
+  f1.nz = nz;
+  f1.w_off = L->off[6];
+  f1.B = B;
+  f1.MG = (B + 31) / 32;
+  f1.part = L->fc1p;
+  DQZ_PHASE(3, if (B <= FC1_GEMV_MAXB)
                  hipLaunchKernelGGL(fc1_gemv_kernel, dim3(fc1_fwd_blocks(Z, 1)), dim3(256), 0, st, f1);
                else
-                 hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(64 * FC1_NW), 0, st, f1);
+                 hipLaunchKernelGGL(fc1_fwd32_kernel, dim3(fc1_fwd_blocks(Z, f1.MG)), dim3(256), 0, st, f1);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
 }
@@ -557,7 +537,7 @@ int dqz_learner_sync_status(dqz_learner* L, int* status) {
     // later launches pass their waits early.  Clear every hand-off word (and
     // the error word) so the next step starts clean; the caller must treat
     // the steps since the previous check as invalid.
-    DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((22 * L->cfg.batch + 3) * Handoff::kStride + 64)));
+    DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
     DQZ_HIP(hipDeviceSynchronize());
   }
   return DQZ_OK;
