@@ -320,6 +320,14 @@ __device__ __forceinline__ float4 load_sc1_f4(const float4* base, int bytes, int
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 16));
 }
 
+// 8-byte sc1 load of the float pair at element e (even) of a float array of
+// `bytes` bytes whose base is wave-uniform (buffer_load_dwordx2 ... sc1).
+__device__ __forceinline__ float2 load_sc1_f2(const float* base, int bytes, int e) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, e * 4, 0, 16));
+}
+
 // 4-byte sc1 load of element e of a float array of `bytes` bytes whose base
 // is wave-uniform (buffer_load_dword ... sc1).
 __device__ __forceinline__ float load_sc1_f1(const float* base, int bytes, int e) {
