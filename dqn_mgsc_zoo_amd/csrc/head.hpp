@@ -593,7 +593,12 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 // per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
 // RMSProp operands are loaded at entry, under the reduction's latency.
 // SC1 (bwd_upd_kernel): the block first waits for the dW jobs of its layers,
-// then reads their slabs with sc1 loads.
+// then reads their slabs with sc1 loads.  Its polls sleep DQZ_UPD_SLEEP x 64
+// cycles: a thousand blocks polling three words every 256 cycles slowed the
+// backward's dX chain 2x.
+#ifndef DQZ_UPD_SLEEP
+#define DQZ_UPD_SLEEP 32
+#endif
 template <bool SC1 = false>
 __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[UPD_PAIRS], int blk) {
   DQZ_STAMP(9, 0);
@@ -656,7 +661,7 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
     const int m = upd_layers(blk, small_blocks, c1, c2, c3);
 #pragma unroll
     for (int l = 0; l < 3; ++l)
-      if (m & (1 << l)) u.dw[l].wait(0);
+      if (m & (1 << l)) u.dw[l].template wait<DQZ_UPD_SLEEP>(0);
   }
   float2 g = make_float2(0.f, 0.f);
   int64_t unused;
