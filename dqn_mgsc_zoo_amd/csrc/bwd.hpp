@@ -898,6 +898,11 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 #ifndef DQZ_EXP_SKIP
 #define DQZ_EXP_SKIP 0
 #endif
+// Timing-only (bwd_upd_kernel): 1 = the update blocks exit at once, 2 = they
+// skip their waits (the numerics of either are wrong)
+#ifndef DQZ_EXP_UPD
+#define DQZ_EXP_UPD 0
+#endif
 // A/B: the fc1 dW range last in the grid (after conv2 dW) instead of second
 #ifndef DQZ_BWD_FC1_LAST
 #define DQZ_BWD_FC1_LAST 0
@@ -998,6 +1003,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
   }
   if constexpr (UPD) {
     i -= 8 * B8;
+    if (DQZ_EXP_UPD == 1) return;  // timing only: the update range dispatched, no work
     const int nsmall = (int)((HID + (int64_t)HID * u.A + u.nb2 + UPD_PARAMS - 1) / UPD_PARAMS);
     const int nall = (int)update_blocks(u.sz, u.A, u.nb2);
     const int blk = i < nsmall ? i : nall - 1 - (i - nsmall);

@@ -599,6 +599,9 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 #ifndef DQZ_UPD_SLEEP
 #define DQZ_UPD_SLEEP 32
 #endif
+#ifndef DQZ_EXP_UPD
+#define DQZ_EXP_UPD 0
+#endif
 template <bool SC1 = false>
 __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[UPD_PAIRS], int blk) {
   DQZ_STAMP(9, 0);
@@ -657,7 +660,7 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         o_nu[h] = pn[dst[h]];
       }
   }
-  if (SC1) {
+  if (SC1 && DQZ_EXP_UPD != 2) {
     const int m = upd_layers(blk, small_blocks, c1, c2, c3);
 #pragma unroll
     for (int l = 0; l < 3; ++l)
