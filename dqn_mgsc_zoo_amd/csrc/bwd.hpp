@@ -156,7 +156,6 @@ struct Conv3BwdArgs {
   float* part;       // [B][577][64]
   int B;
   Handoff sync;      // per-sample dy2 arrival counters (bwd_bc_kernel)
-  Handoff dw_pub = {};  // conv3 dW slabs -> the update blocks of the same launch (bwd_upd_kernel)
 };
 
 // PUB: dy2 is handed to conv2 dX inside the same launch (bwd_bc_kernel): every
@@ -260,9 +259,10 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 // jobs that accumulate several samples, and a per-XCD pre-reduction of the
 // per-sample slabs inside the launch: both slower, commit 1a3be58.)
 // PUB (bwd_upd_kernel): write-through slab stores and an arrival on the
-// conv3 update word.
+// conv3 word of fo.
 template <bool PUB = false>
-__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq) {
+__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq,
+                                             const LayerFanout* fo = nullptr) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   constexpr int NQ4 = C2M * C2CO / 4;  // 1296
@@ -335,7 +335,7 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
         slab[C3KK * C3CO + 16 * nq + n] = sb;
     }
   }
-  if (PUB) a.dw_pub.arrive(0);
+  if (PUB) fo->arrive(2);
 }
 
 // ---- conv2 backward: dX by stride phase and per-sample dW partials --------
@@ -359,7 +359,6 @@ struct Conv2BwdArgs {
   int B;
   Handoff sync;      // dy2 arrival counters (WAIT)
   Handoff sync1;     // dy1 arrival counters (PUB)
-  Handoff dw_pub = {};  // conv2 dW slabs -> the update blocks of the same launch (bwd_upd_kernel)
 };
 
 // WAIT: dy2 of sample b is produced by the 8 conv3 dX jobs of the same launch
@@ -505,9 +504,10 @@ constexpr int C2V_WIN = 9 * C2W_RS;  // 7272 floats
 // conv2 dW job (sample b, kernel row kh, output-channel half ch): y1 rows to
 // LDS (loaded before the wait), the wait for the sample's dy2, the MFMAs.
 // PUB (bwd_upd_kernel): write-through slab stores and an arrival on the
-// conv2 update word.
+// conv2 word of fo.
 template <bool PUB = false>
-__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch) {
+__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch,
+                                                   const LayerFanout* fo = nullptr) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kw
   const int n = lane & 15, kq = lane >> 4;
   constexpr int NV4 = 9 * C1O * C1CO / 4;  // 1440
@@ -599,7 +599,7 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
       }
     }
   }
-  if (PUB) a.dw_pub.arrive(0);
+  if (PUB) fo->arrive(1);
 }
 
 // ---- fc1 dW + RMSProp, 16 rows x 128 columns per block -------------------
@@ -964,7 +964,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
     if (!sj.valid) return;
     if (DQZ_EXP_SKIP & 2) return;
     DQZ_STAMP(12, 0);
-    conv3_bwd_dw<UPD>(c3, smem, sj.s, sj.job);
+    conv3_bwd_dw<UPD>(c3, smem, sj.s, sj.job, &u.fo);
     DQZ_STAMP(12, 3);
     return;
   }
@@ -979,7 +979,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
       c1.sync1.wait(sj.s);
       return;
     }
-    conv1_dw_half<UPD>(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
+    conv1_dw_half<UPD>(c1, smem, sj.job >> 1, sj.job & 1, sj.s, &u.fo);
     return;
   }
   i -= 8 * B8;
@@ -997,7 +997,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
       return;
     }
     DQZ_STAMP(13, 0);
-    conv2_bwd_dw_split<UPD>(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
+    conv2_bwd_dw_split<UPD>(c2, smem, sj.s, sj.job >> 1, sj.job & 1, &u.fo);
     DQZ_STAMP(13, 3);
     return;
   }

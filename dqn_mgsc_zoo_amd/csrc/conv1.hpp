@@ -306,7 +306,6 @@ struct Conv1DwArgs {
   const float* dy1;  // [B][400][32] (online copy)
   float* part;       // [B*4][257][32]: dW rows 0..255 (HWIO order), db row 256
   Handoff sync1;     // dy1 arrival counters (conv1_dw_half in bwd_bc_kernel)
-  Handoff dw_pub = {};  // PUB: the slab's arrival for the update blocks of the same launch (bwd_upd_kernel)
 };
 
 // Half-channel job of conv1 dW for the merged backward launch (bwd_bc_kernel):
@@ -327,9 +326,10 @@ constexpr int C1H_TLD = 136;  // bf16 per co row of the dy1 image (272 B: 16-byt
 constexpr int C1H_SMEM = (2 * C1_PLANE * 2 + 3 * C1CO * C1H_TLD * 2) / 4 + 16 * C1CO;  // floats
 
 // PUB (bwd_upd_kernel): the slab rows go out as write-through stores and the
-// job arrives on the conv1 update word.
+// job arrives on the conv1 word of fo.
 template <bool PUB = false>
-__device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem, int rb, int ch, int b) {
+__device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem, int rb, int ch, int b,
+                                              const LayerFanout* fo = nullptr) {
   DQZ_STAMP(8, 0);
   uint16_t* s_in = reinterpret_cast<uint16_t*>(smem);  // 2 planes x 2016 bf16
   uint16_t* s_dt = s_in + 2 * C1_PLANE;                 // [3][32][C1H_TLD] bf16
@@ -432,7 +432,7 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
         *reinterpret_cast<f32x4*>(part + row * C1CO + 8 * q + 4 * h) = o;
     }
   }
-  if (PUB) a.dw_pub.arrive(0);
+  if (PUB) fo->arrive(0);
   DQZ_STAMP(8, 3);
 }
 

@@ -398,9 +398,6 @@ inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-constexpr int UPD_PAIRS = 32;                  // parameter pairs per workgroup (64 parameters)
-constexpr int UPD_PARAMS = 2 * UPD_PAIRS;
-constexpr int UPD_GROUPS = 8;                  // threads sharing one pair's reduction
 
 struct UpdArgs {
   float *th, *mu, *nu;
@@ -420,19 +417,12 @@ struct UpdArgs {
   int A, B, nb2;
   Rms rms;
   // bwd_upd_kernel: the conv1 / conv2 / conv3 dW partials are produced in the
-  // same launch; a block waits on the layers its parameters belong to
-  // (upd_layers) and reads the slabs with sc1 loads
-  Handoff dw[3] = {};
+  // same launch; a block waits for the layers its parameters belong to
+  // (LayerFanout) and reads the slabs with sc1 loads
+  LayerFanout fo = {};
   int slab_bytes[3] = {0, 0, 0};  // p1 / p2 / p3 sizes (the sc1 loads' buffer ranges)
 };
 
-// Layers (bit 0 conv1, 1 conv2, 2 conv3) whose parameters update block blk
-// owns (a 64-parameter block can straddle two); 0 for the small head leaves.
-__host__ __device__ inline int upd_layers(int blk, int small_blocks, int64_t c1, int64_t c2, int64_t c3) {
-  if (blk < small_blocks) return 0;
-  const int64_t lo = (int64_t)(blk - small_blocks) * UPD_PARAMS, hi = lo + UPD_PARAMS;
-  return (lo < c1 ? 1 : 0) | (lo < c2 && hi > c1 ? 2 : 0) | (lo < c3 && hi > c2 ? 4 : 0);
-}
 
 
 // One float2 of slab s: a plain load, or (SC1: the slabs were written in the
@@ -593,9 +583,8 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 // per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
 // RMSProp operands are loaded at entry, under the reduction's latency.
 // SC1 (bwd_upd_kernel): the block first waits for the dW jobs of its layers,
-// then reads their slabs with sc1 loads.  Its polls sleep DQZ_UPD_SLEEP x 64
-// cycles: a thousand blocks polling three words every 256 cycles slowed the
-// backward's dX chain 2x.
+// then reads their slabs with sc1 loads.  Its polls (of its own flag words)
+// sleep DQZ_UPD_SLEEP x 64 cycles.
 #ifndef DQZ_UPD_SLEEP
 #define DQZ_UPD_SLEEP 32
 #endif
@@ -660,12 +649,7 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         o_nu[h] = pn[dst[h]];
       }
   }
-  if (SC1 && DQZ_EXP_UPD != 2) {
-    const int m = upd_layers(blk, small_blocks, c1, c2, c3);
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-      if (m & (1 << l)) u.dw[l].template wait<DQZ_UPD_SLEEP>(0);
-  }
+  if (SC1 && DQZ_EXP_UPD != 2) u.fo.template wait<DQZ_UPD_SLEEP>(blk);
   float2 g = make_float2(0.f, 0.f);
   int64_t unused;
   if (small) {
