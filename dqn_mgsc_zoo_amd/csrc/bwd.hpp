@@ -258,11 +258,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 // conv3 dW job (sample b, output-channel quarter nq).  (Round 3 measured
 // jobs that accumulate several samples, and a per-XCD pre-reduction of the
 // per-sample slabs inside the launch: both slower, commit 1a3be58.)
-// PUB (bwd_upd_kernel): write-through slab stores and an arrival on the
-// conv3 word of fo.
-template <bool PUB = false>
-__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq,
-                                             const LayerFanout* fo = nullptr) {
+__device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win, int b, int nq) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   constexpr int NQ4 = C2M * C2CO / 4;  // 1296
@@ -316,26 +312,14 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
   for (int kk = 0; kk < 13; ++kk) sb += dr[kk];
   // C layout: row = 4 kq + r -> co = 16 nq + 4 kq + r; col = n -> ci = 16 w + n of tap tp
   float* slab = a.part + (int64_t)b * (C3KK + 1) * C3CO;
-  constexpr int kSlabBytes = (C3KK + 1) * C3CO * 4;
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp) {
-    const int o = (tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq;
-    if (PUB)
-      store_sc1_f4(slab, kSlabBytes, 4 * o, acc[tp]);
-    else
-      *reinterpret_cast<f32x4*>(slab + o) = acc[tp];
-  }
+  for (int tp = 0; tp < 9; ++tp)
+    *reinterpret_cast<f32x4*>(slab + (tp * C3CI + 16 * w + n) * C3CO + 16 * nq + 4 * kq) = acc[tp];
   if (w == 0) {  // bias row
     sb += __shfl_xor(sb, 16, 64);
     sb += __shfl_xor(sb, 32, 64);
-    if (kq == 0) {
-      if (PUB)
-        store_sc1_f1(slab, kSlabBytes, C3KK * C3CO + 16 * nq + n, sb);
-      else
-        slab[C3KK * C3CO + 16 * nq + n] = sb;
-    }
+    if (kq == 0) slab[C3KK * C3CO + 16 * nq + n] = sb;
   }
-  if (PUB) fo->arrive(2);
 }
 
 // ---- conv2 backward: dX by stride phase and per-sample dW partials --------
@@ -503,11 +487,7 @@ constexpr int C2V_WIN = 9 * C2W_RS;  // 7272 floats
 
 // conv2 dW job (sample b, kernel row kh, output-channel half ch): y1 rows to
 // LDS (loaded before the wait), the wait for the sample's dy2, the MFMAs.
-// PUB (bwd_upd_kernel): write-through slab stores and an arrival on the
-// conv2 word of fo.
-template <bool PUB = false>
-__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch,
-                                                   const LayerFanout* fo = nullptr) {
+__device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float* s_win, int b, int kh, int ch) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kw
   const int n = lane & 15, kq = lane >> 4;
   constexpr int NV4 = 9 * C1O * C1CO / 4;  // 1440
@@ -574,32 +554,21 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
     for (int kk = 0; kk < 21; ++kk) sb[ct] += dr[kk][ct];
   // C: row 4 kq + r -> co = 32 ch + 16 ct + 4 kq + r; col n -> ci = 16 mt + n
   float* slab = a.part + (int64_t)b * (C2KK + 1) * C2CO;
-  constexpr int kSlabBytes = (C2KK + 1) * C2CO * 4;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const int o = ((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq;
-      if (PUB)
-        store_sc1_f4(slab, kSlabBytes, 4 * o, acc[mt][ct]);
-      else
-        *reinterpret_cast<f32x4*>(slab + o) = acc[mt][ct];
-    }
+    for (int ct = 0; ct < 2; ++ct)
+      *reinterpret_cast<f32x4*>(slab + ((kh * C2K + w) * C2CI + 16 * mt + n) * C2CO + 32 * ch + 16 * ct + 4 * kq) =
+          acc[mt][ct];
   if (kh == 0 && w == 0) {  // bias row (per lane over its kk, then over kq)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       float v = sb[ct];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (kq == 0) {
-        if (PUB)
-          store_sc1_f1(slab, kSlabBytes, C2KK * C2CO + 32 * ch + 16 * ct + n, v);
-        else
-          slab[C2KK * C2CO + 32 * ch + 16 * ct + n] = v;
-      }
+      if (kq == 0) slab[C2KK * C2CO + 32 * ch + 16 * ct + n] = v;
     }
   }
-  if (PUB) fo->arrive(1);
 }
 
 // ---- fc1 dW + RMSProp, 16 rows x 128 columns per block -------------------
@@ -898,24 +867,21 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 #ifndef DQZ_EXP_SKIP
 #define DQZ_EXP_SKIP 0
 #endif
-// Timing-only (bwd_upd_kernel): 1 = the update blocks exit at once, 2 = they
-// skip their waits (the numerics of either are wrong)
-#ifndef DQZ_EXP_UPD
-#define DQZ_EXP_UPD 0
-#endif
+// (Round 5: the optimizer update as this launch's last range, each update
+// block waiting for the dW jobs of its layers, which stored their slabs
+// write-through and drained before arriving: correct, but the drains
+// stretched the conv1 dW tail by 3 us, as much as the update launch's
+// boundary saved (16,210 against 16,244 steps/s; first-order meta-update
+// 193 -> 201 us; profiles/r05/s13).  With a thousand update blocks polling
+// three shared words the launch ran 1.3x slower (s10-s12).  Removed.)
 // A/B: the fc1 dW range last in the grid (after conv2 dW) instead of second
 #ifndef DQZ_BWD_FC1_LAST
 #define DQZ_BWD_FC1_LAST 0
 #endif
 constexpr bool kBwdFc1Last = DQZ_BWD_FC1_LAST != 0;
-// UPD (bwd_upd_kernel): the optimizer update follows as the last range
-// (update_body's blocks, the conv ones in reverse order so conv3's, whose
-// slabs are ready first, dispatch first); the dW jobs publish their slabs
-// write-through and arrive on their layer's word, and each update block
-// waits for the layers it owns.  Removes the update launch and its boundary.
-template <bool WB, bool UPD = false>
-__device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArgs& f1, const Conv2BwdArgs& c2,
-                                         const Conv1DwArgs& c1, const PerWbArgs& wb, const UpdArgs& u) {
+template <bool WB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
+    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
   constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
   constexpr int kW2 = C2X_WIN > C3W_WIN ? C2X_WIN : C3W_WIN;
   constexpr int kW3 = C2V_WIN > C1H_SMEM ? C2V_WIN : C1H_SMEM;
@@ -964,7 +930,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
     if (!sj.valid) return;
     if (DQZ_EXP_SKIP & 2) return;
     DQZ_STAMP(12, 0);
-    conv3_bwd_dw<UPD>(c3, smem, sj.s, sj.job, &u.fo);
+    conv3_bwd_dw(c3, smem, sj.s, sj.job);
     DQZ_STAMP(12, 3);
     return;
   }
@@ -979,7 +945,7 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
       c1.sync1.wait(sj.s);
       return;
     }
-    conv1_dw_half<UPD>(c1, smem, sj.job >> 1, sj.job & 1, sj.s, &u.fo);
+    conv1_dw_half(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
     return;
   }
   i -= 8 * B8;
@@ -989,38 +955,15 @@ __device__ __forceinline__ void bwd_body(const Conv3BwdArgs& c3, const Fc1BwdArg
     fc1_dw_body(f1, smem, i);
     return;
   }
-  if (!UPD || i < 8 * B8) {
-    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
-    if (!sj.valid) return;
-    if (DQZ_EXP_SKIP & 4) {
-      c2.sync.wait(sj.s);
-      return;
-    }
-    DQZ_STAMP(13, 0);
-    conv2_bwd_dw_split<UPD>(c2, smem, sj.s, sj.job >> 1, sj.job & 1, &u.fo);
-    DQZ_STAMP(13, 3);
+  const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
+  if (!sj.valid) return;
+  if (DQZ_EXP_SKIP & 4) {
+    c2.sync.wait(sj.s);
     return;
   }
-  if constexpr (UPD) {
-    i -= 8 * B8;
-    if (DQZ_EXP_UPD == 1) return;  // timing only: the update range dispatched, no work
-    const int nsmall = (int)((HID + (int64_t)HID * u.A + u.nb2 + UPD_PARAMS - 1) / UPD_PARAMS);
-    const int nall = (int)update_blocks(u.sz, u.A, u.nb2);
-    const int blk = i < nsmall ? i : nall - 1 - (i - nsmall);
-    update_body<true>(u, reinterpret_cast<float2(*)[UPD_PAIRS]>(smem), blk);
-  }
-}
-
-template <bool WB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
-    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
-  bwd_body<WB, false>(c3, f1, c2, c1, wb, UpdArgs{});
-}
-
-template <bool WB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_upd_kernel(
-    Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb, UpdArgs u) {
-  bwd_body<WB, true>(c3, f1, c2, c1, wb, u);
+  DQZ_STAMP(13, 0);
+  conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
+  DQZ_STAMP(13, 3);
 }
 
 }  // namespace dqz

@@ -293,13 +293,11 @@ struct Handoff {
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + b * kStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // SLEEP: s_sleep units (64 cycles each) between polls
-  template <int SLEEP = 4>
   __device__ __forceinline__ void wait(int b) const {
     if (threadIdx.x == 0) {
       unsigned spins = 0;
       while (__hip_atomic_load(cnt + b * kStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        __builtin_amdgcn_s_sleep(SLEEP);
+        __builtin_amdgcn_s_sleep(4);
         if (++spins > spin_max) {
           __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -314,89 +312,12 @@ struct Handoff {
   }
 };
 
-// Optimizer-update blocks (update_body): 64 parameters each, 8 reduction groups.
-constexpr int UPD_PAIRS = 32;                  // parameter pairs per workgroup (64 parameters)
-constexpr int UPD_PARAMS = 2 * UPD_PAIRS;
-constexpr int UPD_GROUPS = 8;                  // threads sharing one pair's reduction
-
-// Layers (bit 0 conv1, 1 conv2, 2 conv3) whose parameters update block blk
-// owns (a 64-parameter block can straddle two); 0 for the small head leaves.
-__host__ __device__ inline int upd_layers(int blk, int small_blocks, int64_t c1, int64_t c2, int64_t c3) {
-  if (blk < small_blocks) return 0;
-  const int64_t lo = (int64_t)(blk - small_blocks) * UPD_PARAMS, hi = lo + UPD_PARAMS;
-  return (lo < c1 ? 1 : 0) | (lo < c2 && hi > c1 ? 2 : 0) | (lo < c3 && hi > c2 ? 4 : 0);
-}
-
-// Layer -> update-block fan-out (bwd_upd_kernel).  The dW jobs of conv layer
-// l count their arrivals on word l (after their write-through slab stores and
-// vmcnt(0), as Handoff::arrive); the one whose add completes the count resets
-// the word and sets flag l of every update block that owns parameters of the
-// layer, each block's flags on a 64-byte line of their own.  An update block
-// polls only its own flags and clears them once past.  (Round 5: a thousand
-// update blocks polling the three shared words queued at their memory channel
-// and slowed the whole backward launch 1.3x, even at one poll per 3.4 us.)
-struct LayerFanout {
-  static constexpr int kFlagStride = 16;  // ints per update block's flag line
-  int* cnt;         // [3 x Handoff::kStride] arrival words
-  int* flag;        // [nblk x kFlagStride]: flag l set once layer l's slabs are all stored
-  int need[3];      // dW jobs per layer (conv1, conv2, conv3)
-  int nblk, nsmall;
-  int64_t c1, c2, c3;  // layer ends in the update blocks' parameter order
-  int* err;
-  unsigned spin_max;
-  // every thread of a producer block, after its slab stores
-  __device__ __forceinline__ void arrive(int l) const {
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(cnt + l * Handoff::kStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               need[l] - 1;
-    __syncthreads();
-    if (s_last) {
-      if (threadIdx.x == 0) __hip_atomic_store(cnt + l * Handoff::kStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int k = nsmall + (int)threadIdx.x; k < nblk; k += (int)blockDim.x)
-        if ((upd_layers(k, nsmall, c1, c2, c3) >> l) & 1)
-          __hip_atomic_store(flag + (int64_t)k * kFlagStride + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  // every thread of update block blk; one lane polls its flags
-  template <int SLEEP>
-  __device__ __forceinline__ void wait(int blk) const {
-    const int m = upd_layers(blk, nsmall, c1, c2, c3);
-    if (threadIdx.x == 0) {
-      for (int l = 0; l < 3; ++l) {
-        if (!((m >> l) & 1)) continue;
-        int* f = flag + (int64_t)blk * kFlagStride + l;
-        unsigned spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-          __builtin_amdgcn_s_sleep(SLEEP);
-          if (++spins > spin_max) {
-            __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-        __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-  }
-};
-
 // 16-byte sc1 (L1-bypassing) load of element e of a float4 array of `bytes`
 // bytes whose base is wave-uniform (buffer_load_dwordx4 ... sc1).
 __device__ __forceinline__ float4 load_sc1_f4(const float4* base, int bytes, int e) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 16));
-}
-
-// 8-byte sc1 load of the float pair at element e (even) of a float array of
-// `bytes` bytes whose base is wave-uniform (buffer_load_dwordx2 ... sc1).
-__device__ __forceinline__ float2 load_sc1_f2(const float* base, int bytes, int e) {
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
-  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, e * 4, 0, 16));
 }
 
 // 4-byte sc1 load of element e of a float array of `bytes` bytes whose base

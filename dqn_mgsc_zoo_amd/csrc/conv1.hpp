@@ -325,11 +325,7 @@ struct Conv1DwArgs {
 constexpr int C1H_TLD = 136;  // bf16 per co row of the dy1 image (272 B: 16-byte lane reads spread over the banks)
 constexpr int C1H_SMEM = (2 * C1_PLANE * 2 + 3 * C1CO * C1H_TLD * 2) / 4 + 16 * C1CO;  // floats
 
-// PUB (bwd_upd_kernel): the slab rows go out as write-through stores and the
-// job arrives on the conv1 word of fo.
-template <bool PUB = false>
-__device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem, int rb, int ch, int b,
-                                              const LayerFanout* fo = nullptr) {
+__device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem, int rb, int ch, int b) {
   DQZ_STAMP(8, 0);
   uint16_t* s_in = reinterpret_cast<uint16_t*>(smem);  // 2 planes x 2016 bf16
   uint16_t* s_dt = s_in + 2 * C1_PLANE;                 // [3][32][C1H_TLD] bf16
@@ -386,14 +382,10 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, i = lane & 31;
   float* part = a.part + ((int64_t)b * C1_BLOCKS + rb) * (C1KK + 1) * C1CO;
-  constexpr int kSlabBytes = (C1KK + 1) * C1CO * 4;
   if (ch == 0 && tid < C1CO) {  // bias row
     float sb = 0.f;
     for (int c = 0; c < 15; ++c) sb += s_bp[c * C1CO + tid];
-    if (PUB)
-      store_sc1_f1(part, kSlabBytes, C1KK * C1CO + tid, sb);
-    else
-      part[C1KK * C1CO + tid] = sb;
+    part[C1KK * C1CO + tid] = sb;
   }
   const int kh = 2 * wave + (i >> 4), kw = (i >> 1) & 7, cp = i & 1;
   const uint16_t* pb = s_in + cp * C1_PLANE + kh * FW + kw;
@@ -424,15 +416,10 @@ __device__ __forceinline__ void conv1_dw_half(const Conv1DwArgs& a, float* smem,
   {
     const int row = (2 * wave + (i >> 4)) * 32 + ((i >> 1) & 7) * 4 + 2 * ch + (i & 1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 o{div255(acc[4 * q]), div255(acc[4 * q + 1]), div255(acc[4 * q + 2]), div255(acc[4 * q + 3])};
-      if (PUB)
-        store_sc1_f4(part, kSlabBytes, 4 * (row * C1CO + 8 * q + 4 * h), o);
-      else
-        *reinterpret_cast<f32x4*>(part + row * C1CO + 8 * q + 4 * h) = o;
-    }
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<f32x4*>(part + row * C1CO + 8 * q + 4 * h) =
+          f32x4{div255(acc[4 * q]), div255(acc[4 * q + 1]), div255(acc[4 * q + 2]), div255(acc[4 * q + 3])};
   }
-  if (PUB) fo->arrive(0);
   DQZ_STAMP(8, 3);
 }
 

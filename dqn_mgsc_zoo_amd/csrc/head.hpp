@@ -398,7 +398,6 @@ inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-
 struct UpdArgs {
   float *th, *mu, *nu;
   int64_t off[10];
@@ -416,29 +415,17 @@ struct UpdArgs {
   int* status;  // learner health word: bit 1 set when the batch loss is not finite
   int A, B, nb2;
   Rms rms;
-  // bwd_upd_kernel: the conv1 / conv2 / conv3 dW partials are produced in the
-  // same launch; a block waits for the layers its parameters belong to
-  // (LayerFanout) and reads the slabs with sc1 loads
-  LayerFanout fo = {};
-  int slab_bytes[3] = {0, 0, 0};  // p1 / p2 / p3 sizes (the sc1 loads' buffer ranges)
 };
 
-
-
-// One float2 of slab s: a plain load, or (SC1: the slabs were written in the
-// same launch, bwd_upd_kernel) an sc1 load within the array's `bytes`.
-template <bool SC1>
-__device__ __forceinline__ float2 slab_f2(const float* p, int bytes, int64_t idx) {
-  if (SC1) return load_sc1_f2(p, bytes, (int)idx);
-  return *reinterpret_cast<const float2*>(p + idx);
-}
+constexpr int UPD_PAIRS = 32;                  // parameter pairs per workgroup (64 parameters)
+constexpr int UPD_PARAMS = 2 * UPD_PAIRS;
+constexpr int UPD_GROUPS = 8;                  // threads sharing one pair's reduction
 
 // Sum of the float2 p[s * stride + j .. +1] over s = g, g + G, ... < S, eight
 // loads in flight per iteration (the slabs are written by the previous
 // kernel, so every load is a cache miss; one dependent chain per slab would
 // be latency-bound).
-template <bool SC1>
-__device__ __forceinline__ float2 sum_split2(const float* p, int bytes, int S, int64_t stride, int64_t j, int g) {
+__device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stride, int64_t j, int g) {
   constexpr int G = UPD_GROUPS;
   float2 a[8];
 #pragma unroll
@@ -447,7 +434,7 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int bytes, int S, i
   for (; s + 7 * G < S; s += 8 * G) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const float2 v = slab_f2<SC1>(p, bytes, (int64_t)(s + u * G) * stride + j);
+      const float2 v = *reinterpret_cast<const float2*>(p + (int64_t)(s + u * G) * stride + j);
       a[u].x += v.x;
       a[u].y += v.y;
     }
@@ -457,7 +444,7 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int bytes, int S, i
   // conditional load per branch waited for each one in turn)
   float2 v[8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) v[u] = slab_f2<SC1>(p, bytes, (int64_t)min(s + u * G, S - 1) * stride + j);
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(p + (int64_t)min(s + u * G, S - 1) * stride + j);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < 8; ++u)
@@ -475,15 +462,15 @@ __device__ __forceinline__ float2 sum_split2(const float* p, int bytes, int S, i
 // loop form above issues one round of eight loads per dependent step and a
 // ninth round for its tail (conv1's 4 B = 128 slabs took three serial round
 // trips at B = 32; conv2 / conv3's 32 slabs one).
-template <int R, bool SC1>
-__device__ __forceinline__ float2 sum_split2_r(const float* p, int bytes, int S, int64_t stride, int64_t j, int g) {
+template <int R>
+__device__ __forceinline__ float2 sum_split2_r(const float* p, int S, int64_t stride, int64_t j, int g) {
   constexpr int G = UPD_GROUPS;
   float2 v[R][8];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      v[r][u] = slab_f2<SC1>(p, bytes, (int64_t)min(g + (8 * r + u) * G, S - 1) * stride + j);
+      v[r][u] = *reinterpret_cast<const float2*>(p + (int64_t)min(g + (8 * r + u) * G, S - 1) * stride + j);
   __builtin_amdgcn_sched_barrier(0);
   float2 a[8];
 #pragma unroll
@@ -505,12 +492,11 @@ __device__ __forceinline__ float2 sum_split2_r(const float* p, int bytes, int S,
 // (Wider forms, up to 56 loads per lane for the M = 100 meta batch's 400
 // conv1 slabs, cost that kernel 0.5 us: 162 VGPRs left its 1,276 blocks no
 // longer all resident; profiles/r05/c7.)
-template <bool SC1>
-__device__ __forceinline__ float2 sum_slabs(const float* p, int bytes, int S, int64_t stride, int64_t j, int g) {
-  if (!DQZ_UPD_BATCH) return sum_split2<SC1>(p, bytes, S, stride, j, g);
-  if (S <= 8 * UPD_GROUPS) return sum_split2_r<1, SC1>(p, bytes, S, stride, j, g);
-  if (S <= 16 * UPD_GROUPS) return sum_split2_r<2, SC1>(p, bytes, S, stride, j, g);
-  return sum_split2<SC1>(p, bytes, S, stride, j, g);
+__device__ __forceinline__ float2 sum_slabs(const float* p, int S, int64_t stride, int64_t j, int g) {
+  if (!DQZ_UPD_BATCH) return sum_split2(p, S, stride, j, g);
+  if (S <= 8 * UPD_GROUPS) return sum_split2_r<1>(p, S, stride, j, g);
+  if (S <= 16 * UPD_GROUPS) return sum_split2_r<2>(p, S, stride, j, g);
+  return sum_split2(p, S, stride, j, g);
 }
 
 // One gradient element of the small head leaves (fc1/b, fc2/w, fc2/b): this
@@ -582,16 +568,6 @@ __device__ __forceinline__ float small_grad(const UpdArgs& u, int64_t e, int grp
 // LDS.  Grid: the small head leaves first (their blocks run the longest
 // per-sample loops), then conv1, conv2, conv3 (float2 partial loads).  The
 // RMSProp operands are loaded at entry, under the reduction's latency.
-// SC1 (bwd_upd_kernel): the block first waits for the dW jobs of its layers,
-// then reads their slabs with sc1 loads.  Its polls (of its own flag words)
-// sleep DQZ_UPD_SLEEP x 64 cycles.
-#ifndef DQZ_UPD_SLEEP
-#define DQZ_UPD_SLEEP 32
-#endif
-#ifndef DQZ_EXP_UPD
-#define DQZ_EXP_UPD 0
-#endif
-template <bool SC1 = false>
 __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[UPD_PAIRS], int blk) {
   DQZ_STAMP(9, 0);
   const int pl = threadIdx.x % UPD_PAIRS, grp = threadIdx.x / UPD_PAIRS;
@@ -649,18 +625,17 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
         o_nu[h] = pn[dst[h]];
       }
   }
-  if (SC1 && DQZ_EXP_UPD != 2) u.fo.template wait<DQZ_UPD_SLEEP>(blk);
   float2 g = make_float2(0.f, 0.f);
   int64_t unused;
   if (small) {
     g.x = small_grad(u, e, grp, unused);
     g.y = small_grad(u, e + 1, grp, unused);
   } else if (e < c1) {
-    g = sum_slabs<SC1>(u.p1, u.slab_bytes[0], u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
+    g = sum_slabs(u.p1, u.S1, (int64_t)(C1KK + 1) * C1CO, e, grp);
   } else if (e < c2) {
-    g = sum_slabs<SC1>(u.p2, u.slab_bytes[1], u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
+    g = sum_slabs(u.p2, u.S2, (int64_t)(C2KK + 1) * C2CO, e - c1, grp);
   } else if (e < c3) {
-    g = sum_slabs<SC1>(u.p3, u.slab_bytes[2], u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
+    g = sum_slabs(u.p3, u.S3, (int64_t)(C3KK + 1) * C3CO, e - c2, grp);
   }
   s_part[grp][pl] = g;
   if (blk == 0 && threadIdx.x < 64) {
@@ -728,7 +703,7 @@ __device__ __forceinline__ void update_body(const UpdArgs& u, float2 (*s_part)[U
   DQZ_STAMP(9, 3);
 }
 
-__host__ __device__ inline unsigned update_blocks(const int64_t sz[10], int A, int nb2) {
+inline unsigned update_blocks(const int64_t sz[10], int A, int nb2) {
   const int64_t nconv = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
   const int64_t nsmall = HID + (int64_t)HID * A + nb2;
   return (unsigned)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS + (nconv + UPD_PARAMS - 1) / UPD_PARAMS);

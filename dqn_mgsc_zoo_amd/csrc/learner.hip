@@ -60,7 +60,7 @@ struct dqz_learner {
   double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
   int32_t* ga;
   int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err,
-                  // dz1 cnt/ack (B = 1, head_dx1_kernel), dW -> update words and flags (sync_ints)
+                  // dz1 cnt/ack (B = 1, head_dx1_kernel)
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
@@ -101,16 +101,6 @@ int dqz_param_layout(int num_actions, int shared_bias, int64_t offsets[10], int6
   return DQZ_OK;
 }
 
-// Hand-off words of a learner of batch B (dqz_learner::sync): [0, 16 B) the
-// per-sample pairs, 16 B the error word, 16 B + 1 / + 2 the B = 1 dz1 pair,
-// [16 B + 3, 16 B + 6) the dW -> update layer words, then LayerFanout's flag
-// lines (one per update block).
-static int64_t sync_ints(int B, int A, int shared_bias) {
-  int64_t off[10], sz[10], total;
-  param_layout(A, shared_bias, off, sz, &total);
-  return (16 * (int64_t)B + 6) * Handoff::kStride + (int64_t)update_blocks(sz, A, shared_bias ? 1 : A) * LayerFanout::kFlagStride + 64;
-}
-
 int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   if (!cfg || !out) return fail(DQZ_ERR_INVALID, "null argument");
   if (cfg->batch < 1 || cfg->batch > MAXB) return fail(DQZ_ERR_INVALID, "batch must be in [1, %d]", MAXB);
@@ -134,7 +124,7 @@ int dqz_learner_create(const dqz_learner_config* cfg, dqz_learner** out) {
   const int64_t n_p1 = (int64_t)B * C1_BLOCKS * (C1KK + 1) * C1CO, n_p2 = (int64_t)L->S2 * (C2KK + 1) * C2CO,
                 n_p3 = (int64_t)L->S3 * (C3KK + 1) * C3CO;
   const int64_t sizes[] = {n_y1, n_y2, n_y3, n_fc1p, n_h1, n_q, n_dz1, n_dy3, n_dy2, n_dy1,
-                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, sync_ints(B, A, L->shared_bias), W3P_N, W2P_N,
+                           n_p1, n_p2, n_p3, B,      1,    B,   B,     B,  4 * B, (16 * B + 3) * Handoff::kStride + 64, W3P_N, W2P_N,
                            2 * (int64_t)B};
   float** ptrs[] = {&L->y1,  &L->y2,  &L->y3,  &L->fc1p, &L->h1,   &L->q,         &L->dz1, &L->dy3,
                     &L->dy2, &L->dy1, &L->p1,  &L->p2,   &L->p3,   &L->td,        &L->loss, &L->loss_part,
@@ -208,13 +198,6 @@ static const PhaseEvents kNoProfile{nullptr, nullptr, 0, nullptr};
 // conv3 as one hand-off launch (fwd_conv_kernel; since conv1 runs on bf16
 // MFMA: 15,590 -> 16,050 steps/s against three launches, which round 4
 // removed), then the split-K fc1.  Used by the learner step and the actor.
-// The optimizer update as the backward launch's last range (bwd_upd_kernel,
-// DQZ_BWD_UPD; 0 keeps the update launch).  Not with the timing-only
-// DQZ_EXP_SKIP switches (skipped dW jobs do not arrive).
-#ifndef DQZ_BWD_UPD
-#define DQZ_BWD_UPD 1
-#endif
-constexpr bool kBwdUpd = DQZ_BWD_UPD != 0 && DQZ_EXP_SKIP == 0;
 // (Round 5: fc1 inside the forward launch for launches of at most 16
 // samples, its W1 loads issued at dispatch and y3 handed over per sample,
 // measured slower at B = 1: the W1 stream stretched the conv chain by 0.9-1.6
@@ -459,6 +442,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.n = B;
   }
   const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
+  DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
+            else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
+            DQZ_HIP(hipGetLastError()));
+  if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
   UpdArgs u{};
   u.th = P->online;
@@ -487,39 +474,6 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   u.rms = rms;
   u.rms.sq_off = 4 * (FLAT / 16);  // meta_rms2 partials: the fc1 dW blocks' first, then the update's
   const unsigned nblk = update_blocks(L->sz, A, u.nb2);
-  if (kBwdUpd && !pe.on()) {
-    // the update as the backward launch's last range (bwd_upd_kernel): the dW
-    // jobs of layer l arrive on word l (after the error word and the B = 1
-    // dz1 pair), the last of them sets the flags of the update blocks that own
-    // the layer's parameters (the flag lines follow the three words)
-    LayerFanout& fo = u.fo;
-    fo.cnt = L->sync + (16 * B + 3) * Handoff::kStride;
-    fo.flag = L->sync + (16 * B + 6) * Handoff::kStride;
-    fo.need[0] = 8 * B;  // conv1 / conv2 / conv3 dW jobs
-    fo.need[1] = 8 * B;
-    fo.need[2] = 4 * B;
-    fo.nblk = (int)nblk;
-    fo.nsmall = (int)((HID + (int64_t)HID * A + u.nb2 + UPD_PARAMS - 1) / UPD_PARAMS);
-    fo.c1 = L->sz[0] + L->sz[1];
-    fo.c2 = fo.c1 + L->sz[2] + L->sz[3];
-    fo.c3 = fo.c2 + L->sz[4] + L->sz[5];
-    fo.err = herr;
-    fo.spin_max = L->spin_max;
-    u.slab_bytes[0] = (int)(sizeof(float) * (int64_t)u.S1 * (C1KK + 1) * C1CO);
-    u.slab_bytes[1] = (int)(sizeof(float) * (int64_t)u.S2 * (C2KK + 1) * C2CO);
-    u.slab_bytes[2] = (int)(sizeof(float) * (int64_t)u.S3 * (C3KK + 1) * C3CO);
-    const dim3 g2(grid + nblk);
-    if (wb)
-      hipLaunchKernelGGL(bwd_upd_kernel<true>, g2, dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk, u);
-    else
-      hipLaunchKernelGGL(bwd_upd_kernel<false>, g2, dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk, u);
-    DQZ_HIP(hipGetLastError());
-    return DQZ_OK;
-  }
-  DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-            else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-            DQZ_HIP(hipGetLastError()));
-  if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
   DQZ_PHASE(9, hipLaunchKernelGGL(update_kernel, dim3(nblk), dim3(256), 0, st, u);
             DQZ_HIP(hipGetLastError()));
   return DQZ_OK;
@@ -583,7 +537,7 @@ int dqz_learner_sync_status(dqz_learner* L, int* status) {
     // later launches pass their waits early.  Clear every hand-off word (and
     // the error word) so the next step starts clean; the caller must treat
     // the steps since the previous check as invalid.
-    DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * sync_ints(L->cfg.batch, L->cfg.num_actions, L->shared_bias)));
+    DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
     DQZ_HIP(hipDeviceSynchronize());
   }
   return DQZ_OK;
