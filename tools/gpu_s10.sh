@@ -1,0 +1,30 @@
+#!/bin/bash
+# Session: the full GPU suite (stop at the first failure), then interleaved
+# learner benches and meta benches of base (update in the backward launch)
+# and noupd, and B = 32 step traces of both.
+set -o pipefail
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/s10
+mkdir -p $OUT
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q -rf --timeout 240 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> $OUT/gpu_tests.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+set -e
+for r in 1 2 3; do
+  for v in base noupd; do
+    DQZ_LIB=$ROOT/dqn_mgsc_zoo_amd/libdqz_$v.so timeout -k 10 120 python bench.py --steps 20000 --warmup 500 --cpu-seconds 0 --capacity 200000 > $OUT/bench_${v}_$r.json 2> $OUT/bench_${v}_$r.err
+    python -c "import json; d=json.load(open('$OUT/bench_${v}_$r.json')); print('$v', $r, d['value'], d['handoff_status'], {k: round(x*1e3,2) for k,x in d['phase_ms'].items()})" | tee -a $OUT/summary.txt
+  done
+done
+for r in 1 2; do
+  for v in base noupd; do
+    DQZ_LIB=$ROOT/dqn_mgsc_zoo_amd/libdqz_$v.so timeout -k 10 300 python tools/meta_bench.py --steps 100 > $OUT/meta_${v}_$r.json 2> $OUT/meta_${v}_$r.err
+    python -c "import json; d=json.load(open('$OUT/meta_${v}_$r.json')); print('$v', $r, {k: round(1e3*x['ms_per_step'],1) for k,x in d.items() if k.startswith('meta')})" | tee -a $OUT/summary.txt
+  done
+done
+export DQZ_TRACE_PREBUILT=1
+DQZ_TRACE_LIB=$ROOT/dqn_mgsc_zoo_amd/libdqz_trace.so timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_base.txt 2>&1
+DQZ_TRACE_LIB=$ROOT/dqn_mgsc_zoo_amd/libdqz_trace_noupd.so timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_noupd.txt 2>&1
+timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver_cmd.json 2> $OUT/bench_driver.err
+exit 0
