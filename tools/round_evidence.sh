@@ -1,11 +1,12 @@
 #!/bin/bash
 # A round's evidence on the GPU box: GPU suite, smoke, the driver's bench
 # command, the default bench, configs 4 / 3 / 1, SURVEY §8(d)'s median of
-# five 10,000-step runs, a kernel-trace profile, the four PMC passes and a
-# step trace.  Test failures (rc 1) do not stop the rest; any other failure does.
+# five 10,000-step runs, the MGSC meta-update bench and its kernel trace, a
+# kernel-trace profile, the four PMC passes and a step trace.  Test failures (rc 1) do not stop the rest; any other failure does.
 # usage: bash tools/round_evidence.sh <tag>
 set -o pipefail
 TAG=${1:-r04}
+ROOT=$(pwd)
 OUT=gpurun_out/ev_$TAG
 mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread > $OUT/gpu_tests.log 2>&1
@@ -20,6 +21,9 @@ timeout -k 10 300 python bench.py --algo per --cpu-seconds 0 > $OUT/bench_per.js
 timeout -k 10 300 python bench.py --algo mgsc --cpu-seconds 0 > $OUT/bench_mgsc.json 2> $OUT/bench_mgsc.err
 timeout -k 10 300 python bench.py --algo agent --steps 2000 --warmup 50 > $OUT/bench_agent.json 2> $OUT/bench_agent.err
 bash tools/bench_median.sh $OUT/median > $OUT/bench_median5.json
+timeout -k 10 300 python tools/meta_bench.py --steps 100 > $OUT/meta_bench.json 2> $OUT/meta_bench.err
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/metaprof -o run -- \
+  python3 $ROOT/tools/meta_bench.py --steps 50 --graph 0 > $ROOT/$OUT/meta_prof.json 2> $ROOT/$OUT/meta_prof.err)
 bash profiles/run_profile.sh ${TAG}_dqn
 bash profiles/run_pmc.sh $TAG
 DQZ_TRACE_PREBUILT=1 timeout -k 10 200 python -u tools/trace_step.py > $OUT/trace_step.txt 2>&1
