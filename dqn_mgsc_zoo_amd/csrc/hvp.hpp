@@ -88,8 +88,16 @@ __global__ __launch_bounds__(256) void hvp_t1_kernel(HvpArgs a) {
   __shared__ float s_w[4];
   const int t = threadIdx.x;
   if (blockIdx.x == C1M) {
+    // eight loads in flight per round (one round trip per 2,048 partials)
     float v = 0.f;
-    for (int j = t; j < a.s1_nparts; j += 256) v += a.s1_part[j];
+    for (int j0 = t; j0 < a.s1_nparts; j0 += 8 * 256) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = a.s1_part[min(j0 + 256 * u, a.s1_nparts - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + 256 * u < a.s1_nparts) v += x[u];
+    }
     v = block_sum256(v, s_w);
     if (t == 0) a.s1[0] = v;
     return;
@@ -128,8 +136,16 @@ __global__ __launch_bounds__(256) void hvp_t2_kernel(HvpArgs a) {
   const int src = ((oh * C2S + kh) * C1O + ow * C2S + kw) * C1CO;
   const float *W = a.th + a.off[2] + tap * C2CI * C2CO + co, *Wd = a.tw + a.off[2] + tap * C2CI * C2CO + co;
   float z = 0.f;
-#pragma unroll 8
-  for (int ci = 0; ci < C2CI; ++ci) z += a.y1[src + ci] * Wd[ci * C2CO] + a.ty1[src + ci] * W[ci * C2CO];
+  float y[C2CI], ty[C2CI], w[C2CI], wd[C2CI];  // every load before the first product
+#pragma unroll
+  for (int ci = 0; ci < C2CI; ++ci) {
+    y[ci] = a.y1[src + ci];
+    ty[ci] = a.ty1[src + ci];
+    wd[ci] = Wd[ci * C2CO];
+    w[ci] = W[ci * C2CO];
+  }
+#pragma unroll
+  for (int ci = 0; ci < C2CI; ++ci) z += y[ci] * wd[ci] + ty[ci] * w[ci];
   s_r[tap][t & 15] = z;
   __syncthreads();
   if (t < 16) {
@@ -225,21 +241,27 @@ __global__ __launch_bounds__(256) void hvp_b2_kernel(HvpArgs a) {
   __shared__ float s_r[16][17];
   const int t = threadIdx.x, pix = blockIdx.x, g = blockIdx.y;
   const int ih = pix / C2O, iw = pix % C2O, cs = t & 15, cl = t >> 4, ci = 16 * g + cl;
+  // the nine taps' operands loaded together (taps outside the output are
+  // clamped to a valid position and skipped in the sum, in tap order)
+  float4 w[9], wd[9], d[9], dd[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int kh = tap / 3, kw = tap % 3;
+    const int oh = min(max(ih - kh, 0), C3O - 1), ow = min(max(iw - kw, 0), C3O - 1);
+    const int src = (oh * C3O + ow) * C3CO + 4 * cs;
+    const int64_t wi = ((kh * C3K + kw) * C3CI + ci) * C3CO + 4 * cs;
+    w[tap] = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
+    wd[tap] = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
+    d[tap] = *reinterpret_cast<const float4*>(a.d3 + src);
+    dd[tap] = *reinterpret_cast<const float4*>(a.td3 + src);
+  }
   float z = 0.f;
-  for (int kh = 0; kh < C3K; ++kh) {
-    const int oh = ih - kh;
-    if (oh < 0 || oh >= C3O) continue;
-    for (int kw = 0; kw < C3K; ++kw) {
-      const int ow = iw - kw;
-      if (ow < 0 || ow >= C3O) continue;
-      const int src = (oh * C3O + ow) * C3CO + 4 * cs;
-      const int64_t wi = ((kh * C3K + kw) * C3CI + ci) * C3CO + 4 * cs;
-      const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
-      const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
-      const float4 d = *reinterpret_cast<const float4*>(a.d3 + src);
-      const float4 dd = *reinterpret_cast<const float4*>(a.td3 + src);
-      z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) + ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
-    }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int oh = ih - tap / 3, ow = iw - tap % 3;
+    if (oh < 0 || oh >= C3O || ow < 0 || ow >= C3O) continue;
+    z += ((d[tap].x * wd[tap].x + dd[tap].x * w[tap].x) + (d[tap].y * wd[tap].y + dd[tap].y * w[tap].y)) +
+         ((d[tap].z * wd[tap].z + dd[tap].z * w[tap].z) + (d[tap].w * wd[tap].w + dd[tap].w * w[tap].w));
   }
   s_r[cl][cs] = z;
   __syncthreads();
@@ -259,25 +281,32 @@ __global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
   __shared__ float s_r[C2CI][9];
   const int t = threadIdx.x, pix = blockIdx.x;
   const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
-  float z = 0.f;
-  for (int kh = (ih & 1); kh < C2K; kh += C2S) {
-    const int oh = (ih - kh) / C2S;
-    if (ih < kh || oh >= C2O) continue;
-    for (int kw = (iw & 1); kw < C2K; kw += C2S) {
-      const int ow = (iw - kw) / C2S;
-      if (iw < kw || ow >= C2O) continue;
-      const int src = (oh * C2O + ow) * C2CO + 8 * cs;
-      const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
+  // the 2 x 2 taps of this pixel's stride phase, every operand loaded before
+  // the first product (taps outside the output clamped and skipped, in order)
+  float4 w[4][2], wd[4][2], d[4][2], dd[4][2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float4 w = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
-        const float4 wd = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
-        const float4 d = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
-        const float4 dd = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
-        z += ((d.x * wd.x + dd.x * w.x) + (d.y * wd.y + dd.y * w.y)) +
-             ((d.z * wd.z + dd.z * w.z) + (d.w * wd.w + dd.w * w.w));
-      }
+  for (int q = 0; q < 4; ++q) {
+    const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
+    const int oh = min(max((ih - kh) / C2S, 0), C2O - 1), ow = min(max((iw - kw) / C2S, 0), C2O - 1);
+    const int src = (oh * C2O + ow) * C2CO + 8 * cs;
+    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      w[q][h] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
+      wd[q][h] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
+      d[q][h] = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
+      dd[q][h] = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
     }
+  }
+  float z = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
+    if (ih < kh || (ih - kh) / C2S >= C2O || iw < kw || (iw - kw) / C2S >= C2O) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      z += ((d[q][h].x * wd[q][h].x + dd[q][h].x * w[q][h].x) + (d[q][h].y * wd[q][h].y + dd[q][h].y * w[q][h].y)) +
+           ((d[q][h].z * wd[q][h].z + dd[q][h].z * w[q][h].z) + (d[q][h].w * wd[q][h].w + dd[q][h].w * w[q][h].w));
   }
   s_r[ci][cs] = z;
   __syncthreads();
@@ -295,10 +324,14 @@ __global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
 //   [513] conv2 rows, [577] conv3 rows (last row = bias):
 //         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
 //         splits (thread (split, co));
-//   [2]   fc2 / fc1 bias / fc2 bias: hdot = relu'(h) (bdot1 + sum of t4's
-//         chunk partials), the fc2 column a = hdot;
+//   [8]   fc2 / fc1 bias / fc2 bias: hdot = relu'(h) (bdot1 + sum of t4's
+//         chunk partials), the fc2 column a = hdot; 64 hidden units per
+//         block, the 196 chunk partials of each in 4 groups of 49 loads;
 //   [...] fc1: ydot3 (x) d4 + y3 (x) ddot4, 4 elements per thread.
-constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = 2;
+// Every per-thread sum issues all its loads before the first addition
+// (round 5: the position and chunk loops waited for one round trip per
+// iteration, 13-21 serial trips, and kept this launch at 12.2 us).
+constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = HID / 64;
 constexpr int HVP_G_FC = FLAT * HID / 4 / 256;  // 1568
 constexpr int HVP_G_BLOCKS = HVP_G_C1 + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC;
 
@@ -308,16 +341,30 @@ __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y,
                                                const HqOut& ho) {
   const int t = threadIdx.x, co = t & 63, sp = t >> 6;  // 4 position splits
   constexpr int P = OH * OH, PS = (P + 3) / 4;
-  const int p0 = sp * PS, p1 = min(P, p0 + PS);
+  const int p0 = sp * PS;
   float g = 0.f;
   if (k == K * K * CI) {
-    for (int p = p0; p < p1; ++p) g += dd[p * CO + co];
+    float v[PS];
+#pragma unroll
+    for (int j = 0; j < PS; ++j) v[j] = dd[min(p0 + j, P - 1) * CO + co];
+#pragma unroll
+    for (int j = 0; j < PS; ++j)
+      if (p0 + j < P) g += v[j];
   } else {
     const int kh = k / (K * CI), kw = (k / CI) % K, ci = k % CI;
-    for (int p = p0; p < p1; ++p) {
+    float u0[PS], u1[PS], w0[PS], w1[PS];
+#pragma unroll
+    for (int j = 0; j < PS; ++j) {
+      const int p = min(p0 + j, P - 1);
       const int src = (((p / OH) * S + kh) * IH + (p % OH) * S + kw) * CI + ci;
-      g += yd[src] * d[p * CO + co] + y[src] * dd[p * CO + co];
+      u0[j] = yd[src];
+      u1[j] = d[p * CO + co];
+      w0[j] = y[src];
+      w1[j] = dd[p * CO + co];
     }
+#pragma unroll
+    for (int j = 0; j < PS; ++j)
+      if (p0 + j < P) g += u0[j] * u1[j] + w0[j] * w1[j];
   }
   s_r[sp][co] = g;
   __syncthreads();
@@ -340,6 +387,9 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
     // the row's 400 patch values x_p[k] staged once (a loop of scattered
     // byte loads per thread was 11 of this launch's 20 us)
     const int k = i, co = t & 31, sp = t >> 5;
+    float tv[50];  // this thread's ddot1 column, loaded before the staging
+#pragma unroll
+    for (int j = 0; j < 50; ++j) tv[j] = a.td1[(50 * sp + j) * C1CO + co];
     if (k < C1KK) {
       const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
       const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
@@ -351,8 +401,8 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
     }
     __syncthreads();
     float g = 0.f;
-#pragma unroll 10
-    for (int p = 50 * sp; p < 50 * sp + 50; ++p) g += s_x[p] * a.td1[p * C1CO + co];
+#pragma unroll
+    for (int j = 0; j < 50; ++j) g += s_x[50 * sp + j] * tv[j];
     s_r[sp][co] = g;
     __syncthreads();
     if (t < C1CO) {
@@ -375,9 +425,22 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
   }
   i -= HVP_G_C3;
   if (i < HVP_G_H) {  // hidden unit n: hdot, fc2 column, fc1 bias; fc2 bias = 0
-    const int n = 256 * i + t, act = a.action[a.slot[0]];
-    float z = a.tw[a.off[7] + n];
-    for (int c = 0; c < HVP_T4_CHUNKS; ++c) z += a.part[(int64_t)c * HID + n];
+    // thread (group q, unit n): chunks [49 q, +49) of unit n, summed in
+    // chunk order, then the four group sums in group order
+    constexpr int NG = 4, CG = HVP_T4_CHUNKS / NG;  // 49
+    static_assert(NG * CG == HVP_T4_CHUNKS, "chunk groups");
+    const int nl = t & 63, q = t >> 6, n = 64 * i + nl;
+    float pv[CG];
+#pragma unroll
+    for (int c = 0; c < CG; ++c) pv[c] = a.part[(int64_t)(CG * q + c) * HID + n];
+    float zq = 0.f;
+#pragma unroll
+    for (int c = 0; c < CG; ++c) zq += pv[c];
+    s_r[q][nl] = zq;
+    __syncthreads();
+    if (q != 0) return;
+    const int act = a.action[a.slot[0]];
+    const float z = a.tw[a.off[7] + n] + ((s_r[0][nl] + s_r[1][nl]) + (s_r[2][nl] + s_r[3][nl]));
     const float hd = a.h[n] > 0.f ? z : 0.f;
     for (int col = 0; col < a.A; ++col) ho.put(a, a.off[8] + (int64_t)n * a.A + col, col == act ? hd : 0.f);
     ho.put(a, a.off[7] + n, a.td4[n]);
