@@ -756,37 +756,42 @@ __device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, i
 }
 
 // ---- B = 1: the head and fc1 dX in one launch (head_dx1_kernel) ----------
-// With one sample (the MGSC meta-update's pass at theta') dz1 is 2 KB, so the
-// fc1 dX blocks can wait for it inside the head's launch: block 0 runs the
-// head (dz1 stored write-through, one arrival), blocks 1.. each own 32 W1
-// rows (two 256-thread halves of 16 rows), load them before the wait, then
-// read dz1 with sc1 loads and form dy3 = relu'(y3) (W1 dz1) as VALU dot
-// products (a one-row GEMV: 16 lanes per row, 32 columns per lane, in
-// column order, then a 16-lane sum).  They also write the dX-ordered W3 / W2
-// copies, as fc1_dx_kernel does.  Saves the head -> fc1 dX boundary and the
-// fc1 dX load phase (they overlap the head).
+// With one sample (the MGSC meta-update's pass at theta', the HVP's
+// unit-cotangent pass) every block of the fc1 dX launch runs the head itself
+// (2 x 7 split-K rows of 512, fc2, the TD error: a few microseconds of
+// latency, no throughput) and takes dz1 from its own LDS; block 0 alone
+// stores the head's outputs.  Each block owns 32 W1 rows (two 256-thread
+// halves of 16 rows), loaded before the head, and forms dy3 = relu'(y3)
+// (W1 dz1) as VALU dot products (a one-row GEMV: 16 lanes per row, 32
+// columns per lane in column order, then a 16-lane sum); it also writes its
+// share of the dX-ordered W3 / W2 copies, as fc1_dx_kernel does.  (Round 5's
+// first form ran the head in block 0 and handed dz1 to the other blocks
+// in-launch: 9.0 us; the head's round trips and the hand-off were serial.)
 constexpr int FC1X1_ROWS = 32;
 constexpr int FC1X1_BLOCKS = FLAT / FC1X1_ROWS;  // 98
-__device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, int row0, int t, const Handoff& hw) {
+
+template <int AMAX, int SMAX, int ZMAX>
+__global__ __launch_bounds__(512) void head_dx1_kernel(HeadArgs h, Fc1BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_dz[HID];
   DQZ_STAMP(5, 0);
+  const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int row0 = FC1X1_ROWS * blockIdx.x + 16 * half;
   const int r = row0 + (t >> 4), c0 = 32 * (t & 15);
   const float* W1 = a.th + a.w_off;
   float4 wv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)r * HID + c0 + 4 * j);
   const float ym = a.y3[r];  // relu'(y3) of the one sample
-  // W3 / W2 dX copies: element g of the 69,632 by thread g of the fc1 dX range
+  // W3 / W2 dX copies: element g of the 69,632 by thread g of the launch
   const int g = (row0 / 16) * 256 + t;
   float v3 = 0.f, v2 = 0.f;
   if (a.w3p) {
     if (g < W3P_N) v3 = a.w3[w3p_src(g)];
     if (g < W2P_N) v2 = a.w2[w2p_src(g)];
   }
-  hw.wait(0);
-  DQZ_STAMP(5, 1);
-  if (threadIdx.x < HID / 4)
-    reinterpret_cast<float4*>(s_dz)[threadIdx.x] = load_sc1_f4(reinterpret_cast<const float4*>(a.dz1), HID * 4, threadIdx.x);
+  head_body<AMAX, SMAX, ZMAX>(h, 0, blockIdx.x == 0, s_dz);
   __syncthreads();
+  DQZ_STAMP(5, 1);
   float d = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -809,21 +814,10 @@ __device__ __forceinline__ void fc1_dx1_rows(const Fc1BwdArgs& a, float* s_dz, i
   DQZ_STAMP(5, 3);
 }
 
-template <int AMAX, int SMAX, int ZMAX>
-__global__ __launch_bounds__(512) void head_dx1_kernel(HeadArgs h, Fc1BwdArgs f) {
-  __shared__ __attribute__((aligned(16))) float s_dz[HID];
-  if (blockIdx.x == 0) {
-    head_body<AMAX, SMAX, ZMAX>(h, 0);
-    return;
-  }
-  const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
-  fc1_dx1_rows(f, s_dz, FC1X1_ROWS * (blockIdx.x - 1) + 16 * half, t, h.dz1_pub);
-}
-
 // head_dx1_kernel's launch: the head_kernel template choice (launch_head)
 inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStream_t st) {
   if (h.S > 7 || h.Z < 1 || h.Z > 3 || h.B != 1) return hipErrorInvalidValue;
-  const dim3 grid(1 + FC1X1_BLOCKS), block(512);
+  const dim3 grid(FC1X1_BLOCKS), block(512);
   if (h.A <= 8) {
     if (h.Z <= 2)
       hipLaunchKernelGGL((head_dx1_kernel<8, 7, 2>), grid, block, 0, st, h, f);

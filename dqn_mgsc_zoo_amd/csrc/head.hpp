@@ -42,10 +42,6 @@ struct HeadArgs {
   float* gq;             // [B] d loss / d q_tm1[b, a_b]
   int32_t* ga;           // [B] a_b
   float* dz1;            // [B][512] d loss / d fc1 pre-activation (online)
-  // B = 1 fused with fc1 dX (head_dx1_kernel): dz1 stored write-through and
-  // published on dz1_pub (zero-initialised: off)
-  int dz1_wt;
-  Handoff dz1_pub;
   // actor mode (fwd_only): eps-greedy draw per sample into act_out (or null)
   dqz_action* act_out;
   double eps;
@@ -110,8 +106,10 @@ __device__ __forceinline__ double wave_max_nonneg(double m) {
 // ZMAX: network copies this instantiation handles (2: online + target, or
 // one copy; 3: double-Q's online(s_t) too), so no load is issued for a copy
 // the launch does not have.
+// out = false (head_dx1_kernel's blocks past the first): the same arithmetic
+// with no global store; s_dzo (or null) receives the block's dz1 row.
 template <int AMAX, int SMAX, int ZMAX>
-__device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
+__device__ __forceinline__ void head_body(const HeadArgs& h, int b, bool out = true, float* s_dzo = nullptr) {
   DQZ_STAMP(4, 0);
   __shared__ float s_red[8][3 * AMAX];
   __shared__ float s_q[3][AMAX];
@@ -176,7 +174,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     if (lane == 0) {
       const double wb = h.per_wb[b];
       wper = (float)(h.per_normalize ? wb / m : wb);
-      if (h.per_w_out) h.per_w_out[b] = wper;
+      if (out && h.per_w_out) h.per_w_out[b] = wper;
     }
   }
   if (h.meta_logits) {
@@ -206,8 +204,10 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     if (n == b) {
       const float pb = expf(x - (c + logf(se)));
       s_pm = pb;
-      h.meta_x_out[b] = x;
-      h.meta_p_out[b] = pb;
+      if (out) {
+        h.meta_x_out[b] = x;
+        h.meta_p_out[b] = pb;
+      }
     }
     __syncthreads();
     pm = s_pm;
@@ -337,7 +337,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
         g = w * td / (float)B;  // d mean(l2(td) * w) / d td
         g = fminf(fmaxf(g, -h.bound), h.bound);
       }
-      if (n == 0) {
+      if (out && n == 0) {
         h.td[b] = td;
         h.loss_part[b] = 0.5f * td * td * w;
         h.gq[b] = -g;
@@ -348,14 +348,12 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
       for (int a = 1; a < AMAX; ++a) wv = a == a_tm1 ? w2v[0][a] : wv;
       DQZ_STAMP(4, 2);
       const float dz = hz[0] > 0.f ? -g * wv : 0.f;
-      if (h.dz1_wt)
-        store_sc1_f1(h.dz1, B * HID * 4, b * HID + n, dz);
-      else
-        h.dz1[(int64_t)b * HID + n] = dz;
+      if (s_dzo) s_dzo[n] = dz;
+      if (out) h.dz1[(int64_t)b * HID + n] = dz;
     }
   } else if (h.act_out) {  // actor: eps-greedy draw b of call act_ctr
     __syncthreads();
-    if (n == 0) {
+    if (out && n == 0) {
       const uint4 r = philox4x32(make_uint4((unsigned)h.act_ctr, (unsigned)(h.act_ctr >> 32), (unsigned)b, 0xAC7u),
                                  make_uint2((unsigned)h.act_seed, (unsigned)(h.act_seed >> 32)));
       const double u = ((((uint64_t)r.x << 32) | r.y) >> 11) * 0x1.0p-53;
@@ -363,6 +361,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
     }
   }
   // deferred outputs: fc1 activations (fc2 dW in the update kernel), q values
+  if (!out) return;
 #pragma unroll
   for (int z = 0; z < ZMAX; ++z)
     if (z < Z) h.h1[((int64_t)z * B + b) * HID + n] = hz[z];
@@ -370,7 +369,6 @@ __device__ __forceinline__ void head_body(const HeadArgs& h, int b) {
   // the fused sampler's step counter: every conv1 block of this step has read it
   if (h.advance && b == 0 && n == 0)
     __hip_atomic_fetch_add(h.advance, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (h.dz1_wt) h.dz1_pub.arrive(b);
   DQZ_STAMP(4, 3);
 }
 

@@ -392,10 +392,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w2p = L->w2p;
   if (B == 1 && !pe.on() && kHeadDx1) {
     // one sample (the MGSC pass at theta', the HVP's unit-cotangent pass):
-    // the head and fc1 dX in one launch, dz1 handed over in-launch
-    h.dz1_wt = 1;
-    h.dz1_pub = Handoff{L->sync + (16 * B + 1) * Handoff::kStride, L->sync + (16 * B + 2) * Handoff::kStride,
-                        L->sync + 16 * B * Handoff::kStride, 1, FC1X1_BLOCKS, L->spin_max};
+    // the head and fc1 dX in one launch, every block forming the head itself
     DQZ_HIP(launch_head_dx1(h, fb, st));
   } else {
     DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));

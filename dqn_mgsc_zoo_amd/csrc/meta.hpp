@@ -574,18 +574,11 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   const int k = blockIdx.x, t = threadIdx.x;
   const bool own = t < a.M;
   const int i0 = own ? t : 0;
+  // Every load is issued before the block learns whether it is active (the
+  // positions are loaded with the rest): one round trip instead of two, for
+  // the inactive blocks' wasted loads (L2 hits but for their own chunk)
   const int32_t pos0 = a.pos[i0];
-  const int lead = a.pos[0] / SM_CHUNK;
-  if (t == 0) {
-    s_act = 0;
-    s_far = 0;
-  }
-  __syncthreads();
-  const bool mine = own && pos0 / SM_CHUNK == k;
-  if (mine) s_act = 1;
-  __syncthreads();
-  const bool leader = k == lead;
-  if (!s_act) return;  // (the leader's chunk holds pos[0])
+  const int32_t posl = a.pos[0];
   // this chunk's logits (before the writes) into LDS, under the Adam loads
   float4 cv[SM_PER_LANE / 4];
   {
@@ -609,14 +602,22 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
     for (int u = 0; u < META_DOT_SLOTS / 4; ++u) dr[u] = q[u];
   }
   float lpv[META_ADAM_LP];
-  if (leader) {
 #pragma unroll
-    for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
-  }
+  for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
   const float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
   const int32_t cnt = *a.count + 1;
   LogitRun r = *a.run;
   __builtin_amdgcn_sched_barrier(0);
+  if (t == 0) {
+    s_act = 0;
+    s_far = 0;
+  }
+  __syncthreads();
+  const bool mine = own && pos0 / SM_CHUNK == k;
+  if (mine) s_act = 1;
+  __syncthreads();
+  const bool leader = k == posl / SM_CHUNK;
+  if (!s_act) return;  // (the leader's chunk holds pos[0])
 #pragma unroll
   for (int q = 0; q < SM_PER_LANE / 4; ++q) *reinterpret_cast<float4*>(s_chunk + t * SM_PER_LANE + 4 * q) = cv[q];
   const float s0 = meta_s_row(dr);
