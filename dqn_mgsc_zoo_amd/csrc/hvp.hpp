@@ -103,19 +103,21 @@ __global__ __launch_bounds__(256) void hvp_t1_kernel(HvpArgs a) {
     return;
   }
   const int p = blockIdx.x, oh = p / C1O, ow = p % C1O;
+  const int kh = t >> 5, co = t & 31;
+  // the thread's 32 weights first: they are in flight under the patch's
+  // slot -> frame-index -> frame chain
+  const float* W = a.tw + a.off[0];
+  float wv[C1K * FC];
+#pragma unroll
+  for (int j = 0; j < C1K * FC; ++j) wv[j] = W[(kh * C1K * FC + j) * C1CO + co];
   {
-    const int kh = t >> 5, kw = (t >> 2) & 7, ci = t & 3;
+    const int kw = (t >> 2) & 7, ci = t & 3;
     s_x[t] = hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci);
   }
   __syncthreads();
-  const int kh = t >> 5, co = t & 31;
-  const float* W = a.tw + a.off[0];
   float z = 0.f;
 #pragma unroll
-  for (int j = 0; j < C1K * FC; ++j) {
-    const int k = kh * C1K * FC + j;  // (kh, kw = j / 4, ci = j % 4)
-    z += s_x[k] * W[k * C1CO + co];
-  }
+  for (int j = 0; j < C1K * FC; ++j) z += s_x[kh * C1K * FC + j] * wv[j];  // (kh, kw = j / 4, ci = j % 4)
   s_r[kh][co] = z;
   __syncthreads();
   if (t < C1CO) {
