@@ -868,6 +868,12 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // boundary saved (16,210 against 16,244 steps/s; first-order meta-update
 // 193 -> 201 us; profiles/r05/s13).  With a thousand update blocks polling
 // three shared words the launch ran 1.3x slower (s10-s12).  Removed.)
+// (Round 5, also removed: the dX chain on XCDs 0..L-1 and the dW sets on the
+// other XCDs.  With L = 4 the chain ended 0.5 us sooner, but the dW side
+// became the tail (+2.8 us) and the boundary after the launch grew 2.8 ->
+// 5.8 us, the written lines now dirty in half the L2s: 15,873-15,901
+// against 16,137-16,223 steps/s; L = 3 / 5 / 6 15,210 / 14,750 / 13,200;
+// profiles/r05/split.)
 // A/B: the fc1 dW range last in the grid (after conv2 dW) instead of second
 #ifndef DQZ_BWD_FC1_LAST
 #define DQZ_BWD_FC1_LAST 0
