@@ -879,35 +879,6 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 #define DQZ_BWD_FC1_LAST 0
 #endif
 constexpr bool kBwdFc1Last = DQZ_BWD_FC1_LAST != 0;
-// XCD split (DQZ_BWD_SPLIT = L, 1..7; 0 = the interleaved ranges above): the
-// dX chain (conv3 dX -> conv2 dX -> conv1 dW) runs on XCDs 0 .. L-1 and the
-// chain-independent dW sets (fc1 dW + RMSProp, conv3 dW, conv2 dW) on XCDs
-// L .. 7, so the chain's MFMA phases and hand-offs no longer share CUs, L2s
-// and memory queues with the dW traffic (workgroup i runs on XCD i % 8).
-// Within each lane group a sample's jobs stay on one XCD (s % L); conv2 dW
-// takes dy2 across XCDs (its loads are sc1 anyway).
-#ifndef DQZ_BWD_SPLIT
-#define DQZ_BWD_SPLIT 0
-#endif
-constexpr int kBwdSplit = DQZ_BWD_SPLIT;
-static_assert(kBwdSplit >= 0 && kBwdSplit < 8, "DQZ_BWD_SPLIT: chain XCDs 1..7, or 0");
-__host__ __device__ inline int bwd_split_rows(int B) {
-  const int L = kBwdSplit > 0 ? kBwdSplit : 1, LW = 8 - L;
-  const int BL = (B + L - 1) / L * L, BW = (B + LW - 1) / LW * LW;
-  const int rc = (24 * BL + L - 1) / L, rw = (4 * (FLAT / 16) + 12 * BW + LW - 1) / LW;
-  return rc > rw ? rc : rw;
-}
-// Grid of bwd_bc_kernel (without the PER write-back's 8 leading blocks).
-__host__ __device__ inline int bwd_grid(int B) {
-  const int B8 = (B + 7) / 8 * 8;
-  return kBwdSplit > 0 ? 8 * bwd_split_rows(B) : 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
-}
-// job j of lane group member c (L lanes): sample L (slot / J) + c % L
-__device__ __forceinline__ SampleJob lane_sample_job(int c, int L, int J, int nsamp) {
-  const int x = c % L, slot = c / L;
-  const int s = L * (slot / J) + x;
-  return SampleJob{s, slot % J, s < nsamp};
-}
 template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
@@ -927,63 +898,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       return;
     }
     i -= 8;
-  }
-  if constexpr (kBwdSplit > 0) {
-    constexpr int L = kBwdSplit, LW = 8 - L;
-    const int x = i & 7, row = i >> 3, B = c3.B;
-    if (x < L) {  // the dX chain
-      const int BL = (B + L - 1) / L * L;
-      int c = row * L + x;
-      if (c < 8 * BL) {
-        const SampleJob sj = lane_sample_job(c, L, 8, B);
-        if (!sj.valid) return;
-        DQZ_STAMP(6, 0);
-        conv3_bwd_dx<true>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
-        DQZ_STAMP(6, 3);
-        return;
-      }
-      c -= 8 * BL;
-      if (c < 8 * BL) {
-        const SampleJob sj = lane_sample_job(c, L, 8, B);
-        if (!sj.valid) return;
-        DQZ_STAMP(7, 0);
-        conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-        DQZ_STAMP(7, 3);
-        return;
-      }
-      c -= 8 * BL;
-      if (c < 8 * BL) {
-        const SampleJob sj = lane_sample_job(c, L, 8, B);
-        if (!sj.valid) return;
-        conv1_dw_half(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
-      }
-      return;
-    }
-    // the dW sets
-    const int BW = (B + LW - 1) / LW * LW;
-    int w = row * LW + (x - L);
-    if (w < NF) {
-      fc1_dw_body(f1, smem, w);
-      return;
-    }
-    w -= NF;
-    if (w < 4 * BW) {
-      const SampleJob sj = lane_sample_job(w, LW, 4, B);
-      if (!sj.valid) return;
-      DQZ_STAMP(12, 0);
-      conv3_bwd_dw(c3, smem, sj.s, sj.job);
-      DQZ_STAMP(12, 3);
-      return;
-    }
-    w -= 4 * BW;
-    if (w < 8 * BW) {
-      const SampleJob sj = lane_sample_job(w, LW, 8, B);
-      if (!sj.valid) return;
-      DQZ_STAMP(13, 0);
-      conv2_bwd_dw_split(c2, smem, sj.s, sj.job >> 1, sj.job & 1);
-      DQZ_STAMP(13, 3);
-    }
-    return;
   }
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
