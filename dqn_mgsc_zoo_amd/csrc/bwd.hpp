@@ -874,11 +874,6 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // 5.8 us, the written lines now dirty in half the L2s: 15,873-15,901
 // against 16,137-16,223 steps/s; L = 3 / 5 / 6 15,210 / 14,750 / 13,200;
 // profiles/r05/split.)
-// A/B: the fc1 dW range last in the grid (after conv2 dW) instead of second
-#ifndef DQZ_BWD_FC1_LAST
-#define DQZ_BWD_FC1_LAST 0
-#endif
-constexpr bool kBwdFc1Last = DQZ_BWD_FC1_LAST != 0;
 template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
@@ -908,14 +903,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  if (!kBwdFc1Last) {
-    if (i < NF) {
-      if (DQZ_EXP_SKIP & 1) return;
-      fc1_dw_body(f1, smem, i);
-      return;
-    }
-    i -= NF;
+  if (i < NF) {
+    if (DQZ_EXP_SKIP & 1) return;
+    fc1_dw_body(f1, smem, i);
+    return;
   }
+  i -= NF;
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
@@ -949,12 +942,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= 8 * B8;
-  if (kBwdFc1Last && i >= 8 * B8) {
-    i -= 8 * B8;
-    if (DQZ_EXP_SKIP & 1) return;
-    fc1_dw_body(f1, smem, i);
-    return;
-  }
   const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
   if (!sj.valid) return;
   if (DQZ_EXP_SKIP & 4) {

@@ -71,10 +71,7 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 // c + 8 of a pixel hit the same banks (4c = 4 (c + 8) mod 32): a 2-way
 // conflict in every access.  The MFMA reads add the same constant per wave
 // (a wave's 16 channels lie in one half), so their bank pattern is unchanged.
-#ifndef DQZ_WIN_HALF_SHIFT
-#define DQZ_WIN_HALF_SHIFT 1
-#endif
-__device__ __forceinline__ int win64_ch(int ch) { return DQZ_WIN_HALF_SHIFT ? ch + 2 * (ch >> 5) : ch; }
+__device__ __forceinline__ int win64_ch(int ch) { return ch + 2 * (ch >> 5); }
 // networks.py:192: x.astype(jnp.float32) / 255.0 (IEEE division, not a reciprocal multiply)
 // x / 255.0f correctly rounded (networks.py:192) without the IEEE division
 // sequence: q = x * (1/255) plus one FMA residual correction.  Checked in

@@ -45,11 +45,7 @@ __device__ __forceinline__ int red_idx(int row, int col) { return row * 16 + 16 
 // starts are 0, 16, 32, 48 mod 64: lane quad q of the wave's 16 takes row
 // 16 (i / 64) + kEpiPerm[q].  Every row of [0, 16 ceil(rows / 16)) is visited
 // once, so loops run i over that range and skip rows past the end.
-#ifndef DQZ_EPI_PERM
-#define DQZ_EPI_PERM 1
-#endif
 __device__ __forceinline__ int epi_row(int i) {
-  if (!DQZ_EPI_PERM) return i >> 2;
   return ((i >> 6) << 4) + (int)((0xFBAE9DC873261540ull >> (4 * ((i >> 2) & 15))) & 15);
 }
 constexpr int epi_range(int rows) { return (rows + 15) / 16 * 64; }
@@ -553,10 +549,7 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 // fc1 forward's load order: every W1 load issued before the y3 loads (round
 // 3's order; round 4's interleaved order made the kernel 0.2-0.3 us slower,
 // fc1 4.90-4.96 -> 4.69-4.75 us back to back and 16,171 -> 16,248 steps/s,
-// three interleaved rounds, profiles/r05/c2).  0 keeps the interleaved order.
-#ifndef DQZ_FC1_LOADS_W_FIRST
-#define DQZ_FC1_LOADS_W_FIRST 1
-#endif
+// three interleaved rounds, profiles/r05/c2).
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
 // (Round 5: 8 waves per block, 56 k each, measured 4.70 -> 4.86 us and
@@ -576,21 +569,12 @@ __device__ __forceinline__ void fc1_fwd_block32(const Fc1FwdArgs& a, float* s_re
   const float* x = a.in + ((int64_t)z * a.B + row) * FLAT + k0;
   float wr[G][4];
   float4 av[G];
-#if DQZ_FC1_LOADS_W_FIRST
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
 #pragma unroll
   for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
-#else
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    av[g] = *reinterpret_cast<const float4*>(x + 8 * g);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) wr[g][e] = W[(int64_t)(k0 + 8 * g + e) * HID];
-  }
-#endif
   f32x16 acc = {};
 #pragma unroll
   for (int g = 0; g < G; ++g) {

@@ -484,14 +484,10 @@ __device__ __forceinline__ float2 sum_split2_r(const float* p, int S, int64_t st
   return make_float2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
                      ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
 }
-#ifndef DQZ_UPD_BATCH
-#define DQZ_UPD_BATCH 1
-#endif
 // (Wider forms, up to 56 loads per lane for the M = 100 meta batch's 400
 // conv1 slabs, cost that kernel 0.5 us: 162 VGPRs left its 1,276 blocks no
 // longer all resident; profiles/r05/c7.)
 __device__ __forceinline__ float2 sum_slabs(const float* p, int S, int64_t stride, int64_t j, int g) {
-  if (!DQZ_UPD_BATCH) return sum_split2(p, S, stride, j, g);
   if (S <= 8 * UPD_GROUPS) return sum_split2_r<1>(p, S, stride, j, g);
   if (S <= 16 * UPD_GROUPS) return sum_split2_r<2>(p, S, stride, j, g);
   return sum_split2(p, S, stride, j, g);

@@ -65,12 +65,6 @@ struct dqz_learner {
   void* block;
 };
 
-// B = 1 learner steps run the head and fc1 dX as one launch (head_dx1_kernel);
-// -DDQZ_HEAD_DX1=0 keeps the two launches (A/B).
-#ifndef DQZ_HEAD_DX1
-#define DQZ_HEAD_DX1 1
-#endif
-constexpr bool kHeadDx1 = DQZ_HEAD_DX1 != 0;
 
 static int g_attr_done = 0;
 
@@ -390,7 +384,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   fb.w2 = P->online + L->off[2];
   fb.w3p = L->w3p;
   fb.w2p = L->w2p;
-  if (B == 1 && !pe.on() && kHeadDx1) {
+  if (B == 1 && !pe.on()) {
     // one sample (the MGSC pass at theta', the HVP's unit-cotangent pass):
     // the head and fc1 dX in one launch, every block forming the head itself
     DQZ_HIP(launch_head_dx1(h, fb, st));
@@ -1098,19 +1092,6 @@ int dqz_target_copy(float* target, const float* online, int64_t total, void* str
 // ---------------------------------------------------------------------------
 // MGSC meta-update (meta.hpp)
 
-// The meta-update's tangent conv part as dot products with the per-sample
-// gradient slabs (tangent_slab_kernel, default) or as the linear conv forward
-// with dot-product epilogues (tangent_fwd_kernel, -DDQZ_META_SLAB=0 for A/B).
-#ifndef DQZ_META_SLAB
-#define DQZ_META_SLAB 1
-#endif
-constexpr bool kMetaSlabDots = DQZ_META_SLAB != 0;
-// Meta Adam fused with the chunk re-sums of the logits it writes
-// (meta_adam_chunks_kernel, default) or the two launches (-DDQZ_META_ADAM_CHUNKS=0).
-#ifndef DQZ_META_ADAM_CHUNKS
-#define DQZ_META_ADAM_CHUNKS 1
-#endif
-constexpr bool kMetaAdamChunks = DQZ_META_ADAM_CHUNKS != 0;
 
 struct dqz_meta {
   dqz_meta_config cfg;
@@ -1421,7 +1402,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
       f1.dot = TangentDot{L->dz1, H->dotp, 12};
       ex = MetaExtra{L->dz1, L->h1, L->gq, L->ga, v, L->off[7], L->off[8], L->off[9], A, H->dotp};
     }
-    if (K == 1 && kMetaSlabDots) {
+    if (K == 1) {
       // the conv layers' dot products from the batch backward's per-sample
       // gradient slabs, beside the fc1 tangent range (meta.hpp SlabDotArgs)
       SlabDotArgs sd{};
@@ -1495,7 +1476,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.run = keep ? logit_buf->run : nullptr;
   ad.dirty = keep ? logit_buf->dirty : nullptr;
   ad.n_logits = keep ? logit_buf->capacity : 0;
-  if (keep && K == 1 && M <= META_THREADS && kMetaAdamChunks) {
+  if (keep && K == 1 && M <= META_THREADS) {
     // Adam and the re-sums of the chunks it writes in one launch
     MetaAdamChunks ck{logit_buf->csum, logit_buf->nblocks, H->arrive};
     hipLaunchKernelGGL(meta_adam_chunks_kernel, dim3(logit_buf->nblocks), dim3(META_THREADS), 0, st, ad, ck);
