@@ -68,12 +68,7 @@ constexpr int FC1X_RED = 256 + 4 * 16;  // one padded 16 x 16 dX partial tile
 constexpr int FC1X_SMEM = 32 * FC1X_LD + 4 * 2 * FC1X_RED;  // floats: dz1 chunk + dX partials
 
 // Samples [c_beg, c_end) of the batch, in chunks of 32 (fc1_dx_block gives a
-// block one chunk).  KT: 16-row W1 tiles per block, all loaded up front and
-// run against the same staged dz1 chunk (KT = 2 for batches above 32: the
-// M = 100 meta batch's 784 one-tile blocks needed 1.5 rounds of the two
-// blocks per CU that the 77 KB of LDS allows, and re-staged each dz1 chunk
-// once per tile).
-template <int KT>
+// block one chunk).
 __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, int blk, int c_beg, int c_end) {
   DQZ_STAMP(5, 0);
   constexpr int LD = FC1X_LD;
@@ -86,14 +81,12 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
   auto red_at = [](int row, int col) { return row * 16 + 16 * (row >> 2) + col; };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
+  const int k0 = 16 * blk;
   const float* W1 = a.th + a.w_off;
-  float4 wv[KT][8];  // B operand: W1[k0 + n][128 w + 16 j + 4 kq + e] of tile kt
+  float4 wv[8];  // B operand: W1[k0 + n][128 w + 16 j + 4 kq + e]
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      wv[kt][j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(16 * (KT * blk + kt) + n) * HID + 128 * w + 16 * j +
-                                                   4 * kq);
+  for (int j = 0; j < 8; ++j)
+    wv[j] = *reinterpret_cast<const float4*>(W1 + (int64_t)(k0 + n) * HID + 128 * w + 16 * j + 4 * kq);
   for (int c = c_beg; c < c_end; c += 32) {
     if (c > c_beg) __syncthreads();  // previous chunk's s_dz / s_red readers are done
     // stage dz1 rows [c, c + 32) (rows past B are zero)
@@ -104,12 +97,10 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
       const float4 x = *reinterpret_cast<const float4*>(a.dz1 + (int64_t)min(c + row, a.B - 1) * HID + 4 * (f & 127));
       v[i] = c + row < a.B ? x : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float ym[KT][2];  // relu'(y3) operands of the epilogue
+    float ym[2];  // relu'(y3) operands of the epilogue
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        ym[kt][h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + 16 * (KT * blk + kt) + (t & 15)];
+    for (int h = 0; h < 2; ++h)
+      ym[h] = a.y3[(int64_t)min(c + 16 * h + (t >> 4), a.B - 1) * FLAT + k0 + (t & 15)];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int f = t + 256 * i;
@@ -117,42 +108,30 @@ __device__ __forceinline__ void fc1_dx_body(const Fc1BwdArgs& a, float* smem, in
     }
     __syncthreads();
     // rows (samples) 16 mt + n, K = hidden [128 w, 128 w + 128)
-    f32x4 xacc[KT][2];
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) xacc[kt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 xacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const float* d = s_dz + (16 * mt + n) * LD + 128 * w + 4 * kq;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float4 av = *reinterpret_cast<const float4*>(d + 16 * j);
-#pragma unroll
-        for (int kt = 0; kt < KT; ++kt) {
-          xacc[kt][mt] = mfma4(av.x, wv[kt][j].x, xacc[kt][mt]);
-          xacc[kt][mt] = mfma4(av.y, wv[kt][j].y, xacc[kt][mt]);
-          xacc[kt][mt] = mfma4(av.z, wv[kt][j].z, xacc[kt][mt]);
-          xacc[kt][mt] = mfma4(av.w, wv[kt][j].w, xacc[kt][mt]);
-        }
+        xacc[mt] = mfma4(av.x, wv[j].x, xacc[mt]);
+        xacc[mt] = mfma4(av.y, wv[j].y, xacc[mt]);
+        xacc[mt] = mfma4(av.z, wv[j].z, xacc[mt]);
+        xacc[mt] = mfma4(av.w, wv[j].w, xacc[mt]);
       }
     }
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      if (kt > 0) __syncthreads();  // the previous tile's reduction reads are done
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int r = 0; r < 4; ++r) s_red[w][mt][red_at(4 * kq + r, n)] = xacc[mt][r];
+    __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[w][mt][red_at(4 * kq + r, n)] = xacc[kt][mt][r];
-      __syncthreads();
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int sample = c + 16 * h + (t >> 4);
-        const int k = red_at(t >> 4, t & 15);
-        const float v2 = (s_red[0][h][k] + s_red[1][h][k]) + (s_red[2][h][k] + s_red[3][h][k]);
-        if (sample < a.B)
-          a.dy3[(int64_t)sample * FLAT + 16 * (KT * blk + kt) + (t & 15)] = ym[kt][h] > 0.f ? v2 : 0.f;
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int sample = c + 16 * h + (t >> 4);
+      const int k = red_at(t >> 4, t & 15);
+      const float v2 = (s_red[0][h][k] + s_red[1][h][k]) + (s_red[2][h][k] + s_red[3][h][k]);
+      if (sample < a.B) a.dy3[(int64_t)sample * FLAT + k0 + (t & 15)] = ym[h] > 0.f ? v2 : 0.f;
     }
   }
   DQZ_STAMP(5, 3);
@@ -753,14 +732,11 @@ __device__ __forceinline__ void fc1_dw_body(const Fc1BwdArgs& a, float* smem, in
 // and the independent dW job sets share one launch, so the latency-bound dX
 // workgroups and the dW workgroups share the CUs (no cross-stream edges).
 
-// Grid: 196 / KT row blocks x ceil(B / 32) sample chunks (block = kb + (196 /
-// KT) chunk), so a batch of more than 32 (the MGSC meta batch) runs its
-// chunks side by side instead of one after another in each block (M = 100:
-// 12.9 -> 12.0 us), with KT = 2 row tiles per block above 32 samples.
+// Grid: 196 row blocks x ceil(B / 32) sample chunks (block = kb + 196 chunk),
+// so a batch of more than 32 (the MGSC meta batch) runs its chunks side by
+// side instead of one after another in each block (M = 100: 12.9 -> ? us).
 constexpr int FC1X_BLOCKS = FLAT / 16;  // 196
-inline int fc1_dx_kt(int B) { return B > 32 ? 2 : 1; }
-inline int fc1_dx_blocks(int B) { return FC1X_BLOCKS / fc1_dx_kt(B) * ((B + 31) / 32); }
-template <int KT>
+inline int fc1_dx_blocks(int B) { return FC1X_BLOCKS * ((B + 31) / 32); }
 __device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, int blk) {
   // W3 / W2 dX copies: element i of the 69,632 is thread i of the grid (the
   // gathers are issued first and land under the block's own work)
@@ -770,9 +746,8 @@ __device__ __forceinline__ void fc1_dx_block(const Fc1BwdArgs& a, float* smem, i
     if (g < W3P_N) v3 = a.w3[w3p_src(g)];
     if (g < W2P_N) v2 = a.w2[w2p_src(g)];
   }
-  constexpr int NKB = FC1X_BLOCKS / KT;
-  const int kb = blk % NKB, c = 32 * (blk / NKB);
-  fc1_dx_body<KT>(a, smem, kb, c, min(c + 32, a.B));
+  const int kb = blk % FC1X_BLOCKS, c = 32 * (blk / FC1X_BLOCKS);
+  fc1_dx_body(a, smem, kb, c, min(c + 32, a.B));
   if (a.w3p) {
     if (g < W3P_N) a.w3p[g] = v3;
     if (g < W2P_N) a.w2p[g] = v2;
@@ -857,10 +832,9 @@ inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStr
   return hipGetLastError();
 }
 
-template <int KT>
 __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
-  fc1_dx_block<KT>(a, smem, blockIdx.x);
+  fc1_dx_block(a, smem, blockIdx.x);
 }
 
 // bwd_bc_kernel: the whole backward after fc1 dX in one launch.  Grid, in

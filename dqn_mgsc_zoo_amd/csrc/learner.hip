@@ -390,8 +390,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     DQZ_HIP(launch_head_dx1(h, fb, st));
   } else {
     DQZ_PHASE(4, DQZ_HIP(launch_head(h, B, st)));
-    DQZ_PHASE(5, if (fc1_dx_kt(B) == 2) hipLaunchKernelGGL(fc1_dx_kernel<2>, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
-              else hipLaunchKernelGGL(fc1_dx_kernel<1>, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
+    DQZ_PHASE(5, hipLaunchKernelGGL(fc1_dx_kernel, dim3(fc1_dx_blocks(B)), dim3(256), 0, st, fb);
               DQZ_HIP(hipGetLastError()));
   }
 
