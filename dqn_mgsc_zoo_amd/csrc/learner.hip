@@ -423,8 +423,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8,
-                       L->spin_max};
+  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr,
+                       c2x_jobs(small), 8, L->spin_max};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
   PerWbArgs wbk{};
@@ -433,7 +433,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int grid = (wb ? 8 : 0) + c3x_jobs(small) * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
+  const int grid = (wb ? 8 : 0) + c3x_jobs(small) * B8 + 4 * (FLAT / 16) + c2x_jobs(small) * B8 + 4 * B8 + 8 * B8 +
+                   8 * B8;
   DQZ_PHASE(6, if (small) {
               if (wb) hipLaunchKernelGGL((bwd_bc_kernel<true, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
               else hipLaunchKernelGGL((bwd_bc_kernel<false, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
