@@ -230,13 +230,15 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   const int Bc = L->cfg.batch;
   int* hw = L->sync + 2 * Bc * Handoff::kStride;
   int* err = L->sync + 16 * Bc * Handoff::kStride;
-  const int jobs = fwd_conv_jobs(Z * B);
-  c2.jobs = c3.jobs = jobs;
-  c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, jobs};
+  const bool rows = Z * B <= kFwdRowMaxSamples && src.fused == 0;  // one-row jobs (fwd_conv_kernel<0>)
+  const int j2 = rows ? C2F_JOBS_ROW : fwd_conv_jobs(Z * B), j3 = rows ? C3F_JOBS_ROW : fwd_conv_jobs(Z * B);
+  c2.jobs = j2;
+  c3.jobs = j3;
+  c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, j2};
   c2.wait = c1.pub;
-  c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
+  c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, j2, j3};
   c3.wait = c2.pub;
-  const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
+  const dim3 grid(xcd_grid(4, Z * B).x + xcd_grid(j2, Z * B).x + xcd_grid(j3, Z * B).x);
   DQZ_PHASE(0, switch (src.fused) {
     case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
     case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
