@@ -407,8 +407,10 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  const bool small = B <= 2;  // one-sample launches: conv3 dX in 24 jobs per sample
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, c3x_jobs(small), 16, L->spin_max};
+  const bool small = B <= 2;  // one-sample launches: conv3 dX and conv2 dX in 24 jobs per sample
+  // dy2: the conv3 dX jobs arrive, the conv2 dX and the 8 conv2 dW jobs consume
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, c3x_jobs(small), c2x_jobs(small) + 8,
+                     L->spin_max};
   Conv2BwdArgs c2b{};
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
