@@ -356,19 +356,8 @@ struct Conv2BwdArgs {
 // polls the sample's counter, and every dy2 load is an sc1 (L1-bypassing)
 // buffer load.  PUB: dy1 is handed on to the conv1 dW jobs of the same launch
 // (sc1 stores + arrival on sync1).
-// NG: pixel groups per (phase, channel half).  1 (the default): a job owns
-// the phase's 100 pixels (6 MFMA row tiles + 4 on the VALU), 8 jobs per
-// sample; 3 (the one-sample launches): group mh owns tiles 2 mh, 2 mh + 1
-// (and the 4 VALU pixels when mh = 2), 24 jobs per sample.
-template <bool WAIT, bool PUB = false, int NG = 1>
-__device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh,
-                                             int mh = 0) {
-  static_assert(NG == 1 || NG == 3, "conv2 dX pixel groups");
-  constexpr int MT = 6 / NG;           // MFMA row tiles per job
-  constexpr int RP = NG == 1 ? 112 : 16 * MT + 4;  // s_red rows per wave: the tiles + the 4 VALU pixels
-  constexpr int NQ = NG == 1 ? 2 : 1;  // epilogue passes of 64 positions
-  const int p0 = 16 * MT * mh;         // first pixel of the job
-  const bool tail = NG == 1 || mh == NG - 1;  // the job with pixels 96..99
+template <bool WAIT, bool PUB = false>
+__device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win, int b, int ph, int pw, int hh) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   float wr[16];  // wr[4 t + j] = W2[kh(t)][kw(t)][16 hh + n][16 w + 4 j + kq]
@@ -384,13 +373,12 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
       wr[4 * tp + 3] = v.w;
     }
   }
-  // relu'(y1) operands of the epilogue, loaded early: thread t owns the
-  // job's output positions t / 4 (and t / 4 + 64), channels 16 hh + 4 (t & 3) .. +3
-  float4 ym4[NQ];
+  // relu'(y1) operands of the epilogue, loaded early: thread t owns output
+  // positions q = t / 4 and q + 64 (< 100), channels 16 hh + 4 (t & 3) .. +3
+  float4 ym4[2];
 #pragma unroll
-  for (int k = 0; k < NQ; ++k) {
-    const int r = (t >> 2) + 64 * k;  // job row: tile rows, then the 4 VALU pixels
-    const int q = min(r < 16 * MT ? p0 + r : 96 + (r - 16 * MT), 99), ah = q / 10, cw = q % 10;
+  for (int k = 0; k < 2; ++k) {
+    const int q = min((t >> 2) + 64 * k, 99), ah = q / 10, cw = q % 10;
     ym4[k] = *reinterpret_cast<const float4*>(a.y1 + ((int64_t)b * C1M + (2 * ah + ph) * C1O + 2 * cw + pw) * C1CO +
                                               16 * hh + 4 * (t & 3));
   }
@@ -427,10 +415,11 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   __syncthreads();
   DQZ_STAMP(7, 1);
   // 100 pixels = 6 MFMA row tiles + pixels 96..99 on the VALU (fwd.hpp's trim)
+  constexpr int MT = 6;
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int p = min(p0 + 16 * m + n, 99);  // p = 10 a + c
+    const int p = min(16 * m + n, 99);  // p = 10 a + c
     base[m] = (p / 10) * C2X_RS + (p % 10) * C2X_S + win64_ch(16 * w) + kq;
   }
   f32x4 acc[MT];
@@ -443,7 +432,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
     const int off = (tp >> 1) * C2X_RS + (tp & 1) * C2X_S + 4 * (kk & 3);
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
-    if (tail) {
+    {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         last[e] = __fmaf_rn(s_win[9 * C2X_RS + (6 + e) * C2X_S + win64_ch(16 * w) + kq + off], wr[kk], last[e]);
@@ -458,30 +447,27 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   }
   __syncthreads();
   DQZ_STAMP(7, 2);
-  constexpr int RW = RP * 16;  // one wave's partial tile
-  float* s_red = s_win;        // [4][RP][16]
+  float* s_red = s_win;  // [4][112][16]
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
-  if (tail && kq == 0) {
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 1792 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+  if (kq == 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s_red[w * RW + (16 * MT + e) * 16 + n] = last[e];
+    for (int e = 0; e < 4; ++e) s_red[w * 1792 + (96 + e) * 16 + n] = last[e];
   }
   __syncthreads();
   // 4 channels per lane: one 16-byte (write-through when PUB) store each
   // (a 4-byte write-through store costs ~6x the 16-byte one per byte)
-  const int nrow = 16 * MT + (tail ? 4 : 0);
 #pragma unroll
-  for (int k = 0; k < NQ; ++k) {
-    const int r = (t >> 2) + 64 * k;
-    if (r < nrow) {
-      const int q = r < 16 * MT ? p0 + r : 96 + (r - 16 * MT);
-      const int i = 16 * r + 4 * (t & 3), ah = q / 10, cw = q % 10;
+  for (int k = 0; k < 2; ++k) {
+    const int q = (t >> 2) + 64 * k;
+    if (q < 100) {
+      const int i = 16 * q + 4 * (t & 3), ah = q / 10, cw = q % 10;
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = (s_red[i + e] + s_red[RW + i + e]) + (s_red[2 * RW + i + e] + s_red[3 * RW + i + e]);
+        v[e] = (s_red[i + e] + s_red[1792 + i + e]) + (s_red[3584 + i + e] + s_red[5376 + i + e]);
       v[0] = ym4[k].x > 0.f ? v[0] : 0.f;
       v[1] = ym4[k].y > 0.f ? v[1] : 0.f;
       v[2] = ym4[k].z > 0.f ? v[2] : 0.f;
@@ -895,12 +881,9 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // against 16,137-16,223 steps/s; L = 3 / 5 / 6 15,210 / 14,750 / 13,200;
 // profiles/r05/split.)
 // SMALL (the one-sample launches: the MGSC pass at theta', the HVP's
-// unit-cotangent pass): conv3 dX and conv2 dX as 24 jobs per sample each
-// (conv3_bwd_dx<., 1>, conv2_bwd_dx<., ., 3>).
+// unit-cotangent pass): conv3 dX as 24 jobs per sample (conv3_bwd_dx<., 1>).
 constexpr int C3X_JOBS_SMALL = 4 * ((C2M + 15) / 16);  // 24
-constexpr int C2X_JOBS_SMALL = 8 * 3;                   // conv2_bwd_dx<., ., 3>
 __host__ __device__ inline int c3x_jobs(bool small) { return small ? C3X_JOBS_SMALL : 8; }
-__host__ __device__ inline int c2x_jobs(bool small) { return small ? C2X_JOBS_SMALL : 8; }
 template <bool WB, bool SMALL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
@@ -937,21 +920,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   i -= NF;
-  constexpr int J2 = SMALL ? C2X_JOBS_SMALL : 8;
-  if (i < J2 * B8) {
-    const SampleJob sj = xcd_sample_job_at(i, J2, c2.B);
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
     DQZ_STAMP(7, 0);
-    if constexpr (SMALL) {
-      const int jb = sj.job & 7;
-      conv2_bwd_dx<true, true, 3>(c2, smem, sj.s, (jb & 3) >> 1, jb & 1, jb >> 2, sj.job >> 3);
-    } else {
-      conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
-    }
+    conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
     return;
   }
-  i -= J2 * B8;
+  i -= 8 * B8;
   if (i < 4 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 4, c3.B);
     if (!sj.valid) return;

@@ -197,14 +197,11 @@ __device__ __forceinline__ void conv2_fwd_body(const LayerFwdArgs& a, float* s_i
 // arrive after the hand-off wait) and runs 3 MFMA row tiles instead of 5, so
 // the per-sample chain after conv1 is shorter; y2 goes out as 16-byte
 // write-through stores (4 channels per lane) and conv3 waits for 8 arrivals.
-// R: output rows per job (5: the 8-job form; 1: the one-row jobs of the
-// smallest launches, 36 per sample, fwd_conv_kernel<0>).
 constexpr int C2F_ROWS0 = 5;
-template <int R = C2F_ROWS0>
 __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(1, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
-  const int oh0 = rh * R, npos = (R == C2F_ROWS0 ? (rh ? C2O - R : R) : min(R, C2O - oh0)) * C2O;  // 45 / 36
+  const int oh0 = rh * C2F_ROWS0, npos = (rh ? C2O - C2F_ROWS0 : C2F_ROWS0) * C2O;  // 45 / 36
   const int ih0 = C2S * oh0, nrows = C2S * (npos / C2O - 1) + C2K;               // 12 / 10
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // w = kh
   const int n = lane & 15, kq = lane >> 4;
@@ -218,7 +215,7 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
                       ih0 * C1O * (C1CO / 4);
   const int nq4 = nrows * C1O * (C1CO / 4);  // 1920 / 1600 float4
   a.wait.wait(sj.s);
-  constexpr int NL = (2 * R + 2) * C1O * (C1CO / 4) / 256;  // 7.5 -> 8 loads per thread at most (R = 5)
+  constexpr int NL = (2 * C2F_ROWS0 + 2) * C1O * (C1CO / 4) / 256;  // 7.5 -> 8 loads per thread at most
   float4 r[NL + 1];
 #pragma unroll
   for (int q = 0; q <= NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
@@ -237,7 +234,7 @@ __device__ __forceinline__ void conv2_fwd8_body(const LayerFwdArgs& a, float* s_
   }
   DQZ_STAMP(1, 1);
   __syncthreads();
-  constexpr int MT = (R * C2O + 15) / 16;  // 3 (48 rows): the tail rows clamp to the last position and are not stored
+  constexpr int MT = 3;  // 48 rows: the tail rows clamp to the last position and are not stored
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -397,17 +394,10 @@ constexpr int C3F_ROWS0 = 4;
 // MFMA row tiles and every conv2 block resident from the start).
 constexpr int kFwd8MaxSamples = 16;
 inline int fwd_conv_jobs(int zb) { return zb <= kFwd8MaxSamples ? 8 : 4; }
-// The smallest launches (at most kFwdRowMaxSamples samples, fwd_conv_kernel<0>:
-// the MGSC pass at theta', the HVP pass, the actor's state): one output row
-// per job, conv2 36 and conv3 28 jobs per sample, a third / half of the 8-job
-// forms' MFMAs per wave on a chip those forms left idle.
-constexpr int kFwdRowMaxSamples = 2;
-constexpr int C2F_JOBS_ROW = 4 * C2O, C3F_JOBS_ROW = 4 * C3O;  // 36, 28
-template <int R = C3F_ROWS0>
 __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
   DQZ_STAMP(2, 0);
   const int rh = sj.job >> 2, nq = sj.job & 3, b = sj.s % a.B, z = sj.s / a.B;
-  const int oh0 = rh * R, npos = (R == C3F_ROWS0 ? (rh ? C3O - R : R) : min(R, C3O - oh0)) * C3O;  // 28 / 21
+  const int oh0 = rh * C3F_ROWS0, npos = (rh ? C3O - C3F_ROWS0 : C3F_ROWS0) * C3O;  // 28 / 21
   const int nrows = npos / C3O + C3K - 1;                                          // 6 / 5
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
@@ -421,7 +411,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
                       oh0 * C2O * (C2CO / 4);
   const int nq4 = nrows * C2O * (C2CO / 4);  // 864 / 720 float4
   a.wait.wait(sj.s);
-  constexpr int NL = ((R + C3K - 1) * C2O * (C2CO / 4) + 255) / 256;  // 4 (R = 4)
+  constexpr int NL = ((C3F_ROWS0 + C3K - 1) * C2O * (C2CO / 4) + 255) / 256;  // 4
   float4 r[NL];
 #pragma unroll
   for (int q = 0; q < NL; ++q) r[q] = load_sc1_f4(src, nq4 * 16, min(t + 256 * q, nq4 - 1));
@@ -440,7 +430,7 @@ __device__ __forceinline__ void conv3_fwd8_body(const LayerFwdArgs& a, float* s_
   }
   DQZ_STAMP(2, 1);
   __syncthreads();
-  constexpr int MT = (R * C3O + 15) / 16;  // 32 rows: the tail rows clamp to the last position and are not stored
+  constexpr int MT = 2;  // 32 rows: the tail rows clamp to the last position and are not stored
   int base[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -511,13 +501,11 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
     return;
   }
   i -= n;
-  const int j2 = c2.jobs, j3 = c3.jobs;  // 4 or 8 per sample (fwd_conv_jobs), or 36 / 28 (F = 0)
+  const int j2 = c2.jobs, j3 = c3.jobs;  // 4 or 8 per sample (fwd_conv_jobs)
   if (i < (j2 / 4) * n) {
     const SampleJob sj = xcd_sample_job_at(i, j2, zb);
     if (sj.valid) {
-      if (F == 0 && j2 == C2F_JOBS_ROW)
-        conv2_fwd8_body<1>(c2, smem, sj);
-      else if (j2 == 8)
+      if (j2 == 8)
         conv2_fwd8_body(c2, smem, sj);
       else
         conv2_fwd_body<true, true>(c2, smem, sj);
@@ -526,9 +514,7 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
   }
   const SampleJob sj = xcd_sample_job_at(i - (j2 / 4) * n, j3, zb);
   if (sj.valid) {
-    if (F == 0 && j3 == C3F_JOBS_ROW)
-      conv3_fwd8_body<1>(c3, smem, sj);
-    else if (j3 == 8)
+    if (j3 == 8)
       conv3_fwd8_body(c3, smem, sj);
     else
       conv3_fwd_body<true>(c3, smem, sj);

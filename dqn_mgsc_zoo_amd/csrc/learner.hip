@@ -230,15 +230,13 @@ static int forward_impl(dqz_learner* L, const NetZ& nz, int Z, int B, const Conv
   const int Bc = L->cfg.batch;
   int* hw = L->sync + 2 * Bc * Handoff::kStride;
   int* err = L->sync + 16 * Bc * Handoff::kStride;
-  const bool rows = Z * B <= kFwdRowMaxSamples && src.fused == 0;  // one-row jobs (fwd_conv_kernel<0>)
-  const int j2 = rows ? C2F_JOBS_ROW : fwd_conv_jobs(Z * B), j3 = rows ? C3F_JOBS_ROW : fwd_conv_jobs(Z * B);
-  c2.jobs = j2;
-  c3.jobs = j3;
-  c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, j2};
+  const int jobs = fwd_conv_jobs(Z * B);
+  c2.jobs = c3.jobs = jobs;
+  c1.pub = Handoff{hw, hw + 3 * Bc * Handoff::kStride, err, 4, jobs};
   c2.wait = c1.pub;
-  c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, j2, j3};
+  c2.pub = Handoff{hw + 6 * Bc * Handoff::kStride, hw + 9 * Bc * Handoff::kStride, err, jobs, jobs};
   c3.wait = c2.pub;
-  const dim3 grid(xcd_grid(4, Z * B).x + xcd_grid(j2, Z * B).x + xcd_grid(j3, Z * B).x);
+  const dim3 grid(xcd_grid(4, Z * B).x + 2 * xcd_grid(jobs, Z * B).x);
   DQZ_PHASE(0, switch (src.fused) {
     case 1: hipLaunchKernelGGL(fwd_conv_kernel<1>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
     case 2: hipLaunchKernelGGL(fwd_conv_kernel<2>, grid, dim3(256), kConv1FwdSmem, st, c1, c2, c3); break;
@@ -407,10 +405,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  const bool small = B <= 2;  // one-sample launches: conv3 dX and conv2 dX in 24 jobs per sample
-  // dy2: the conv3 dX jobs arrive, the conv2 dX and the 8 conv2 dW jobs consume
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, c3x_jobs(small), c2x_jobs(small) + 8,
-                     L->spin_max};
+  const bool small = B <= 2;  // one-sample launches: conv3 dX in 24 jobs per sample
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, c3x_jobs(small), 16, L->spin_max};
   Conv2BwdArgs c2b{};
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -427,8 +423,8 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
   c1dw.part = L->p1;
-  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr,
-                       c2x_jobs(small), 8, L->spin_max};
+  c1dw.sync1 = Handoff{L->sync + 14 * B * Handoff::kStride, L->sync + 15 * B * Handoff::kStride, herr, 8, 8,
+                       L->spin_max};
   c2b.sync1 = c1dw.sync1;
   const int B8 = (B + 7) / 8 * 8;
   PerWbArgs wbk{};
@@ -437,8 +433,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int grid = (wb ? 8 : 0) + c3x_jobs(small) * B8 + 4 * (FLAT / 16) + c2x_jobs(small) * B8 + 4 * B8 + 8 * B8 +
-                   8 * B8;
+  const int grid = (wb ? 8 : 0) + c3x_jobs(small) * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
   DQZ_PHASE(6, if (small) {
               if (wb) hipLaunchKernelGGL((bwd_bc_kernel<true, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
               else hipLaunchKernelGGL((bwd_bc_kernel<false, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
