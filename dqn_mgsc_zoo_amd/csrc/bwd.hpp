@@ -162,13 +162,8 @@ struct Conv3BwdArgs {
 // dy2 store is write-through (sc1), every storing wave drains (vmcnt(0)), and
 // after the workgroup barrier one lane adds to the sample's arrival counter
 // (MI355X_MICROARCH.md visibility table, row 1; the consumer loads sc1).
-// MT: 16-position row tiles per job.  3 (the default): jobs are (channel
-// quarter nq, position half mh: 48 / 33 positions), 8 per sample; 1 (the
-// one-sample launches, bwd_bc_kernel<., true>): 16-position sixths, 24 per
-// sample, a third of the MFMAs per wave on a chip the 8 jobs left idle.
-template <bool PUB, int MT = 3>
+template <bool PUB>
 __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win, int b, int nq, int mh) {
-  constexpr int P = 16 * MT;  // positions per job
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = lane & 15, kq = lane >> 4;
   // B operand: flipped kernel, k = (tap' = kh'*3 + kw', co), wave w owns co [16w, 16w + 16)
@@ -184,9 +179,9 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
       wr[4 * tp + 3] = v.w;
     }
   }
-  // relu'(y2) operands of the epilogue, loaded early: thread t < 4 P owns
-  // position P mh + t / 4, channels 16 nq + 4 (t & 3) .. +3
-  const int ep = min(P * mh + (t >> 2), C2M - 1);
+  // relu'(y2) operands of the epilogue, loaded early: thread t < 192 owns
+  // position 48 mh + t / 4, channels 16 nq + 4 (t & 3) .. +3
+  const int ep = min(48 * mh + (t >> 2), C2M - 1);
   const float4 ym4 = *reinterpret_cast<const float4*>(a.y2 + ((int64_t)b * C2M + ep) * C2CO + 16 * nq + 4 * (t & 3));
   // padded dy3 window: (ph, pw) in 11 x 11, interior [2, 9)
   const float4* src = reinterpret_cast<const float4*>(a.dy3 + (int64_t)b * FLAT);
@@ -215,44 +210,43 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
   }
   __syncthreads();
   DQZ_STAMP(6, 1);
-  int base[MT];
+  int base[3];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int p = min(P * mh + 16 * m + n, C2M - 1);
+  for (int m = 0; m < 3; ++m) {
+    const int p = min(48 * mh + 16 * m + n, C2M - 1);
     base[m] = (p / C2O) * C3X_RS + (p % C2O) * C3X_S + win64_ch(16 * w) + kq;
   }
-  f32x4 acc[MT];
+  f32x4 acc[3];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < 3; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kk = 0; kk < 36; ++kk) {
     const int tp = kk >> 2;  // tap' = kh'*3 + kw'
     const int off = (tp / 3) * C3X_RS + (tp % 3) * C3X_S + 4 * (kk & 3);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
+    for (int m = 0; m < 3; ++m) acc[m] = mfma4(s_win[base[m] + off], wr[kk], acc[m]);
   }
   __syncthreads();
   DQZ_STAMP(6, 2);
-  constexpr int RW = P * 16;  // one wave's partial tile
-  float* s_red = s_win;       // [4][P][16]
+  float* s_red = s_win;  // [4][48][16]
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < 3; ++m)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) s_red[w * RW + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
+    for (int rr = 0; rr < 4; ++rr) s_red[w * 768 + (16 * m + 4 * kq + rr) * 16 + n] = acc[m][rr];
   __syncthreads();
   // 4 channels per lane: one 16-byte (write-through when PUB) store each
-  if (t < 4 * P && P * mh + (t >> 2) < C2M) {
+  if (t < 192 && 48 * mh + (t >> 2) < C2M) {
     const int i = 4 * t;  // s_red index of (position t / 4, channel 4 (t & 3))
     f32x4 v;  // (a 4-byte write-through store costs ~6x the 16-byte one per byte)
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      v[e] = (s_red[i + e] + s_red[RW + i + e]) + (s_red[2 * RW + i + e] + s_red[3 * RW + i + e]);
+      v[e] = (s_red[i + e] + s_red[768 + i + e]) + (s_red[1536 + i + e] + s_red[2304 + i + e]);
     v[0] = ym4.x > 0.f ? v[0] : 0.f;
     v[1] = ym4.y > 0.f ? v[1] : 0.f;
     v[2] = ym4.z > 0.f ? v[2] : 0.f;
     v[3] = ym4.w > 0.f ? v[3] : 0.f;
     float* slab = a.dy2 + (int64_t)b * C2M * C2CO;
-    const int off = ((P * mh + (t >> 2)) * C2CO + 16 * nq + 4 * (t & 3)) * 4;
+    const int off = ((48 * mh + (t >> 2)) * C2CO + 16 * nq + 4 * (t & 3)) * 4;
     if constexpr (PUB)
       store_sc1_f4(slab, C2M * C2CO * 4, off, v);
     else
@@ -880,11 +874,7 @@ __global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // 5.8 us, the written lines now dirty in half the L2s: 15,873-15,901
 // against 16,137-16,223 steps/s; L = 3 / 5 / 6 15,210 / 14,750 / 13,200;
 // profiles/r05/split.)
-// SMALL (the one-sample launches: the MGSC pass at theta', the HVP's
-// unit-cotangent pass): conv3 dX as 24 jobs per sample (conv3_bwd_dx<., 1>).
-constexpr int C3X_JOBS_SMALL = 4 * ((C2M + 15) / 16);  // 24
-__host__ __device__ inline int c3x_jobs(bool small) { return small ? C3X_JOBS_SMALL : 8; }
-template <bool WB, bool SMALL = false>
+template <bool WB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void bwd_bc_kernel(
     Conv3BwdArgs c3, Fc1BwdArgs f1, Conv2BwdArgs c2, Conv1DwArgs c1, PerWbArgs wb) {
   constexpr int kW = C3X_WIN > FC1W_SMEM ? C3X_WIN : FC1W_SMEM;
@@ -904,16 +894,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     i -= 8;
   }
-  constexpr int J3 = SMALL ? C3X_JOBS_SMALL : 8;
-  if (i < J3 * B8) {
-    const SampleJob sj = xcd_sample_job_at(i, J3, c3.B);
+  if (i < 8 * B8) {
+    const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
     if (!sj.valid) return;
     DQZ_STAMP(6, 0);
-    conv3_bwd_dx<true, SMALL ? 1 : 3>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
+    conv3_bwd_dx<true>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
     DQZ_STAMP(6, 3);
     return;
   }
-  i -= J3 * B8;
+  i -= 8 * B8;
   if (i < NF) {
     if (DQZ_EXP_SKIP & 1) return;
     fc1_dw_body(f1, smem, i);

@@ -405,8 +405,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   // hand-off words (units of Handoff::kStride ints): dy2 cnt [0, B), ack [B, 2B);
   // forward y1 / y2 [2B, 14B); dy1 cnt [14B, 15B), ack [15B, 16B); err at 16B
   int* const herr = L->sync + 16 * B * Handoff::kStride;
-  const bool small = B <= 2;  // one-sample launches: conv3 dX in 24 jobs per sample
-  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, c3x_jobs(small), 16, L->spin_max};
+  c3b.sync = Handoff{L->sync, L->sync + B * Handoff::kStride, herr, 8, 16, L->spin_max};
   Conv2BwdArgs c2b{};
   c2b.dy2 = L->dy2;
   c2b.y1 = L->y1;
@@ -433,14 +432,9 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
     wbk.td = L->td;
     wbk.n = B;
   }
-  const int grid = (wb ? 8 : 0) + c3x_jobs(small) * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
-  DQZ_PHASE(6, if (small) {
-              if (wb) hipLaunchKernelGGL((bwd_bc_kernel<true, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-              else hipLaunchKernelGGL((bwd_bc_kernel<false, true>), dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-            } else {
-              if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-              else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
-            }
+  const int grid = (wb ? 8 : 0) + 8 * B8 + 4 * (FLAT / 16) + 8 * B8 + 4 * B8 + 8 * B8 + 8 * B8;
+  DQZ_PHASE(6, if (wb) hipLaunchKernelGGL(bwd_bc_kernel<true>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
+            else hipLaunchKernelGGL(bwd_bc_kernel<false>, dim3(grid), dim3(256), 0, st, c3b, fb, c2b, c1dw, wbk);
             DQZ_HIP(hipGetLastError()));
   if (pe.on()) pe.ms[7] = pe.ms[8] = 0.f;
 
