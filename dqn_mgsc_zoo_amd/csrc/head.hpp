@@ -419,38 +419,37 @@ constexpr int UPD_PAIRS = 32;                  // parameter pairs per workgroup 
 constexpr int UPD_PARAMS = 2 * UPD_PAIRS;
 constexpr int UPD_GROUPS = 8;                  // threads sharing one pair's reduction
 
-// Sum of the float2 p[s * stride + j .. +1] over s = g, g + G, ... < S in
-// rounds of eight slabs per thread, software-pipelined: round r + 1's eight
-// loads are issued before round r is summed, so two rounds are in flight
-// and each round costs one addition chain instead of a round trip (the
-// M = 100 meta batch's conv1 takes 400 slabs: 7 rounds).  Loads past S are
-// clamped to the last slab and their sums skipped; a[u] accumulates its
-// rounds in order, so the bits are those of the unpipelined loop.
+// Sum of the float2 p[s * stride + j .. +1] over s = g, g + G, ... < S, eight
+// loads in flight per iteration (the slabs are written by the previous
+// kernel, so every load is a cache miss; one dependent chain per slab would
+// be latency-bound).
 __device__ __forceinline__ float2 sum_split2(const float* p, int S, int64_t stride, int64_t j, int g) {
   constexpr int G = UPD_GROUPS;
-  float2 a[8], cur[8], nxt[8];
+  float2 a[8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    a[u] = make_float2(0.f, 0.f);
-    cur[u] = *reinterpret_cast<const float2*>(p + (int64_t)min(g + u * G, S - 1) * stride + j);
-  }
-  for (int s0 = g;; s0 += 8 * G) {
-    const bool more = s0 + 8 * G < S;
-    if (more) {
+  for (int u = 0; u < 8; ++u) a[u] = make_float2(0.f, 0.f);
+  int s = g;
+  for (; s + 7 * G < S; s += 8 * G) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        nxt[u] = *reinterpret_cast<const float2*>(p + (int64_t)min(s0 + (8 + u) * G, S - 1) * stride + j);
+    for (int u = 0; u < 8; ++u) {
+      const float2 v = *reinterpret_cast<const float2*>(p + (int64_t)(s + u * G) * stride + j);
+      a[u].x += v.x;
+      a[u].y += v.y;
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (s0 + u * G < S) {
-        a[u].x += cur[u].x;
-        a[u].y += cur[u].y;
-      }
-    if (!more) break;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
   }
+  // the tail without branches: each load is unconditional (clamped to the
+  // last slab) and its sum selected, so all eight are in flight together (a
+  // conditional load per branch waited for each one in turn)
+  float2 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(p + (int64_t)min(s + u * G, S - 1) * stride + j);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (s + u * G < S) {
+      a[u].x += v[u].x;
+      a[u].y += v[u].y;
+    }
   return make_float2(((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x)),
                      ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y)));
 }
