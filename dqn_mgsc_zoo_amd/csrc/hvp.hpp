@@ -10,14 +10,28 @@
 //   d/deps grad     dW_l = sum_p (ydot_{l-1} (x) d_l + y_{l-1} (x) ddot_l), db_l = sum_p ddot_l,
 // with d_l the unit-cotangent backward signals of q[a] (d_5 = e_a).
 //
-// Eight launches, one per dependent stage (t1 t2 t3 t4 b3 b2 b1, then every
-// parameter-gradient block in one launch).  Each stage splits its reduction
-// over the threads of a workgroup and sums the splits through LDS in a fixed
-// order (deterministic, no partial-sum launches); the two passes over fc1's
-// 3136 x 512 weights (t4, b3) read whole rows with coalesced 8- / 16-byte
-// loads over hundreds of workgroups (they are the chain's HBM traffic:
-// 2 x 2 x 6.4 MB).  t4's K-chunk partials are summed by the gradient launch,
-// the only consumer of the fc1 tangent output.
+// Four launches.  The tangent forward (t1 .. t4) and the tangent backward
+// (b3 .. b1) are independent chains: b3 needs only the primal d4, the
+// tangent weights and ddot4 = relu'(h) Wdot2[:, a], which each b3 wave forms
+// from eight gathers.  So the chains run side by side, and two more stage
+// boundaries go by recomputation or alignment:
+//   L1 hvp_l1_kernel  t12 (each conv2 block recomputes the conv1 tangent of
+//                     its 4 x 4 input window, then its conv2 outputs) |
+//                     s1 and ddot4 | b3
+//   L2 hvp_l2_kernel  t34 (conv3 block (p, g) = fc1 K-chunk 4 p + g: the 16
+//                     conv3 outputs it forms are the chunk's 16 rows) | b2
+//   L3 hvp_l3_kernel  b1 | every parameter block of H_q w but conv1's
+//   L4 hvp_g1_kernel  conv1's parameter blocks (the only ones that need all
+//                     of ddot1).
+// Round 5 ran eight launches, one per dependent stage, each ≈ 5.1 us
+// (rocprofv3) for a few microseconds of latency.  Every per-element sum
+// keeps the order of that form.  Each stage splits its reduction over the
+// threads of a workgroup and sums the splits through LDS in a fixed order
+// (deterministic, no partial-sum launches); the two passes over fc1's 3136
+// x 512 weights (t4, b3) read whole rows with coalesced 8- / 16-byte loads
+// over hundreds of workgroups (they are the chain's HBM traffic: 2 x 2 x
+// 6.4 MB).  t4's K-chunk partials are summed by the gradient launch, the only
+// consumer of the fc1 tangent output.
 #pragma once
 #include "common.hpp"
 
@@ -40,19 +54,19 @@ struct HvpArgs {
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1;
   float* hq;    // output, parameter layout
   float* part;  // [HVP_T4_CHUNKS][512] fc1 tangent K-chunk partials
-  // grad q . w: the meta_second_kernel partials, summed once (t1's last block)
+  // grad q . w: the meta_second_kernel partials, summed once (L1's s1 block)
   const float* s1_part;
   int s1_nparts;
   float* s1;  // [1]
-  // meta_combine in hvp_g_kernel's epilogue (vout != null): instead of H_q w
-  // -> hq, v = v_dir + J (alpha s1 grad q - clip(td') H_q w) -> vout,
+  // meta_combine in the gradient blocks' epilogue (vout != null): instead of
+  // H_q w -> hq, v = v_dir + J (alpha s1 grad q - clip(td') H_q w) -> vout,
   // alpha = [|td'| < bound]
   const float *vdir, *J, *gq, *td;
   float bound;
   float* vout;
 };
 
-// One element of hvp_g_kernel's output: H_q w itself, or meta_combine's v.
+// One element of the gradient blocks' output: H_q w itself, or meta_combine's v.
 struct HqOut {
   float a_s1, clip;  // alpha s1, clip(td')
   __device__ __forceinline__ HqOut(const HvpArgs& a) {
@@ -73,98 +87,211 @@ struct HqOut {
 };
 
 constexpr int HVP_T4_KC = 16, HVP_T4_CHUNKS = FLAT / HVP_T4_KC;  // 196 chunks of 16 rows
+constexpr int HVP_T12 = C2M * (C2CO / 16);                       // 324: (conv2 position, 16-channel group)
+constexpr int HVP_T34 = C3M * (C3CO / 16);                       // 196: (conv3 position, 16-channel group)
+constexpr int HVP_B3 = FLAT / 4;                                 // 784: 4 fc1 rows each
+constexpr int HVP_B2 = C2M * (C2CO / 16);                        // 324: (conv2 position, 16-channel group)
+static_assert(HVP_T34 == HVP_T4_CHUNKS, "conv3 block i forms fc1 chunk i's rows");
 
-__device__ __forceinline__ float hvp_x(const HvpArgs& a, int ih, int iw, int ci) {
-  const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
-  return f < 0 ? 0.f : u8n(a.frames[(int64_t)f * FB + ih * FW + iw]);
-}
+// ---- L1 -----------------------------------------------------------------
 
-// 1. conv1 tangent: ty1[p][co] = relu'(y1) (bdot1[co] + sum_k x_p[k] Wdot1[k][co]).
-// Block p (400), thread (kh = t / 32, co = t % 32) sums kw, ci; the 8 kh
-// partials are summed in order.  Block 400 sums the s1 partials.
-__global__ __launch_bounds__(256) void hvp_t1_kernel(HvpArgs a) {
-  __shared__ float s_x[C1KK];
-  __shared__ float s_r[C1K][C1CO];
-  __shared__ float s_w[4];
-  const int t = threadIdx.x;
-  if (blockIdx.x == C1M) {
-    // eight loads in flight per round (one round trip per 2,048 partials)
-    float v = 0.f;
-    for (int j0 = t; j0 < a.s1_nparts; j0 += 8 * 256) {
-      float x[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = a.s1_part[min(j0 + 256 * u, a.s1_nparts - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (j0 + 256 * u < a.s1_nparts) v += x[u];
-    }
-    v = block_sum256(v, s_w);
-    if (t == 0) a.s1[0] = v;
-    return;
-  }
-  const int p = blockIdx.x, oh = p / C1O, ow = p % C1O;
+// A conv2 block's conv1 window: conv1 outputs (2 oh + dy, 2 ow + dx), dy, dx
+// in 0..3, read the 20 x 20 input tile at rows / columns 8 oh, 8 ow.
+constexpr int T12_IN = C1S * 3 + C1K;  // 20
+struct HvpT12Smem {
+  float4 in[T12_IN * T12_IN];  // [row][col], the 4 channels of one pixel
+  float r[16][C1K][C1CO];      // conv1 kh partials per window position
+  float t1[16][C1CO];          // ty1 over the window
+  float r2[16][16];            // conv2 tap partials
+};
+
+// t1 + t2: ty1 = relu'(y1) (bdot1 + sum_k x_p[k] Wdot1[k][co]) over the
+// block's window (thread (kh = t / 32, co = t % 32) sums kw, ci of row kh
+// for each window position; the 8 kh partials are summed in order), then
+// ty2 = relu'(y2) (bdot2 + conv(y1, Wdot2) + conv(ty1, W2)) for 16 channels
+// (thread (tap = t / 16 = kh * 4 + kw, co)).  Each conv1 position is stored
+// by one block: channel group 0 of the conv2 position oh = min(ih / 2, 8),
+// ow = min(iw / 2, 8).
+__device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Smem& s) {
+  const int t = threadIdx.x, p = i >> 2, g = i & 3;
+  const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
-  // the thread's 32 weights first: they are in flight under the patch's
-  // slot -> frame-index -> frame chain
-  const float* W = a.tw + a.off[0];
+  // the thread's 32 conv1 tangent weights, its two window outputs' y1 and
+  // its conv2 operands: in flight under the slot -> frame-index -> frame chain
+  const float* W1d = a.tw + a.off[0];
   float wv[C1K * FC];
 #pragma unroll
-  for (int j = 0; j < C1K * FC; ++j) wv[j] = W[(kh * C1K * FC + j) * C1CO + co];
-  {
-    const int kw = (t >> 2) & 7, ci = t & 3;
-    s_x[t] = hvp_x(a, C1S * oh + kh, C1S * ow + kw, ci);
-  }
-  __syncthreads();
-  float z = 0.f;
+  for (int j = 0; j < C1K * FC; ++j) wv[j] = W1d[(kh * C1K * FC + j) * C1CO + co];
+  float y1v[2];
+  int p1[2];
 #pragma unroll
-  for (int j = 0; j < C1K * FC; ++j) z += s_x[kh * C1K * FC + j] * wv[j];  // (kh, kw = j / 4, ci = j % 4)
-  s_r[kh][co] = z;
-  __syncthreads();
-  if (t < C1CO) {
-    float s = a.tw[a.off[1] + t];
-#pragma unroll
-    for (int k = 0; k < C1K; ++k) s += s_r[k][t];
-    a.ty1[p * C1CO + t] = a.y1[p * C1CO + t] > 0.f ? s : 0.f;
+  for (int h = 0; h < 2; ++h) {
+    const int pos = kh + 8 * h;
+    p1[h] = (2 * oh + (pos >> 2)) * C1O + 2 * ow + (pos & 3);
+    y1v[h] = a.y1[p1[h] * C1CO + co];
   }
-}
-
-// 2. conv2 tangent: ty2 = relu'(y2) (bdot2 + conv(y1, Wdot2) + conv(ty1, W2)).
-// Block (p, 16-channel group g); thread (tap = t / 16 = kh * 4 + kw, co).
-__global__ __launch_bounds__(256) void hvp_t2_kernel(HvpArgs a) {
-  __shared__ float s_r[16][16];
-  const int t = threadIdx.x, p = blockIdx.x, g = blockIdx.y;
-  const int oh = p / C2O, ow = p % C2O, tap = t >> 4, kh = tap >> 2, kw = tap & 3;
-  const int co = 16 * g + (t & 15);
-  const int src = ((oh * C2S + kh) * C1O + ow * C2S + kw) * C1CO;
-  const float *W = a.th + a.off[2] + tap * C2CI * C2CO + co, *Wd = a.tw + a.off[2] + tap * C2CI * C2CO + co;
-  float z = 0.f;
-  float y[C2CI], ty[C2CI], w[C2CI], wd[C2CI];  // every load before the first product
+  const int tap = t >> 4, c2 = 16 * g + (t & 15);
+  const int src = ((2 * oh + (tap >> 2)) * C1O + 2 * ow + (tap & 3)) * C1CO;
+  const float *W = a.th + a.off[2] + tap * C2CI * C2CO + c2, *Wd = a.tw + a.off[2] + tap * C2CI * C2CO + c2;
+  float y[C2CI], w[C2CI], wd[C2CI];
 #pragma unroll
   for (int ci = 0; ci < C2CI; ++ci) {
     y[ci] = a.y1[src + ci];
-    ty[ci] = a.ty1[src + ci];
     wd[ci] = Wd[ci * C2CO];
     w[ci] = W[ci * C2CO];
   }
+  const float y2v = t < 16 ? a.y2[p * C2CO + c2] : 0.f;
+  const float b2v = t < 16 ? a.tw[a.off[3] + c2] : 0.f;
+  const float b1v = a.tw[a.off[1] + co];
+  // the input tile: element e = pixel * 4 + channel, channel = t % 4
+  {
+    const int f = a.fidx[(int64_t)a.slot[0] * 8 + (t & 3)];
+    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB + C1S * 2 * oh * FW + C1S * 2 * ow;
+    constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600, 7 rounds
+    unsigned xb[R];
 #pragma unroll
-  for (int ci = 0; ci < C2CI; ++ci) z += y[ci] * wd[ci] + ty[ci] * w[ci];
-  s_r[tap][t & 15] = z;
+    for (int u = 0; u < R; ++u) {
+      const int px = min(t + 256 * u, N - 1) >> 2;
+      xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
+    }
+    float* in = reinterpret_cast<float*>(s.in);
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (t + 256 * u < N) in[t + 256 * u] = f < 0 ? 0.f : u8n(xb[u]);
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int pos = 0; pos < 16; ++pos) {
+    const float4* row = s.in + (4 * (pos >> 2) + kh) * T12_IN + 4 * (pos & 3);
+    float z = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < C1K; ++kw) {  // (kh, kw, ci = j % 4) as j = 4 kw + ci
+      const float4 x = row[kw];
+      z += x.x * wv[4 * kw];
+      z += x.y * wv[4 * kw + 1];
+      z += x.z * wv[4 * kw + 2];
+      z += x.w * wv[4 * kw + 3];
+    }
+    s.r[pos][kh][co] = z;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pos = kh + 8 * h, dy = pos >> 2, dx = pos & 3;
+    float v = b1v;
+#pragma unroll
+    for (int k = 0; k < C1K; ++k) v += s.r[pos][k][co];
+    const float ty = y1v[h] > 0.f ? v : 0.f;
+    s.t1[pos][co] = ty;
+    if (g == 0 && (dy < 2 || oh == C2O - 1) && (dx < 2 || ow == C2O - 1)) a.ty1[p1[h] * C1CO + co] = ty;
+  }
+  __syncthreads();
+  float z = 0.f;
+#pragma unroll
+  for (int ci = 0; ci < C2CI; ++ci) z += y[ci] * wd[ci] + s.t1[tap][ci] * w[ci];
+  s.r2[tap][t & 15] = z;
   __syncthreads();
   if (t < 16) {
-    const int c = 16 * g + t;
-    float s = a.tw[a.off[3] + c];
+    float v = b2v;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += s_r[k][t];
-    a.ty2[p * C2CO + c] = a.y2[p * C2CO + c] > 0.f ? s : 0.f;
+    for (int k = 0; k < 16; ++k) v += s.r2[k][t];
+    a.ty2[p * C2CO + c2] = y2v > 0.f ? v : 0.f;
   }
 }
 
-// 3. conv3 tangent: ty3 = relu'(y3) (bdot3 + conv(y2, Wdot3) + conv(ty2, W3)).
-// Block (p, 16-channel group g); thread (input-channel quad s = t / 16, co)
-// over the 9 taps.
-__global__ __launch_bounds__(256) void hvp_t3_kernel(HvpArgs a) {
-  __shared__ float s_r[16][16];
-  const int t = threadIdx.x, p = blockIdx.x, g = blockIdx.y;
+// s1 = sum of the grad q . w partials (eight loads in flight per round: one
+// round trip per 2,048 partials), and ddot4 = relu'(h) Wdot2[:, a] stored
+// for the gradient blocks.
+__device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
+  const int t = threadIdx.x;
+  const int act = a.action[a.slot[0]];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int n = t + 256 * h;
+    a.td4[n] = a.h[n] > 0.f ? a.tw[a.off[8] + n * a.A + act] : 0.f;
+  }
+  float v = 0.f;
+  for (int j0 = t; j0 < a.s1_nparts; j0 += 8 * 256) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = a.s1_part[min(j0 + 256 * u, a.s1_nparts - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + 256 * u < a.s1_nparts) v += x[u];
+  }
+  v = block_sum256(v, s_w);
+  if (t == 0) a.s1[0] = v;
+}
+
+// b3: ddot3[k] = relu'(y3[k]) sum_n (Wdot1[k][n] d4[n] + W1[k][n] ddot4[n]):
+// one wave per row k (lane l: columns 8 l .. 8 l + 7, 16-byte loads); the
+// lane's eight ddot4 values are formed here from h and Wdot2.
+__device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
+  const int lane = threadIdx.x & 63, k = 4 * i + (threadIdx.x >> 6);
+  const float *W = a.th + a.off[6] + (int64_t)k * HID + 8 * lane, *Wd = a.tw + a.off[6] + (int64_t)k * HID + 8 * lane;
+  float4 w[2], wd[2], d[2], hv[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    w[h] = reinterpret_cast<const float4*>(W)[h];
+    wd[h] = reinterpret_cast<const float4*>(Wd)[h];
+    d[h] = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
+    hv[h] = reinterpret_cast<const float4*>(a.h + 8 * lane)[h];
+  }
+  const float y3 = a.y3[k];
+  const int act = a.action[a.slot[0]];
+  const float* w2 = a.tw + a.off[8] + (int64_t)(8 * lane) * a.A + act;
+  float g[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) g[q] = w2[q * a.A];
+  float4 dd[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    dd[h] = make_float4(hv[h].x > 0.f ? g[4 * h] : 0.f, hv[h].y > 0.f ? g[4 * h + 1] : 0.f,
+                        hv[h].z > 0.f ? g[4 * h + 2] : 0.f, hv[h].w > 0.f ? g[4 * h + 3] : 0.f);
+  float z = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    z += ((wd[h].x * d[h].x + w[h].x * dd[h].x) + (wd[h].y * d[h].y + w[h].y * dd[h].y)) +
+         ((wd[h].z * d[h].z + w[h].z * dd[h].z) + (wd[h].w * d[h].w + w[h].w * dd[h].w));
+  z = wave_sum(z);
+  if (lane == 0) a.td3[k] = y3 > 0.f ? z : 0.f;
+}
+
+constexpr int HVP_L1_BLOCKS = HVP_T12 + 1 + HVP_B3;  // 1,109
+__global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
+  __shared__ HvpT12Smem s;
+  int i = blockIdx.x;
+  if (i < HVP_T12) {
+    hvp_t12_block(a, i, s);
+    return;
+  }
+  i -= HVP_T12;
+  if (i == 0) {
+    hvp_s1_block(a, &s.r2[0][0]);
+    return;
+  }
+  hvp_b3_block(a, i - 1);
+}
+
+// ---- L2 -----------------------------------------------------------------
+
+// t3 + t4: ty3 = relu'(y3) (bdot3 + conv(y2, Wdot3) + conv(ty2, W3)) for
+// conv3 position p, channels 16 g .. 16 g + 15 (thread (input-channel quad
+// s = t / 16, co) over the 9 taps) — flat rows 16 i .. 16 i + 15, which are
+// fc1 K-chunk i: part[i][n] = sum_j y3[k] Wdot1[k][n] + ty3[k] W1[k][n]
+// (thread t: columns 2t, 2t + 1; whole-row float2 loads issued first).
+__device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, float (*s_r)[17], float* s_ty) {
+  const int t = threadIdx.x, p = i >> 2, g = i & 3;
+  const float *W1 = a.th + a.off[6], *W1d = a.tw + a.off[6];
+  float2 fw[HVP_T4_KC], fwd[HVP_T4_KC];
+  float fy[HVP_T4_KC];
+#pragma unroll
+  for (int j = 0; j < HVP_T4_KC; ++j) {
+    const int k = i * HVP_T4_KC + j;
+    fw[j] = *reinterpret_cast<const float2*>(W1 + (int64_t)k * HID + 2 * t);
+    fwd[j] = *reinterpret_cast<const float2*>(W1d + (int64_t)k * HID + 2 * t);
+    fy[j] = a.y3[k];
+  }
   const int oh = p / C3O, ow = p % C3O, s = t >> 4;
   const int co = 16 * g + (t & 15);
   const float *W = a.th + a.off[4] + co, *Wd = a.tw + a.off[4] + co;
@@ -186,62 +313,26 @@ __global__ __launch_bounds__(256) void hvp_t3_kernel(HvpArgs a) {
     float v = a.tw[a.off[5] + c];
 #pragma unroll
     for (int k = 0; k < 16; ++k) v += s_r[k][t];
-    a.ty3[p * C3CO + c] = a.y3[p * C3CO + c] > 0.f ? v : 0.f;
+    const float ty = a.y3[p * C3CO + c] > 0.f ? v : 0.f;
+    a.ty3[p * C3CO + c] = ty;
+    s_ty[t] = ty;
   }
-}
-
-// 4. fc1 tangent K-chunk partials: part[c][n] = sum_{k in chunk c} y3[k]
-// Wdot1[k][n] + ty3[k] W1[k][n] (thread t: columns 2t, 2t + 1; whole-row
-// float2 loads), and the fc2-level backward tangent ddot4 = relu'(h)
-// Wdot2[:, a] (block 0).
-__global__ __launch_bounds__(256) void hvp_t4_kernel(HvpArgs a) {
-  const int t = threadIdx.x, c = blockIdx.x;
-  const float *W = a.th + a.off[6], *Wd = a.tw + a.off[6];
-  float2 z = make_float2(0.f, 0.f);
+  __syncthreads();
+  float2 zc = make_float2(0.f, 0.f);
 #pragma unroll
   for (int j = 0; j < HVP_T4_KC; ++j) {
-    const int k = c * HVP_T4_KC + j;
-    const float2 w = *reinterpret_cast<const float2*>(W + (int64_t)k * HID + 2 * t);
-    const float2 wd = *reinterpret_cast<const float2*>(Wd + (int64_t)k * HID + 2 * t);
-    const float y = a.y3[k], ty = a.ty3[k];
-    z.x += y * wd.x + ty * w.x;
-    z.y += y * wd.y + ty * w.y;
+    const float ty = s_ty[j];
+    zc.x += fy[j] * fwd[j].x + ty * fw[j].x;
+    zc.y += fy[j] * fwd[j].y + ty * fw[j].y;
   }
-  *reinterpret_cast<float2*>(a.part + (int64_t)c * HID + 2 * t) = z;
-  if (c == 0) {
-    const int act = a.action[a.slot[0]];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int n = t + 256 * h;
-      a.td4[n] = a.h[n] > 0.f ? a.tw[a.off[8] + n * a.A + act] : 0.f;
-    }
-  }
+  *reinterpret_cast<float2*>(a.part + (int64_t)i * HID + 2 * t) = zc;
 }
 
-// 5. ddot3[k] = relu'(y3[k]) sum_n (Wdot1[k][n] d4[n] + W1[k][n] ddot4[n]):
-// one wave per row k (lane l: columns 8 l .. 8 l + 7, 16-byte loads).
-__global__ __launch_bounds__(256) void hvp_b3_kernel(HvpArgs a) {
-  const int lane = threadIdx.x & 63, k = 4 * blockIdx.x + (threadIdx.x >> 6);
-  if (k >= FLAT) return;
-  const float *W = a.th + a.off[6] + (int64_t)k * HID + 8 * lane, *Wd = a.tw + a.off[6] + (int64_t)k * HID + 8 * lane;
-  float z = 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const float4 w = reinterpret_cast<const float4*>(W)[h], wd = reinterpret_cast<const float4*>(Wd)[h];
-    const float4 d = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
-    const float4 dd = reinterpret_cast<const float4*>(a.td4 + 8 * lane)[h];
-    z += ((wd.x * d.x + w.x * dd.x) + (wd.y * d.y + w.y * dd.y)) + ((wd.z * d.z + w.z * dd.z) + (wd.w * d.w + w.w * dd.w));
-  }
-  z = wave_sum(z);
-  if (lane == 0) a.td3[k] = a.y3[k] > 0.f ? z : 0.f;
-}
-
-// 6. ddot2[pix][ci] = relu'(y2) sum_{taps, co} (d3 Wdot3 + ddot3 W3) (the
+// b2: ddot2[pix][ci] = relu'(y2) sum_{taps, co} (d3 Wdot3 + ddot3 W3) (the
 // transposed conv3, stride 1).  Block (pix, 16-channel group g); thread
 // (ci, output-channel quad cs = t % 16): 16-byte W loads along co.
-__global__ __launch_bounds__(256) void hvp_b2_kernel(HvpArgs a) {
-  __shared__ float s_r[16][17];
-  const int t = threadIdx.x, pix = blockIdx.x, g = blockIdx.y;
+__device__ __forceinline__ void hvp_b2_block(const HvpArgs& a, int i, float (*s_r)[17]) {
+  const int t = threadIdx.x, pix = i >> 2, g = i & 3;
   const int ih = pix / C2O, iw = pix % C2O, cs = t & 15, cl = t >> 4, ci = 16 * g + cl;
   // the nine taps' operands loaded together (taps outside the output are
   // clamped to a valid position and skipped in the sum, in tap order)
@@ -276,12 +367,24 @@ __global__ __launch_bounds__(256) void hvp_b2_kernel(HvpArgs a) {
   }
 }
 
-// 7. ddot1[pix][ci] = relu'(y1) sum_{taps, co} (d2 Wdot2 + ddot2 W2) (the
+constexpr int HVP_L2_BLOCKS = HVP_T34 + HVP_B2;  // 520
+__global__ __launch_bounds__(256) void hvp_l2_kernel(HvpArgs a) {
+  __shared__ float s_r[16][17];
+  __shared__ float s_ty[16];
+  const int i = blockIdx.x;
+  if (i < HVP_T34)
+    hvp_t34_block(a, i, s_r, s_ty);
+  else
+    hvp_b2_block(a, i - HVP_T34, s_r);
+}
+
+// ---- L3 -----------------------------------------------------------------
+
+// b1: ddot1[pix][ci] = relu'(y1) sum_{taps, co} (d2 Wdot2 + ddot2 W2) (the
 // transposed conv2, stride 2: at most 2 x 2 live taps).  Block pix; thread
 // (ci = t / 8, output-channel octet cs = t % 8).
-__global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
-  __shared__ float s_r[C2CI][9];
-  const int t = threadIdx.x, pix = blockIdx.x;
+__device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*s_r)[9]) {
+  const int t = threadIdx.x;
   const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
   // the 2 x 2 taps of this pixel's stride phase, every operand loaded before
   // the first product (taps outside the output clamped and skipped, in order)
@@ -320,9 +423,9 @@ __global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
   }
 }
 
-// 8. Every parameter-gradient block of H_q w in one launch, grid in ranges:
+// ---- the parameter-gradient blocks of H_q w (L3 and L4) ------------------
 //   [257] conv1 rows k (row 256 = bias): sum_p x_p[k] ddot1[p][co] over 8
-//         position splits (thread (split, co));
+//         position splits (thread (split, co)) — L4;
 //   [513] conv2 rows, [577] conv3 rows (last row = bias):
 //         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
 //         splits (thread (split, co));
@@ -332,10 +435,9 @@ __global__ __launch_bounds__(256) void hvp_b1_kernel(HvpArgs a) {
 //   [...] fc1: ydot3 (x) d4 + y3 (x) ddot4, 4 elements per thread.
 // Every per-thread sum issues all its loads before the first addition
 // (round 5: the position and chunk loops waited for one round trip per
-// iteration, 13-21 serial trips, and kept this launch at 12.2 us).
+// iteration, 13-21 serial trips, and kept the gradient launch at 12.2 us).
 constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = HID / 64;
 constexpr int HVP_G_FC = FLAT * HID / 4 / 256;  // 1568
-constexpr int HVP_G_BLOCKS = HVP_G_C1 + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC;
 
 template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
@@ -379,43 +481,64 @@ __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y,
   }
 }
 
-__global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
-  __shared__ float s_r[8][64];
-  __shared__ float s_x[C1M];
+// hidden unit n = 64 i + t % 64: hdot, fc2 column, fc1 bias; fc2 bias = 0.
+// Thread (group q, unit n): chunks [49 q, +49) of unit n, summed in chunk
+// order, then the four group sums in group order.
+__device__ __forceinline__ void hvp_g_hidden(const HvpArgs& a, int i, float (*s_r)[64], const HqOut& ho) {
+  constexpr int NG = 4, CG = HVP_T4_CHUNKS / NG;  // 49
+  static_assert(NG * CG == HVP_T4_CHUNKS, "chunk groups");
+  const int t = threadIdx.x, nl = t & 63, q = t >> 6, n = 64 * i + nl;
+  float pv[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) pv[c] = a.part[(int64_t)(CG * q + c) * HID + n];
+  float zq = 0.f;
+#pragma unroll
+  for (int c = 0; c < CG; ++c) zq += pv[c];
+  s_r[q][nl] = zq;
+  __syncthreads();
+  if (q != 0) return;
+  const int act = a.action[a.slot[0]];
+  const float z = a.tw[a.off[7] + n] + ((s_r[0][nl] + s_r[1][nl]) + (s_r[2][nl] + s_r[3][nl]));
+  const float hd = a.h[n] > 0.f ? z : 0.f;
+  for (int col = 0; col < a.A; ++col) ho.put(a, a.off[8] + (int64_t)n * a.A + col, col == act ? hd : 0.f);
+  ho.put(a, a.off[7] + n, a.td4[n]);
+  if (i == 0 && t < a.A) ho.put(a, a.off[9] + t, 0.f);
+}
+
+// fc1 rows: 4 consecutive columns per thread.
+__device__ __forceinline__ void hvp_g_fc1(const HvpArgs& a, int i, const HqOut& ho) {
   const int t = threadIdx.x;
-  const HqOut ho(a);
+  const int64_t e = ((int64_t)i * 256 + t) * 4;
+  const int k = (int)(e / HID), n = (int)(e % HID);
+  const float ty = a.ty3[k], y = a.y3[k];
+  const float4 d = *reinterpret_cast<const float4*>(a.d4 + n);
+  const float4 dd = *reinterpret_cast<const float4*>(a.td4 + n);
+  const float4 hq = make_float4(ty * d.x + y * dd.x, ty * d.y + y * dd.y, ty * d.z + y * dd.z, ty * d.w + y * dd.w);
+  if (a.vout) {
+    const int64_t j = a.off[6] + e;
+    const float4 vd = *reinterpret_cast<const float4*>(a.vdir + j);
+    const float4 jj = *reinterpret_cast<const float4*>(a.J + j);
+    const float4 g = *reinterpret_cast<const float4*>(a.gq + j);
+    *reinterpret_cast<float4*>(a.vout + j) =
+        make_float4(vd.x + jj.x * (ho.a_s1 * g.x - ho.clip * hq.x), vd.y + jj.y * (ho.a_s1 * g.y - ho.clip * hq.y),
+                    vd.z + jj.z * (ho.a_s1 * g.z - ho.clip * hq.z), vd.w + jj.w * (ho.a_s1 * g.w - ho.clip * hq.w));
+  } else {
+    *reinterpret_cast<float4*>(a.hq + a.off[6] + e) = hq;
+  }
+}
+
+// L3: b1 first (L4 waits on it), then every gradient block that does not
+// need ddot1.
+constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC;  // 3,066
+__global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
+  __shared__ float s_r[8][64];
   int i = blockIdx.x;
-  if (i < HVP_G_C1) {  // conv1: thread (split = t / 32 of 50 positions, co)
-    // the row's 400 patch values x_p[k] staged once (a loop of scattered
-    // byte loads per thread was 11 of this launch's 20 us)
-    const int k = i, co = t & 31, sp = t >> 5;
-    float tv[50];  // this thread's ddot1 column, loaded before the staging
-#pragma unroll
-    for (int j = 0; j < 50; ++j) tv[j] = a.td1[(50 * sp + j) * C1CO + co];
-    if (k < C1KK) {
-      const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
-      const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
-      const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
-      for (int p = t; p < C1M; p += 256)
-        s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
-    } else {
-      for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
-    }
-    __syncthreads();
-    float g = 0.f;
-#pragma unroll
-    for (int j = 0; j < 50; ++j) g += s_x[50 * sp + j] * tv[j];
-    s_r[sp][co] = g;
-    __syncthreads();
-    if (t < C1CO) {
-      float v = 0.f;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) v += s_r[s][t];
-      ho.put(a, a.off[0] + (int64_t)k * C1CO + t, v);  // row 256 is the bias (off[1] = off[0] + 8192)
-    }
+  if (i < C1M) {
+    hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
     return;
   }
-  i -= HVP_G_C1;
+  i -= C1M;
+  const HqOut ho(a);
   if (i < HVP_G_C2) {
     hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i, a.off[2], a.off[3], s_r, ho);
     return;
@@ -426,55 +549,50 @@ __global__ __launch_bounds__(256) void hvp_g_kernel(HvpArgs a) {
     return;
   }
   i -= HVP_G_C3;
-  if (i < HVP_G_H) {  // hidden unit n: hdot, fc2 column, fc1 bias; fc2 bias = 0
-    // thread (group q, unit n): chunks [49 q, +49) of unit n, summed in
-    // chunk order, then the four group sums in group order
-    constexpr int NG = 4, CG = HVP_T4_CHUNKS / NG;  // 49
-    static_assert(NG * CG == HVP_T4_CHUNKS, "chunk groups");
-    const int nl = t & 63, q = t >> 6, n = 64 * i + nl;
-    float pv[CG];
-#pragma unroll
-    for (int c = 0; c < CG; ++c) pv[c] = a.part[(int64_t)(CG * q + c) * HID + n];
-    float zq = 0.f;
-#pragma unroll
-    for (int c = 0; c < CG; ++c) zq += pv[c];
-    s_r[q][nl] = zq;
-    __syncthreads();
-    if (q != 0) return;
-    const int act = a.action[a.slot[0]];
-    const float z = a.tw[a.off[7] + n] + ((s_r[0][nl] + s_r[1][nl]) + (s_r[2][nl] + s_r[3][nl]));
-    const float hd = a.h[n] > 0.f ? z : 0.f;
-    for (int col = 0; col < a.A; ++col) ho.put(a, a.off[8] + (int64_t)n * a.A + col, col == act ? hd : 0.f);
-    ho.put(a, a.off[7] + n, a.td4[n]);
-    if (i == 0 && t < a.A) ho.put(a, a.off[9] + t, 0.f);
+  if (i < HVP_G_H) {
+    hvp_g_hidden(a, i, s_r, ho);
     return;
   }
-  i -= HVP_G_H;
-  {  // fc1 rows: 4 consecutive columns per thread
-    const int64_t e = ((int64_t)i * 256 + t) * 4;
-    const int k = (int)(e / HID), n = (int)(e % HID);
-    const float ty = a.ty3[k], y = a.y3[k];
-    const float4 d = *reinterpret_cast<const float4*>(a.d4 + n);
-    const float4 dd = *reinterpret_cast<const float4*>(a.td4 + n);
-    const float4 hq =
-        make_float4(ty * d.x + y * dd.x, ty * d.y + y * dd.y, ty * d.z + y * dd.z, ty * d.w + y * dd.w);
-    if (a.vout) {
-      const int64_t j = a.off[6] + e;
-      const float4 vd = *reinterpret_cast<const float4*>(a.vdir + j);
-      const float4 jj = *reinterpret_cast<const float4*>(a.J + j);
-      const float4 g = *reinterpret_cast<const float4*>(a.gq + j);
-      *reinterpret_cast<float4*>(a.vout + j) =
-          make_float4(vd.x + jj.x * (ho.a_s1 * g.x - ho.clip * hq.x), vd.y + jj.y * (ho.a_s1 * g.y - ho.clip * hq.y),
-                      vd.z + jj.z * (ho.a_s1 * g.z - ho.clip * hq.z), vd.w + jj.w * (ho.a_s1 * g.w - ho.clip * hq.w));
-    } else {
-      *reinterpret_cast<float4*>(a.hq + a.off[6] + e) = hq;
-    }
+  hvp_g_fc1(a, i - HVP_G_H, ho);
+}
+
+// L4: conv1 row k (thread (split = t / 32 of 50 positions, co)).  The row's
+// 400 patch values x_p[k] are staged once (a loop of scattered byte loads
+// per thread was 11 of the gradient launch's 20 us in round 4).
+__global__ __launch_bounds__(256) void hvp_g1_kernel(HvpArgs a) {
+  __shared__ float s_r[8][C1CO];
+  __shared__ float s_x[C1M];
+  const int t = threadIdx.x, k = blockIdx.x, co = t & 31, sp = t >> 5;
+  const HqOut ho(a);
+  float tv[50];  // this thread's ddot1 column, loaded before the staging
+#pragma unroll
+  for (int j = 0; j < 50; ++j) tv[j] = a.td1[(50 * sp + j) * C1CO + co];
+  if (k < C1KK) {
+    const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
+    const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
+    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
+    for (int p = t; p < C1M; p += 256)
+      s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
+  } else {
+    for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
+  }
+  __syncthreads();
+  float g = 0.f;
+#pragma unroll
+  for (int j = 0; j < 50; ++j) g += s_x[50 * sp + j] * tv[j];
+  s_r[sp][co] = g;
+  __syncthreads();
+  if (t < C1CO) {
+    float v = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v += s_r[s][t];
+    ho.put(a, a.off[0] + (int64_t)k * C1CO + t, v);  // row 256 is the bias (off[1] = off[0] + 8192)
   }
 }
 
 // The second order's elementwise stages run in gradient epilogues: the
 // u' / v_dir / w pieces in the one-transition backward's (common.hpp
-// Rms::meta3), v = v_dir + J (alpha s1 grad q - clip(td') H_q w) in
-// hvp_g_kernel's (HqOut).
+// Rms::meta3), v = v_dir + J (alpha s1 grad q - clip(td') H_q w) in the
+// gradient blocks' (HqOut).
 
 }  // namespace dqz

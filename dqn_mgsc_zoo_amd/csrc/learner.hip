@@ -1339,16 +1339,12 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hv.td = L1->td;
     hv.bound = H->cfg.grad_error_bound;
     hv.vout = H->thp;
-    // eight dependent stages (hvp.hpp): tangent forward, tangent backward,
-    // then every parameter block of H_q w
-    hipLaunchKernelGGL(hvp_t1_kernel, dim3(C1M + 1), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t2_kernel, dim3(C2M, C2CO / 16), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t3_kernel, dim3(C3M, C3CO / 16), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_t4_kernel, dim3(HVP_T4_CHUNKS), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b3_kernel, dim3(FLAT / 4), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b2_kernel, dim3(C2M, C2CO / 16), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_b1_kernel, dim3(C1M), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_g_kernel, dim3(HVP_G_BLOCKS), dim3(256), 0, st, hv);
+    // four launches (hvp.hpp): the tangent forward and backward side by
+    // side, then the parameter blocks of H_q w (conv1's last)
+    hipLaunchKernelGGL(hvp_l1_kernel, dim3(HVP_L1_BLOCKS), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_l2_kernel, dim3(HVP_L2_BLOCKS), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_l3_kernel, dim3(HVP_L3_BLOCKS), dim3(256), 0, st, hv);
+    hipLaunchKernelGGL(hvp_g1_kernel, dim3(HVP_G_C1), dim3(256), 0, st, hv);
     DQZ_HIP(hipGetLastError());
     nloss = nparts1;
   }
