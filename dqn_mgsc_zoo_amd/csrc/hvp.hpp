@@ -10,7 +10,7 @@
 //   d/deps grad     dW_l = sum_p (ydot_{l-1} (x) d_l + y_{l-1} (x) ddot_l), db_l = sum_p ddot_l,
 // with d_l the unit-cotangent backward signals of q[a] (d_5 = e_a).
 //
-// Four launches.  The tangent forward (t1 .. t4) and the tangent backward
+// Three launches.  The tangent forward (t1 .. t4) and the tangent backward
 // (b3 .. b1) are independent chains: b3 needs only the primal d4, the
 // tangent weights and ddot4 = relu'(h) Wdot2[:, a], which each b3 wave forms
 // from eight gathers.  So the chains run side by side, and two more stage
@@ -20,9 +20,8 @@
 //                     s1 and ddot4 | b3
 //   L2 hvp_l2_kernel  t34 (conv3 block (p, g) = fc1 K-chunk 4 p + g: the 16
 //                     conv3 outputs it forms are the chunk's 16 rows) | b2
-//   L3 hvp_l3_kernel  b1 | every parameter block of H_q w but conv1's
-//   L4 hvp_g1_kernel  conv1's parameter blocks (the only ones that need all
-//                     of ddot1).
+//   L3 hvp_l3_kernel  b1 | every parameter block of H_q w, conv1's last:
+//                     they need all of ddot1 and wait for it in-launch.
 // Round 5 ran eight launches, one per dependent stage, each ≈ 5.1 us
 // (rocprofv3) for a few microseconds of latency.  Every per-element sum
 // keeps the order of that form.  Each stage splits its reduction over the
@@ -64,6 +63,9 @@ struct HvpArgs {
   const float *vdir, *J, *gq, *td;
   float bound;
   float* vout;
+  // ddot1 complete: the 400 b1 blocks arrive, the 257 conv1 parameter
+  // blocks at the end of the same launch wait (sample word 0)
+  Handoff td1_pub;
 };
 
 // One element of the gradient blocks' output: H_q w itself, or meta_combine's v.
@@ -89,7 +91,7 @@ struct HqOut {
 constexpr int HVP_T4_KC = 16, HVP_T4_CHUNKS = FLAT / HVP_T4_KC;  // 196 chunks of 16 rows
 constexpr int HVP_T12 = C2M * (C2CO / 16);                       // 324: (conv2 position, 16-channel group)
 constexpr int HVP_T34 = C3M * (C3CO / 16);                       // 196: (conv3 position, 16-channel group)
-constexpr int HVP_B3 = FLAT / 4;                                 // 784: 4 fc1 rows each
+constexpr int HVP_B3 = FLAT / 16;                                // 196: 16 fc1 rows each
 constexpr int HVP_B2 = C2M * (C2CO / 16);                        // 324: (conv2 position, 16-channel group)
 static_assert(HVP_T34 == HVP_T4_CHUNKS, "conv3 block i forms fc1 chunk i's rows");
 
@@ -224,20 +226,30 @@ __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
 }
 
 // b3: ddot3[k] = relu'(y3[k]) sum_n (Wdot1[k][n] d4[n] + W1[k][n] ddot4[n]):
-// one wave per row k (lane l: columns 8 l .. 8 l + 7, 16-byte loads); the
-// lane's eight ddot4 values are formed here from h and Wdot2.
+// 16 rows per block, wave w rows 16 i + 4 w .. + 3 (lane l: columns 8 l ..
+// 8 l + 7, 16-byte loads, all four rows' loads issued together); the lane's
+// eight ddot4 values are formed here from h and Wdot2.
 __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
-  const int lane = threadIdx.x & 63, k = 4 * i + (threadIdx.x >> 6);
-  const float *W = a.th + a.off[6] + (int64_t)k * HID + 8 * lane, *Wd = a.tw + a.off[6] + (int64_t)k * HID + 8 * lane;
-  float4 w[2], wd[2], d[2], hv[2];
+  constexpr int R = 4;
+  const int lane = threadIdx.x & 63, k0 = 16 * i + R * (threadIdx.x >> 6);
+  float4 w[R][2], wd[R][2], d[2], hv[2];
+  float y3[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float *W = a.th + a.off[6] + (int64_t)(k0 + r) * HID + 8 * lane,
+                *Wd = a.tw + a.off[6] + (int64_t)(k0 + r) * HID + 8 * lane;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      w[r][h] = reinterpret_cast<const float4*>(W)[h];
+      wd[r][h] = reinterpret_cast<const float4*>(Wd)[h];
+    }
+    y3[r] = a.y3[k0 + r];
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    w[h] = reinterpret_cast<const float4*>(W)[h];
-    wd[h] = reinterpret_cast<const float4*>(Wd)[h];
     d[h] = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
     hv[h] = reinterpret_cast<const float4*>(a.h + 8 * lane)[h];
   }
-  const float y3 = a.y3[k];
   const int act = a.action[a.slot[0]];
   const float* w2 = a.tw + a.off[8] + (int64_t)(8 * lane) * a.A + act;
   float g[8];
@@ -248,16 +260,19 @@ __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
   for (int h = 0; h < 2; ++h)
     dd[h] = make_float4(hv[h].x > 0.f ? g[4 * h] : 0.f, hv[h].y > 0.f ? g[4 * h + 1] : 0.f,
                         hv[h].z > 0.f ? g[4 * h + 2] : 0.f, hv[h].w > 0.f ? g[4 * h + 3] : 0.f);
-  float z = 0.f;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-    z += ((wd[h].x * d[h].x + w[h].x * dd[h].x) + (wd[h].y * d[h].y + w[h].y * dd[h].y)) +
-         ((wd[h].z * d[h].z + w[h].z * dd[h].z) + (wd[h].w * d[h].w + w[h].w * dd[h].w));
-  z = wave_sum(z);
-  if (lane == 0) a.td3[k] = y3 > 0.f ? z : 0.f;
+  for (int r = 0; r < R; ++r) {
+    float z = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      z += ((wd[r][h].x * d[h].x + w[r][h].x * dd[h].x) + (wd[r][h].y * d[h].y + w[r][h].y * dd[h].y)) +
+           ((wd[r][h].z * d[h].z + w[r][h].z * dd[h].z) + (wd[r][h].w * d[h].w + w[r][h].w * dd[h].w));
+    z = wave_sum(z);
+    if (lane == 0) a.td3[k0 + r] = y3[r] > 0.f ? z : 0.f;
+  }
 }
 
-constexpr int HVP_L1_BLOCKS = HVP_T12 + 1 + HVP_B3;  // 1,109
+constexpr int HVP_L1_BLOCKS = HVP_T12 + 1 + HVP_B3;  // 521
 __global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
   __shared__ HvpT12Smem s;
   int i = blockIdx.x;
@@ -419,13 +434,14 @@ __device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += s_r[t][k];
-    a.td1[pix * C1CO + t] = a.y1[pix * C1CO + t] > 0.f ? v : 0.f;
+    store_sc1_f1(a.td1, C1M * C1CO * 4, pix * C1CO + t, a.y1[pix * C1CO + t] > 0.f ? v : 0.f);
   }
+  a.td1_pub.arrive(0);
 }
 
-// ---- the parameter-gradient blocks of H_q w (L3 and L4) ------------------
+// ---- the parameter-gradient blocks of H_q w (L3) -------------------------
 //   [257] conv1 rows k (row 256 = bias): sum_p x_p[k] ddot1[p][co] over 8
-//         position splits (thread (split, co)) — L4;
+//         position splits (thread (split, co)), last;
 //   [513] conv2 rows, [577] conv3 rows (last row = bias):
 //         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
 //         splits (thread (split, co));
@@ -527,11 +543,45 @@ __device__ __forceinline__ void hvp_g_fc1(const HvpArgs& a, int i, const HqOut& 
   }
 }
 
-// L3: b1 first (L4 waits on it), then every gradient block that does not
-// need ddot1.
-constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC;  // 3,066
+// conv1 row k (thread (split = t / 32 of 50 positions, co)).  The row's
+// 400 patch values x_p[k] are staged before the wait for ddot1 (a loop of
+// scattered byte loads per thread was 11 of the gradient launch's 20 us in
+// round 4), ddot1 is read with sc1 loads after it.
+__device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r)[64], float* s_x, const HqOut& ho) {
+  const int t = threadIdx.x, co = t & 31, sp = t >> 5;
+  if (k < C1KK) {
+    const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
+    const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
+    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
+    for (int p = t; p < C1M; p += 256)
+      s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
+  } else {
+    for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
+  }
+  a.td1_pub.wait(0);  // its barrier also publishes s_x
+  float tv[50];       // this thread's ddot1 column
+#pragma unroll
+  for (int j = 0; j < 50; ++j) tv[j] = load_sc1_f1(a.td1, C1M * C1CO * 4, (50 * sp + j) * C1CO + co);
+  float g = 0.f;
+#pragma unroll
+  for (int j = 0; j < 50; ++j) g += s_x[50 * sp + j] * tv[j];
+  s_r[sp][co] = g;
+  __syncthreads();
+  if (t < C1CO) {
+    float v = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v += s_r[s][t];
+    ho.put(a, a.off[0] + (int64_t)k * C1CO + t, v);  // row 256 is the bias (off[1] = off[0] + 8192)
+  }
+}
+
+// L3: b1 first, then every gradient block that does not need ddot1, then
+// conv1's, which wait in-launch for the 400 b1 blocks (all dispatched before
+// any of them on every XCD, so the wait cannot hold a b1 block out).
+constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC + HVP_G_C1;  // 3,323
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
+  __shared__ float s_x[C1M];
   int i = blockIdx.x;
   if (i < C1M) {
     hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
@@ -553,41 +603,12 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
     hvp_g_hidden(a, i, s_r, ho);
     return;
   }
-  hvp_g_fc1(a, i - HVP_G_H, ho);
-}
-
-// L4: conv1 row k (thread (split = t / 32 of 50 positions, co)).  The row's
-// 400 patch values x_p[k] are staged once (a loop of scattered byte loads
-// per thread was 11 of the gradient launch's 20 us in round 4).
-__global__ __launch_bounds__(256) void hvp_g1_kernel(HvpArgs a) {
-  __shared__ float s_r[8][C1CO];
-  __shared__ float s_x[C1M];
-  const int t = threadIdx.x, k = blockIdx.x, co = t & 31, sp = t >> 5;
-  const HqOut ho(a);
-  float tv[50];  // this thread's ddot1 column, loaded before the staging
-#pragma unroll
-  for (int j = 0; j < 50; ++j) tv[j] = a.td1[(50 * sp + j) * C1CO + co];
-  if (k < C1KK) {
-    const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
-    const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
-    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
-    for (int p = t; p < C1M; p += 256)
-      s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
-  } else {
-    for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
+  i -= HVP_G_H;
+  if (i < HVP_G_FC) {
+    hvp_g_fc1(a, i, ho);
+    return;
   }
-  __syncthreads();
-  float g = 0.f;
-#pragma unroll
-  for (int j = 0; j < 50; ++j) g += s_x[50 * sp + j] * tv[j];
-  s_r[sp][co] = g;
-  __syncthreads();
-  if (t < C1CO) {
-    float v = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v += s_r[s][t];
-    ho.put(a, a.off[0] + (int64_t)k * C1CO + t, v);  // row 256 is the bias (off[1] = off[0] + 8192)
-  }
+  hvp_g_conv1(a, i - HVP_G_FC, s_r, s_x, ho);
 }
 
 // The second order's elementwise stages run in gradient epilogues: the

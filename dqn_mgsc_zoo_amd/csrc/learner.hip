@@ -1113,7 +1113,8 @@ struct dqz_meta {
   float *GQ, *HQ, *s1_part, *hpart;
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
   float* dotp;  // [C][META_DOT_SLOTS] the tangent launch's dot-product partials (one chunk)
-  int* arrive;  // meta_adam_chunks_kernel's re-seed arrival counter (zero between launches)
+  int* arrive;  // [0] meta_adam_chunks_kernel's re-seed arrival counter, [kStride, 3 kStride) the
+                // HVP's ddot1 hand-off words (all zero between launches)
   int nparts2;
   void* block;
 };
@@ -1160,7 +1161,7 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
                            so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID,
-                           (int64_t)C * META_DOT_SLOTS, 64};
+                           (int64_t)C * META_DOT_SLOTS, 3 * Handoff::kStride};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
@@ -1339,12 +1340,15 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     hv.td = L1->td;
     hv.bound = H->cfg.grad_error_bound;
     hv.vout = H->thp;
-    // four launches (hvp.hpp): the tangent forward and backward side by
-    // side, then the parameter blocks of H_q w (conv1's last)
+    // ddot1's in-launch hand-off: words after the Adam re-seed counter, the
+    // one-transition learner's error word (dqz_learner_sync_status)
+    hv.td1_pub = Handoff{H->arrive + Handoff::kStride, H->arrive + 2 * Handoff::kStride,
+                         L1->sync + 16 * Handoff::kStride, C1M, HVP_G_C1, L1->spin_max};
+    // three launches (hvp.hpp): the tangent forward and backward side by
+    // side, then the parameter blocks of H_q w
     hipLaunchKernelGGL(hvp_l1_kernel, dim3(HVP_L1_BLOCKS), dim3(256), 0, st, hv);
     hipLaunchKernelGGL(hvp_l2_kernel, dim3(HVP_L2_BLOCKS), dim3(256), 0, st, hv);
     hipLaunchKernelGGL(hvp_l3_kernel, dim3(HVP_L3_BLOCKS), dim3(256), 0, st, hv);
-    hipLaunchKernelGGL(hvp_g1_kernel, dim3(HVP_G_C1), dim3(256), 0, st, hv);
     DQZ_HIP(hipGetLastError());
     nloss = nparts1;
   }
