@@ -118,8 +118,21 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
   const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
-  // the thread's 32 conv1 tangent weights, its two window outputs' y1 and
-  // its conv2 operands: in flight under the slot -> frame-index -> frame chain
+  // the slot -> frame-index -> frame chain first (three dependent trips),
+  // then the thread's 32 conv1 tangent weights, its two window outputs' y1
+  // and its conv2 operands, in flight under the chain's last trip (no
+  // branch among the loads: a branch made the compiler drain them all)
+  const int f = a.fidx[(int64_t)a.slot[0] * 8 + (t & 3)];
+  constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600 tile elements, 7 rounds
+  unsigned xb[R];
+  {
+    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB + C1S * 2 * oh * FW + C1S * 2 * ow;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int px = min(t + 256 * u, N - 1) >> 2;  // element e = pixel * 4 + channel, channel = t % 4
+      xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
+    }
+  }
   const float* W1d = a.tw + a.off[0];
   float wv[C1K * FC];
 #pragma unroll
@@ -142,20 +155,10 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
     wd[ci] = Wd[ci * C2CO];
     w[ci] = W[ci * C2CO];
   }
-  const float y2v = t < 16 ? a.y2[p * C2CO + c2] : 0.f;
-  const float b2v = t < 16 ? a.tw[a.off[3] + c2] : 0.f;
+  const float y2v = a.y2[p * C2CO + c2];  // used by t < 16
+  const float b2v = a.tw[a.off[3] + c2];
   const float b1v = a.tw[a.off[1] + co];
-  // the input tile: element e = pixel * 4 + channel, channel = t % 4
   {
-    const int f = a.fidx[(int64_t)a.slot[0] * 8 + (t & 3)];
-    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB + C1S * 2 * oh * FW + C1S * 2 * ow;
-    constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600, 7 rounds
-    unsigned xb[R];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const int px = min(t + 256 * u, N - 1) >> 2;
-      xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
-    }
     float* in = reinterpret_cast<float*>(s.in);
 #pragma unroll
     for (int u = 0; u < R; ++u)
@@ -232,6 +235,8 @@ __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
 __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
   constexpr int R = 4;
   const int lane = threadIdx.x & 63, k0 = 16 * i + R * (threadIdx.x >> 6);
+  // the slot -> action chain first, the rows' loads under its second trip
+  const int act = a.action[a.slot[0]];
   float4 w[R][2], wd[R][2], d[2], hv[2];
   float y3[R];
 #pragma unroll
@@ -250,7 +255,6 @@ __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
     d[h] = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
     hv[h] = reinterpret_cast<const float4*>(a.h + 8 * lane)[h];
   }
-  const int act = a.action[a.slot[0]];
   const float* w2 = a.tw + a.off[8] + (int64_t)(8 * lane) * a.A + act;
   float g[8];
 #pragma unroll
