@@ -34,6 +34,15 @@
 #pragma once
 #include "common.hpp"
 
+// Timing-only builds (tools/gpu_hvp_split.sh): DQZ_EXP_HVP_SKIP is a mask of
+// block ranges that return at once (1 t12, 2 b3, 4 b1's sums — its arrival
+// stays, 8 conv2 / conv3 parameter rows, 16 fc1 parameters, 32 conv1
+// parameter rows, 64 t34, 128 b2).  The numerics of those builds are wrong
+// by design.
+#ifndef DQZ_EXP_HVP_SKIP
+#define DQZ_EXP_HVP_SKIP 0
+#endif
+
 namespace dqz {
 
 struct HvpArgs {
@@ -115,6 +124,7 @@ struct HvpT12Smem {
 // by one block: channel group 0 of the conv2 position oh = min(ih / 2, 8),
 // ow = min(iw / 2, 8).
 __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Smem& s) {
+  if (DQZ_EXP_HVP_SKIP & 1) return;
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
   const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
@@ -233,6 +243,7 @@ __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
 // 8 l + 7, 16-byte loads, all four rows' loads issued together); the lane's
 // eight ddot4 values are formed here from h and Wdot2.
 __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
+  if (DQZ_EXP_HVP_SKIP & 2) return;
   constexpr int R = 4;
   const int lane = threadIdx.x & 63, k0 = 16 * i + R * (threadIdx.x >> 6);
   // the slot -> action chain first, the rows' loads under its second trip
@@ -300,6 +311,7 @@ __global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
 // fc1 K-chunk i: part[i][n] = sum_j y3[k] Wdot1[k][n] + ty3[k] W1[k][n]
 // (thread t: columns 2t, 2t + 1; whole-row float2 loads issued first).
 __device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, float (*s_r)[17], float* s_ty) {
+  if (DQZ_EXP_HVP_SKIP & 64) return;
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
   const float *W1 = a.th + a.off[6], *W1d = a.tw + a.off[6];
   float2 fw[HVP_T4_KC], fwd[HVP_T4_KC];
@@ -351,6 +363,7 @@ __device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, float (*s
 // transposed conv3, stride 1).  Block (pix, 16-channel group g); thread
 // (ci, output-channel quad cs = t % 16): 16-byte W loads along co.
 __device__ __forceinline__ void hvp_b2_block(const HvpArgs& a, int i, float (*s_r)[17]) {
+  if (DQZ_EXP_HVP_SKIP & 128) return;
   const int t = threadIdx.x, pix = i >> 2, g = i & 3;
   const int ih = pix / C2O, iw = pix % C2O, cs = t & 15, cl = t >> 4, ci = 16 * g + cl;
   // the nine taps' operands loaded together (taps outside the output are
@@ -403,6 +416,10 @@ __global__ __launch_bounds__(256) void hvp_l2_kernel(HvpArgs a) {
 // transposed conv2, stride 2: at most 2 x 2 live taps).  Block pix; thread
 // (ci = t / 8, output-channel octet cs = t % 8).
 __device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*s_r)[9]) {
+  if (DQZ_EXP_HVP_SKIP & 4) {
+    a.td1_pub.arrive(0);
+    return;
+  }
   const int t = threadIdx.x;
   const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
   // the 2 x 2 taps of this pixel's stride phase, every operand loaded before
@@ -463,6 +480,7 @@ template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
                                                const float* dd, int k, int64_t off_w, int64_t off_b, float (*s_r)[64],
                                                const HqOut& ho) {
+  if (DQZ_EXP_HVP_SKIP & 8) return;
   const int t = threadIdx.x, co = t & 63, sp = t >> 6;  // 4 position splits
   constexpr int P = OH * OH, PS = (P + 3) / 4;
   const int p0 = sp * PS;
@@ -527,6 +545,7 @@ __device__ __forceinline__ void hvp_g_hidden(const HvpArgs& a, int i, float (*s_
 
 // fc1 rows: 4 consecutive columns per thread.
 __device__ __forceinline__ void hvp_g_fc1(const HvpArgs& a, int i, const HqOut& ho) {
+  if (DQZ_EXP_HVP_SKIP & 16) return;
   const int t = threadIdx.x;
   const int64_t e = ((int64_t)i * 256 + t) * 4;
   const int k = (int)(e / HID), n = (int)(e % HID);
@@ -552,6 +571,7 @@ __device__ __forceinline__ void hvp_g_fc1(const HvpArgs& a, int i, const HqOut& 
 // scattered byte loads per thread was 11 of the gradient launch's 20 us in
 // round 4), ddot1 is read with sc1 loads after it.
 __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r)[64], float* s_x, const HqOut& ho) {
+  if (DQZ_EXP_HVP_SKIP & 32) return;
   const int t = threadIdx.x, co = t & 31, sp = t >> 5;
   if (k < C1KK) {
     const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
