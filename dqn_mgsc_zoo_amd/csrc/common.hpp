@@ -182,7 +182,7 @@ struct Rms {
 // every workgroup records s_memrealtime (100 MHz, chip-wide) at named points;
 // tools/trace_step.py reads them back with dqz_debug_trace().
 #ifdef DQZ_TRACE
-constexpr int TRACE_KERNELS = 16, TRACE_BLOCKS = 4096, TRACE_SLOTS = 4;
+constexpr int TRACE_KERNELS = 20, TRACE_BLOCKS = 4096, TRACE_SLOTS = 4;
 __device__ unsigned long long g_dqz_trace[TRACE_KERNELS * TRACE_BLOCKS * TRACE_SLOTS];
 #define DQZ_STAMP(kid, slot)                                                                              \
   do {                                                                                                    \

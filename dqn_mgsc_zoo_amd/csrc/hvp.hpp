@@ -175,6 +175,7 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
       if (t + 256 * u < N) in[t + 256 * u] = f < 0 ? 0.f : u8n(xb[u]);
   }
   __syncthreads();
+  DQZ_STAMP(16, 1);
 #pragma unroll 4
   for (int pos = 0; pos < 16; ++pos) {
     const float4* row = s.in + (4 * (pos >> 2) + kh) * T12_IN + 4 * (pos & 3);
@@ -201,6 +202,7 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
     if (g == 0 && (dy < 2 || oh == C2O - 1) && (dx < 2 || ow == C2O - 1)) a.ty1[p1[h] * C1CO + co] = ty;
   }
   __syncthreads();
+  DQZ_STAMP(16, 2);
   float z = 0.f;
 #pragma unroll
   for (int ci = 0; ci < C2CI; ++ci) z += y[ci] * wd[ci] + s.t1[tap][ci] * w[ci];
@@ -290,17 +292,15 @@ __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
 constexpr int HVP_L1_BLOCKS = HVP_T12 + 1 + HVP_B3;  // 521
 __global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
   __shared__ HvpT12Smem s;
-  int i = blockIdx.x;
-  if (i < HVP_T12) {
+  const int i = blockIdx.x;
+  DQZ_STAMP(16, 0);
+  if (i < HVP_T12)
     hvp_t12_block(a, i, s);
-    return;
-  }
-  i -= HVP_T12;
-  if (i == 0) {
+  else if (i == HVP_T12)
     hvp_s1_block(a, &s.r2[0][0]);
-    return;
-  }
-  hvp_b3_block(a, i - 1);
+  else
+    hvp_b3_block(a, i - HVP_T12 - 1);
+  DQZ_STAMP(16, 3);
 }
 
 // ---- L2 -----------------------------------------------------------------
@@ -339,6 +339,7 @@ __device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, float (*s
   }
   s_r[s][t & 15] = z;
   __syncthreads();
+  DQZ_STAMP(17, 1);
   if (t < 16) {
     const int c = 16 * g + t;
     float v = a.tw[a.off[5] + c];
@@ -404,10 +405,12 @@ __global__ __launch_bounds__(256) void hvp_l2_kernel(HvpArgs a) {
   __shared__ float s_r[16][17];
   __shared__ float s_ty[16];
   const int i = blockIdx.x;
+  DQZ_STAMP(17, 0);
   if (i < HVP_T34)
     hvp_t34_block(a, i, s_r, s_ty);
   else
     hvp_b2_block(a, i - HVP_T34, s_r);
+  DQZ_STAMP(17, 3);
 }
 
 // ---- L3 -----------------------------------------------------------------
@@ -582,7 +585,9 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
   } else {
     for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
   }
+  DQZ_STAMP(18, 1);
   a.td1_pub.wait(0);  // its barrier also publishes s_x
+  DQZ_STAMP(18, 2);
   float tv[50];       // this thread's ddot1 column
 #pragma unroll
   for (int j = 0; j < 50; ++j) tv[j] = load_sc1_f1(a.td1, C1M * C1CO * 4, (50 * sp + j) * C1CO + co);
@@ -606,33 +611,25 @@ constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC + H
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-  int i = blockIdx.x;
-  if (i < C1M) {
+  constexpr int G2 = C1M, G3 = G2 + HVP_G_C2, GH = G3 + HVP_G_C3, GF = GH + HVP_G_H, G1 = GF + HVP_G_FC;
+  const int i = blockIdx.x;
+  DQZ_STAMP(18, 0);
+  if (i < G2) {
     hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
-    return;
+  } else {
+    const HqOut ho(a);
+    if (i < G3)
+      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
+    else if (i < GH)
+      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
+    else if (i < GF)
+      hvp_g_hidden(a, i - GH, s_r, ho);
+    else if (i < G1)
+      hvp_g_fc1(a, i - GF, ho);
+    else
+      hvp_g_conv1(a, i - G1, s_r, s_x, ho);
   }
-  i -= C1M;
-  const HqOut ho(a);
-  if (i < HVP_G_C2) {
-    hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i, a.off[2], a.off[3], s_r, ho);
-    return;
-  }
-  i -= HVP_G_C2;
-  if (i < HVP_G_C3) {
-    hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i, a.off[4], a.off[5], s_r, ho);
-    return;
-  }
-  i -= HVP_G_C3;
-  if (i < HVP_G_H) {
-    hvp_g_hidden(a, i, s_r, ho);
-    return;
-  }
-  i -= HVP_G_H;
-  if (i < HVP_G_FC) {
-    hvp_g_fc1(a, i, ho);
-    return;
-  }
-  hvp_g_conv1(a, i - HVP_G_FC, s_r, s_x, ho);
+  DQZ_STAMP(18, 3);
 }
 
 // The second order's elementwise stages run in gradient epilogues: the

@@ -27,7 +27,7 @@ from dqn_mgsc_zoo_amd import _native, learner as learner_lib, networks, syntheti
 NAMES = {10: 'sample', 0: 'conv1_fwd', 1: 'conv2_fwd', 2: 'conv3_fwd', 3: 'fc1_fwd', 4: 'head', 5: 'fc1_dx',
          6: 'conv3_dx', 7: 'conv2_dx', 8: 'conv1_dw', 9: 'update', 11: 'fc1_dw*', 12: 'conv3_dw*', 13: 'conv2_dw*', 14: 'c1_stage*', 15: 'head_sub*'}
 ORDER = [10, 0, 14, 1, 2, 3, 4, 15, 5, 6, 11, 7, 12, 8, 13, 9]
-K, NB, NS = 16, 4096, 4
+K, NB, NS = 20, 4096, 4  # common.hpp TRACE_*: kernels 16-18 are the HVP launches (tools/trace_hvp.py)
 
 dev = torch.device('cuda:0')
 cap = int(os.environ.get('CAP', '200000'))
