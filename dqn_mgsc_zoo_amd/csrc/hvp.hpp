@@ -20,8 +20,8 @@
 //                     s1 and ddot4 | b3
 //   L2 hvp_l2_kernel  t34 (conv3 block (p, g) = fc1 K-chunk 4 p + g: the 16
 //                     conv3 outputs it forms are the chunk's 16 rows) | b2
-//   L3 hvp_l3_kernel  b1 | every parameter block of H_q w, conv1's last:
-//                     they need all of ddot1 and wait for it in-launch.
+//   L3 hvp_l3_kernel  b1 | every parameter block of H_q w (conv1's need
+//                     all of ddot1 and wait for it in-launch).
 // Round 5 ran eight launches, one per dependent stage, each ≈ 5.1 us
 // (rocprofv3) for a few microseconds of latency.  Every per-element sum
 // keeps the order of that form.  Each stage splits its reduction over the
@@ -95,6 +95,26 @@ struct HqOut {
     else
       a.hq[i] = hq;
   }
+  // the first n of N puts, every load issued before the first store
+  template <int N>
+  __device__ __forceinline__ void put_n(const HvpArgs& a, const int64_t* i, const float* hq, int n) const {
+    if (a.vout) {
+      float vd[N], jj[N], g[N];
+#pragma unroll
+      for (int u = 0; u < N; ++u) {
+        vd[u] = a.vdir[i[u]];
+        jj[u] = a.J[i[u]];
+        g[u] = a.gq[i[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < N; ++u)
+        if (u < n) a.vout[i[u]] = vd[u] + jj[u] * (a_s1 * g[u] - clip * hq[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < N; ++u)
+        if (u < n) a.hq[i[u]] = hq[u];
+    }
+  }
 };
 
 constexpr int HVP_T4_KC = 16, HVP_T4_CHUNKS = FLAT / HVP_T4_KC;  // 196 chunks of 16 rows
@@ -111,27 +131,33 @@ static_assert(HVP_T34 == HVP_T4_CHUNKS, "conv3 block i forms fc1 chunk i's rows"
 constexpr int T12_IN = C1S * 3 + C1K;  // 20
 struct HvpT12Smem {
   float4 in[T12_IN * T12_IN];  // [row][col], the 4 channels of one pixel
-  float r[16][C1K][C1CO];      // conv1 kh partials per window position
-  float t1[16][C1CO];          // ty1 over the window
-  float r2[16][16];            // conv2 tap partials
+  union {
+    float w1[C1KK][C1CO];       // Wdot1, staged with 16-byte loads
+    float r[16][C1K][C1CO];     // then: conv1 kh partials per window position
+  };
+  float t1[16][C1CO];           // ty1 over the window
+  float r2[64][16];             // conv2 (tap, input-channel group) partials
 };
 
 // t1 + t2: ty1 = relu'(y1) (bdot1 + sum_k x_p[k] Wdot1[k][co]) over the
 // block's window (thread (kh = t / 32, co = t % 32) sums kw, ci of row kh
 // for each window position; the 8 kh partials are summed in order), then
 // ty2 = relu'(y2) (bdot2 + conv(y1, Wdot2) + conv(ty1, W2)) for 16 channels
-// (thread (tap = t / 16 = kh * 4 + kw, co)).  Each conv1 position is stored
-// by one block: channel group 0 of the conv2 position oh = min(ih / 2, 8),
-// ow = min(iw / 2, 8).
+// (thread (tap = t / 16, co quad cq = t / 4 % 4, input-channel group cg =
+// t % 4): 4 output channels x 8 input channels with 16-byte loads; the 64
+// (tap, cg) partials are summed in order).  Each conv1 position is stored by
+// one block: channel group 0 of the conv2 position oh = min(ih / 2, 8),
+// ow = min(iw / 2, 8).  Every thread issues 38 loads, most of them 16 bytes
+// (a form with 130 scalar loads per thread waited for its loads in two
+// rounds: a wave cannot hold more than 63 in flight).
 __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Smem& s) {
   if (DQZ_EXP_HVP_SKIP & 1) return;
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
   const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
-  // the slot -> frame-index -> frame chain first (three dependent trips),
-  // then the thread's 32 conv1 tangent weights, its two window outputs' y1
-  // and its conv2 operands, in flight under the chain's last trip (no
-  // branch among the loads: a branch made the compiler drain them all)
+  // the slot -> frame-index -> frame chain first (three dependent trips);
+  // every other load in flight under its last trip (no branch among the
+  // loads: a branch made the compiler drain them all)
   const int f = a.fidx[(int64_t)a.slot[0] * 8 + (t & 3)];
   constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600 tile elements, 7 rounds
   unsigned xb[R];
@@ -143,10 +169,10 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
       xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
     }
   }
-  const float* W1d = a.tw + a.off[0];
-  float wv[C1K * FC];
+  constexpr int W1Q = C1KK * C1CO / 4 / 256;  // 8 float4 per thread
+  float4 wl[W1Q];
 #pragma unroll
-  for (int j = 0; j < C1K * FC; ++j) wv[j] = W1d[(kh * C1K * FC + j) * C1CO + co];
+  for (int u = 0; u < W1Q; ++u) wl[u] = reinterpret_cast<const float4*>(a.tw + a.off[0])[t + 256 * u];
   float y1v[2];
   int p1[2];
 #pragma unroll
@@ -155,16 +181,18 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
     p1[h] = (2 * oh + (pos >> 2)) * C1O + 2 * ow + (pos & 3);
     y1v[h] = a.y1[p1[h] * C1CO + co];
   }
-  const int tap = t >> 4, c2 = 16 * g + (t & 15);
-  const int src = ((2 * oh + (tap >> 2)) * C1O + 2 * ow + (tap & 3)) * C1CO;
-  const float *W = a.th + a.off[2] + tap * C2CI * C2CO + c2, *Wd = a.tw + a.off[2] + tap * C2CI * C2CO + c2;
-  float y[C2CI], w[C2CI], wd[C2CI];
+  const int tap = t >> 4, cq = (t >> 2) & 3, cg = t & 3;
+  const int src = ((2 * oh + (tap >> 2)) * C1O + 2 * ow + (tap & 3)) * C1CO + 8 * cg;
+  const int64_t wo = (int64_t)(tap * C2CI + 8 * cg) * C2CO + 16 * g + 4 * cq;
+  float4 w2[8], wd2[8], yv[2];
 #pragma unroll
-  for (int ci = 0; ci < C2CI; ++ci) {
-    y[ci] = a.y1[src + ci];
-    wd[ci] = Wd[ci * C2CO];
-    w[ci] = W[ci * C2CO];
+  for (int e = 0; e < 8; ++e) {
+    w2[e] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wo + e * C2CO);
+    wd2[e] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wo + e * C2CO);
   }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) yv[h] = *reinterpret_cast<const float4*>(a.y1 + src + 4 * h);
+  const int c2 = 16 * g + (t & 15);
   const float y2v = a.y2[p * C2CO + c2];  // used by t < 16
   const float b2v = a.tw[a.off[3] + c2];
   const float b1v = a.tw[a.off[1] + co];
@@ -173,23 +201,32 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
 #pragma unroll
     for (int u = 0; u < R; ++u)
       if (t + 256 * u < N) in[t + 256 * u] = f < 0 ? 0.f : u8n(xb[u]);
+#pragma unroll
+    for (int u = 0; u < W1Q; ++u) reinterpret_cast<float4*>(&s.w1[0][0])[t + 256 * u] = wl[u];
   }
   __syncthreads();
   DQZ_STAMP(16, 1);
-#pragma unroll 4
+  float wv[C1K * FC];  // row kh of Wdot1, column co: (kw, ci) as j = 4 kw + ci
+#pragma unroll
+  for (int j = 0; j < C1K * FC; ++j) wv[j] = s.w1[kh * C1K * FC + j][co];
+  float zp[16];
+#pragma unroll
   for (int pos = 0; pos < 16; ++pos) {
     const float4* row = s.in + (4 * (pos >> 2) + kh) * T12_IN + 4 * (pos & 3);
     float z = 0.f;
 #pragma unroll
-    for (int kw = 0; kw < C1K; ++kw) {  // (kh, kw, ci = j % 4) as j = 4 kw + ci
+    for (int kw = 0; kw < C1K; ++kw) {
       const float4 x = row[kw];
       z += x.x * wv[4 * kw];
       z += x.y * wv[4 * kw + 1];
       z += x.z * wv[4 * kw + 2];
       z += x.w * wv[4 * kw + 3];
     }
-    s.r[pos][kh][co] = z;
+    zp[pos] = z;
   }
+  __syncthreads();  // s.r overwrites s.w1
+#pragma unroll
+  for (int pos = 0; pos < 16; ++pos) s.r[pos][kh][co] = zp[pos];
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -203,15 +240,24 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   }
   __syncthreads();
   DQZ_STAMP(16, 2);
-  float z = 0.f;
+  float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* tt = reinterpret_cast<const float4*>(&s.t1[tap][8 * cg]);
+  const float4 ta[2] = {tt[0], tt[1]};
 #pragma unroll
-  for (int ci = 0; ci < C2CI; ++ci) z += y[ci] * wd[ci] + s.t1[tap][ci] * w[ci];
-  s.r2[tap][t & 15] = z;
+  for (int e = 0; e < 8; ++e) {
+    const float yy = e < 4 ? (&yv[0].x)[e] : (&yv[1].x)[e - 4];
+    const float ty = e < 4 ? (&ta[0].x)[e] : (&ta[1].x)[e - 4];
+    z.x += yy * wd2[e].x + ty * w2[e].x;
+    z.y += yy * wd2[e].y + ty * w2[e].y;
+    z.z += yy * wd2[e].z + ty * w2[e].z;
+    z.w += yy * wd2[e].w + ty * w2[e].w;
+  }
+  *reinterpret_cast<float4*>(&s.r2[4 * tap + cg][4 * cq]) = z;
   __syncthreads();
   if (t < 16) {
     float v = b2v;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v += s.r2[k][t];
+    for (int k = 0; k < 64; ++k) v += s.r2[k][t];
     a.ty2[p * C2CO + c2] = y2v > 0.f ? v : 0.f;
   }
 }
@@ -465,19 +511,19 @@ __device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*
 
 // ---- the parameter-gradient blocks of H_q w (L3) -------------------------
 //   [257] conv1 rows k (row 256 = bias): sum_p x_p[k] ddot1[p][co] over 8
-//         position splits (thread (split, co)), last;
+//         position splits (thread (split, co)), after b1's hand-off;
 //   [513] conv2 rows, [577] conv3 rows (last row = bias):
 //         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
 //         splits (thread (split, co));
 //   [8]   fc2 / fc1 bias / fc2 bias: hdot = relu'(h) (bdot1 + sum of t4's
 //         chunk partials), the fc2 column a = hdot; 64 hidden units per
 //         block, the 196 chunk partials of each in 4 groups of 49 loads;
-//   [...] fc1: ydot3 (x) d4 + y3 (x) ddot4, 4 elements per thread.
+//   [392] fc1: ydot3 (x) d4 + y3 (x) ddot4, 16 elements per thread.
 // Every per-thread sum issues all its loads before the first addition
 // (round 5: the position and chunk loops waited for one round trip per
 // iteration, 13-21 serial trips, and kept the gradient launch at 12.2 us).
 constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = HID / 64;
-constexpr int HVP_G_FC = FLAT * HID / 4 / 256;  // 1568
+constexpr int HVP_G_FC = FLAT * HID / 16 / 256;  // 392 (hvp_g_fc1: 16 elements per thread)
 
 template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
@@ -541,31 +587,58 @@ __device__ __forceinline__ void hvp_g_hidden(const HvpArgs& a, int i, float (*s_
   const int act = a.action[a.slot[0]];
   const float z = a.tw[a.off[7] + n] + ((s_r[0][nl] + s_r[1][nl]) + (s_r[2][nl] + s_r[3][nl]));
   const float hd = a.h[n] > 0.f ? z : 0.f;
-  for (int col = 0; col < a.A; ++col) ho.put(a, a.off[8] + (int64_t)n * a.A + col, col == act ? hd : 0.f);
-  ho.put(a, a.off[7] + n, a.td4[n]);
+  // the row's A fc2 entries and the fc1 bias: every put's loads before its
+  // store (a put per column waited one round trip each)
+  constexpr int NP = 9;
+  for (int c0 = 0; c0 < a.A + 1; c0 += NP) {
+    int64_t idx[NP];
+    float hq[NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int col = min(c0 + u, a.A);  // col A: the fc1 bias
+      idx[u] = col < a.A ? a.off[8] + (int64_t)n * a.A + col : a.off[7] + n;
+      hq[u] = col < a.A ? (col == act ? hd : 0.f) : a.td4[n];
+    }
+    ho.put_n<NP>(a, idx, hq, min(NP, a.A + 1 - c0));
+  }
   if (i == 0 && t < a.A) ho.put(a, a.off[9] + t, 0.f);
 }
 
-// fc1 rows: 4 consecutive columns per thread.
+// fc1 rows: 4 groups of 4 consecutive columns per thread (group u: element
+// ((4 i + u) 256 + t) 4), every group's loads before the first store.
+constexpr int HVP_G_FCU = 4;
 __device__ __forceinline__ void hvp_g_fc1(const HvpArgs& a, int i, const HqOut& ho) {
   if (DQZ_EXP_HVP_SKIP & 16) return;
   const int t = threadIdx.x;
-  const int64_t e = ((int64_t)i * 256 + t) * 4;
-  const int k = (int)(e / HID), n = (int)(e % HID);
-  const float ty = a.ty3[k], y = a.y3[k];
-  const float4 d = *reinterpret_cast<const float4*>(a.d4 + n);
-  const float4 dd = *reinterpret_cast<const float4*>(a.td4 + n);
-  const float4 hq = make_float4(ty * d.x + y * dd.x, ty * d.y + y * dd.y, ty * d.z + y * dd.z, ty * d.w + y * dd.w);
-  if (a.vout) {
-    const int64_t j = a.off[6] + e;
-    const float4 vd = *reinterpret_cast<const float4*>(a.vdir + j);
-    const float4 jj = *reinterpret_cast<const float4*>(a.J + j);
-    const float4 g = *reinterpret_cast<const float4*>(a.gq + j);
-    *reinterpret_cast<float4*>(a.vout + j) =
-        make_float4(vd.x + jj.x * (ho.a_s1 * g.x - ho.clip * hq.x), vd.y + jj.y * (ho.a_s1 * g.y - ho.clip * hq.y),
-                    vd.z + jj.z * (ho.a_s1 * g.z - ho.clip * hq.z), vd.w + jj.w * (ho.a_s1 * g.w - ho.clip * hq.w));
-  } else {
-    *reinterpret_cast<float4*>(a.hq + a.off[6] + e) = hq;
+  constexpr int U = HVP_G_FCU;
+  int64_t e[U];
+  float ty[U], y[U];
+  float4 d[U], dd[U], vd[U], jj[U], g[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    e[u] = ((int64_t)(U * i + u) * 256 + t) * 4;
+    const int k = (int)(e[u] / HID), n = (int)(e[u] % HID);
+    ty[u] = a.ty3[k];
+    y[u] = a.y3[k];
+    d[u] = *reinterpret_cast<const float4*>(a.d4 + n);
+    dd[u] = *reinterpret_cast<const float4*>(a.td4 + n);
+    if (a.vout) {
+      const int64_t j = a.off[6] + e[u];
+      vd[u] = *reinterpret_cast<const float4*>(a.vdir + j);
+      jj[u] = *reinterpret_cast<const float4*>(a.J + j);
+      g[u] = *reinterpret_cast<const float4*>(a.gq + j);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float4 hq = make_float4(ty[u] * d[u].x + y[u] * dd[u].x, ty[u] * d[u].y + y[u] * dd[u].y,
+                                  ty[u] * d[u].z + y[u] * dd[u].z, ty[u] * d[u].w + y[u] * dd[u].w);
+    if (a.vout)
+      *reinterpret_cast<float4*>(a.vout + a.off[6] + e[u]) = make_float4(
+          vd[u].x + jj[u].x * (ho.a_s1 * g[u].x - ho.clip * hq.x), vd[u].y + jj[u].y * (ho.a_s1 * g[u].y - ho.clip * hq.y),
+          vd[u].z + jj[u].z * (ho.a_s1 * g[u].z - ho.clip * hq.z), vd[u].w + jj[u].w * (ho.a_s1 * g[u].w - ho.clip * hq.w));
+    else
+      *reinterpret_cast<float4*>(a.hq + a.off[6] + e[u]) = hq;
   }
 }
 
@@ -604,30 +677,31 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
   }
 }
 
-// L3: b1 first, then every gradient block that does not need ddot1, then
-// conv1's, which wait in-launch for the 400 b1 blocks (all dispatched before
-// any of them on every XCD, so the wait cannot hold a b1 block out).
-constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C2 + HVP_G_C3 + HVP_G_H + HVP_G_FC + HVP_G_C1;  // 3,323
+// L3: b1 first, then conv1's parameter blocks, which stage their patch
+// values and wait in-launch for the 400 b1 blocks (all dispatched before any
+// of them on every XCD, so the wait cannot hold a b1 block out), then every
+// other parameter block (the fc2 / bias rows first: the longest-lived).
+constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-  constexpr int G2 = C1M, G3 = G2 + HVP_G_C2, GH = G3 + HVP_G_C3, GF = GH + HVP_G_H, G1 = GF + HVP_G_FC;
+  constexpr int G1 = C1M, GH = G1 + HVP_G_C1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
-  if (i < G2) {
+  if (i < G1) {
     hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
   } else {
     const HqOut ho(a);
-    if (i < G3)
-      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
-    else if (i < GH)
-      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
-    else if (i < GF)
-      hvp_g_hidden(a, i - GH, s_r, ho);
-    else if (i < G1)
-      hvp_g_fc1(a, i - GF, ho);
-    else
+    if (i < GH)
       hvp_g_conv1(a, i - G1, s_r, s_x, ho);
+    else if (i < G2)
+      hvp_g_hidden(a, i - GH, s_r, ho);
+    else if (i < G3)
+      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
+    else if (i < GF)
+      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
+    else
+      hvp_g_fc1(a, i - GF, ho);
   }
   DQZ_STAMP(18, 3);
 }
