@@ -34,6 +34,11 @@ struct Conv1Src {
   const float* reward = nullptr;
   const float* discount = nullptr;
   float4* rec = nullptr;
+  // Stack copy (the MGSC theta' pass): the conv1 blocks of sample 0, stack 0,
+  // copy the bytes they stage (zero padding applied) to xout [4][84][84], so
+  // the HVP launches read the online transition's input without the slot ->
+  // frame-index -> frame chain.
+  uint8_t* xout = nullptr;
 };
 
 struct Conv1FwdArgs {
@@ -181,6 +186,8 @@ __device__ __forceinline__ void stage_conv1_input(uint16_t* s_in, const Conv1Src
         const int ci = i / QPC, j = i % QPC;
         if (fq[q] < 0) v[q] = make_uint4(0u, 0u, 0u, 0u);  // trailing zero padding
         store_bytes_as_bf16(s_in + ci * C1_PLANE + j * 16, v[q]);
+        if (src.xout && b == 0 && which == 0 && z == 0)
+          reinterpret_cast<uint4*>(src.xout + (int64_t)ci * FB + row0 * FW)[j] = v[q];
       }
     }
     if (wrec) src.rec[b] = recv;

@@ -46,9 +46,9 @@
 namespace dqz {
 
 struct HvpArgs {
-  // x: the online transition's s_tm1 from a one-slot frame store
-  const uint8_t* frames;
-  const int32_t* fidx;
+  // x: the online transition's s_tm1 bytes [4][84][84], copied by the theta'
+  // forward's conv1 stage (Conv1Src::xout)
+  const uint8_t* x;
   const int32_t* slot;
   const int32_t* action;  // store action table (a = action[slot])
   const float* th;        // primal params theta'
@@ -155,14 +155,13 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
   const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
-  // the slot -> frame-index -> frame chain first (three dependent trips);
-  // every other load in flight under its last trip (no branch among the
-  // loads: a branch made the compiler drain them all)
-  const int f = a.fidx[(int64_t)a.slot[0] * 8 + (t & 3)];
+  // the input tile's bytes (the theta' forward's copy: one trip, no slot ->
+  // frame-index -> frame chain) and every other load together (no branch
+  // among the loads: a branch made the compiler drain them all)
   constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600 tile elements, 7 rounds
   unsigned xb[R];
   {
-    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB + C1S * 2 * oh * FW + C1S * 2 * ow;
+    const uint8_t* fr = a.x + (t & 3) * FB + C1S * 2 * oh * FW + C1S * 2 * ow;
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const int px = min(t + 256 * u, N - 1) >> 2;  // element e = pixel * 4 + channel, channel = t % 4
@@ -200,7 +199,7 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
     float* in = reinterpret_cast<float*>(s.in);
 #pragma unroll
     for (int u = 0; u < R; ++u)
-      if (t + 256 * u < N) in[t + 256 * u] = f < 0 ? 0.f : u8n(xb[u]);
+      if (t + 256 * u < N) in[t + 256 * u] = u8n(xb[u]);
 #pragma unroll
     for (int u = 0; u < W1Q; ++u) reinterpret_cast<float4*>(&s.w1[0][0])[t + 256 * u] = wl[u];
   }
@@ -289,13 +288,19 @@ __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
 // b3: ddot3[k] = relu'(y3[k]) sum_n (Wdot1[k][n] d4[n] + W1[k][n] ddot4[n]):
 // 16 rows per block, wave w rows 16 i + 4 w .. + 3 (lane l: columns 8 l ..
 // 8 l + 7, 16-byte loads, all four rows' loads issued together); the lane's
-// eight ddot4 values are formed here from h and Wdot2.
-__device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
+// eight ddot4 = relu'(h) Wdot2[n][a] are formed here.  For A <= 16 the block
+// stages all of Wdot2 (512 x A) in LDS beside the row loads, so the slot ->
+// action chain runs under them instead of before a third trip (the gathers
+// of column a).
+__device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i, float* s_w2) {
   if (DQZ_EXP_HVP_SKIP & 2) return;
   constexpr int R = 4;
-  const int lane = threadIdx.x & 63, k0 = 16 * i + R * (threadIdx.x >> 6);
-  // the slot -> action chain first, the rows' loads under its second trip
+  const int t = threadIdx.x, lane = t & 63, k0 = 16 * i + R * (t >> 6);
   const int act = a.action[a.slot[0]];
+  const bool staged = a.A <= 16;
+  float4 wq[8];  // Wdot2 as float4: 128 A elements, A / 2 per thread (A <= 16; always in range)
+#pragma unroll
+  for (int u = 0; u < 8; ++u) wq[u] = reinterpret_cast<const float4*>(a.tw + a.off[8])[min(t + 256 * u, HID * a.A / 4 - 1)];
   float4 w[R][2], wd[R][2], d[2], hv[2];
   float y3[R];
 #pragma unroll
@@ -314,10 +319,19 @@ __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i) {
     d[h] = reinterpret_cast<const float4*>(a.d4 + 8 * lane)[h];
     hv[h] = reinterpret_cast<const float4*>(a.h + 8 * lane)[h];
   }
-  const float* w2 = a.tw + a.off[8] + (int64_t)(8 * lane) * a.A + act;
   float g[8];
+  if (staged) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) g[q] = w2[q * a.A];
+    for (int u = 0; u < 8; ++u)
+      if (t + 256 * u < HID * a.A / 4) reinterpret_cast<float4*>(s_w2)[t + 256 * u] = wq[u];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = s_w2[(8 * lane + q) * a.A + act];
+  } else {
+    const float* w2 = a.tw + a.off[8] + (int64_t)(8 * lane) * a.A + act;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = w2[q * a.A];
+  }
   float4 dd[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -345,7 +359,7 @@ __global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
   else if (i == HVP_T12)
     hvp_s1_block(a, &s.r2[0][0]);
   else
-    hvp_b3_block(a, i - HVP_T12 - 1);
+    hvp_b3_block(a, i - HVP_T12 - 1, &s.w1[0][0]);
   DQZ_STAMP(16, 3);
 }
 
@@ -651,10 +665,8 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
   const int t = threadIdx.x, co = t & 31, sp = t >> 5;
   if (k < C1KK) {
     const int kh = k / (C1K * FC), kw = (k / FC) % C1K, ci = k % FC;
-    const int f = a.fidx[(int64_t)a.slot[0] * 8 + ci];
-    const uint8_t* fr = a.frames + (int64_t)max(f, 0) * FB;
-    for (int p = t; p < C1M; p += 256)
-      s_x[p] = f < 0 ? 0.f : u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
+    const uint8_t* fr = a.x + ci * FB;
+    for (int p = t; p < C1M; p += 256) s_x[p] = u8n(fr[(C1S * (p / C1O) + kh) * FW + C1S * (p % C1O) + kw]);
   } else {
     for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
   }
@@ -677,31 +689,33 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
   }
 }
 
-// L3: b1 first, then conv1's parameter blocks, which stage their patch
-// values and wait in-launch for the 400 b1 blocks (all dispatched before any
-// of them on every XCD, so the wait cannot hold a b1 block out), then every
-// other parameter block (the fc2 / bias rows first: the longest-lived).
-constexpr int HVP_L3_BLOCKS = C1M + HVP_G_C1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC;  // 2,147
+// L3: b1 first, then every parameter block that does not need ddot1 (the
+// fc2 / bias rows first: the longest-lived), then conv1's, which wait
+// in-launch for the 400 b1 blocks (all dispatched before any of them on
+// every XCD, so the wait cannot hold a b1 block out).  With the conv1 blocks
+// right after b1, 257 pollers slowed every other block of the launch (its
+// span 15.6 -> 25 us, profiles/r05/s27).
+constexpr int HVP_L3_BLOCKS = C1M + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-  constexpr int G1 = C1M, GH = G1 + HVP_G_C1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3;
+  constexpr int GH = C1M, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
-  if (i < G1) {
+  if (i < GH) {
     hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
   } else {
     const HqOut ho(a);
-    if (i < GH)
-      hvp_g_conv1(a, i - G1, s_r, s_x, ho);
-    else if (i < G2)
+    if (i < G2)
       hvp_g_hidden(a, i - GH, s_r, ho);
     else if (i < G3)
       hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
     else if (i < GF)
       hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
-    else
+    else if (i < G1)
       hvp_g_fc1(a, i - GF, ho);
+    else
+      hvp_g_conv1(a, i - G1, s_r, s_x, ho);
   }
   DQZ_STAMP(18, 3);
 }

@@ -288,7 +288,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
                      const float* meta_p = nullptr, const UniformDraw* draw = nullptr, int unit = 0,
                      int gacc = 0, const PerWbArgs* wb = nullptr, const SoftmaxDraw* sm = nullptr,
                      const PerSampleArgs* pd = nullptr, const Rms* meta_epi = nullptr,
-                     const HeadArgs* meta_sm = nullptr) {
+                     const HeadArgs* meta_sm = nullptr, uint8_t* xout = nullptr) {
   if (!L || !P || !P->online || !P->target || !slots) return fail(DQZ_ERR_INVALID, "null argument");
   if (!gout && !meta_epi && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
   if (meta_epi && meta_epi->meta == 1 && (!P->mu || !P->nu)) return fail(DQZ_ERR_INVALID, "null optimizer state");
@@ -308,6 +308,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   src.reward = S->reward;
   src.discount = S->discount;
   src.rec = reinterpret_cast<float4*>(L->rec);
+  src.xout = xout;
   if (draw || sm || pd) {  // conv1 draws the batch itself; later kernels read the published slots
     Conv1Src fsrc = src;
     if (draw) {
@@ -418,6 +419,7 @@ static int step_impl(dqz_learner* L, const dqz_params* P, const dqz_store* S, co
   Conv1DwArgs c1dw{};
   c1dw.src = src;
   c1dw.src.rec = nullptr;
+  c1dw.src.xout = nullptr;
   c1dw.which = 0;
   c1dw.B = B;
   c1dw.dy1 = L->dy1;
@@ -1112,6 +1114,7 @@ struct dqz_meta {
   // second-order (reservoir) meta-gradient
   float *GQ, *HQ, *s1_part, *hpart;
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
+  uint8_t* x1;  // [4][84][84] the online transition's s_tm1 bytes (written by the theta' forward)
   float* dotp;  // [C][META_DOT_SLOTS] the tangent launch's dot-product partials (one chunk)
   int* arrive;  // [0] meta_adam_chunks_kernel's re-seed arrival counter, [kStride, 3 kStride) the
                 // HVP's ddot1 hand-off words (all zero between launches)
@@ -1161,13 +1164,13 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
                            so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID,
-                           (int64_t)C * META_DOT_SLOTS, 3 * Handoff::kStride};
+                           (int64_t)C * META_DOT_SLOTS, 3 * Handoff::kStride, so * FC * FB / 4};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
                     &H->GQ, &H->HQ, &H->s1_part,
                     &H->ty1, &H->ty2, &H->ty3, &H->td4, &H->td3, &H->td2, &H->td1, &H->s1, &H->hpart,
-                    &H->dotp, reinterpret_cast<float**>(&H->arrive)};
+                    &H->dotp, reinterpret_cast<float**>(&H->arrive), reinterpret_cast<float**>(&H->x1)};
   static_assert(sizeof(sizes) / sizeof(sizes[0]) == sizeof(ptrs) / sizeof(ptrs[0]), "meta scratch table");
   int64_t tot = 0;
   for (int64_t n : sizes) tot += (n + 63) / 64 * 64;
@@ -1300,12 +1303,11 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     epi.bound = H->cfg.grad_error_bound;
     epi.s1_part = H->s1_part;
     if (int rc = step_impl(L1, &P1, S1, online_slot, nullptr, stream, kNoProfile, H->GQ, nullptr, nullptr, 1, 0,
-                           nullptr, nullptr, nullptr, &epi))
+                           nullptr, nullptr, nullptr, &epi, nullptr, H->x1))
       return rc;
     const int nparts1 = 4 * (FLAT / 16) + (int)update_blocks(L1->sz, A, L1->shared_bias ? 1 : A);
     HvpArgs hv{};
-    hv.frames = S1->frames;
-    hv.fidx = S1->fidx;
+    hv.x = H->x1;
     hv.slot = online_slot;
     hv.action = S1->action;
     hv.th = H->thp;
