@@ -72,7 +72,7 @@ struct HvpArgs {
   const float *vdir, *J, *gq, *td;
   float bound;
   float* vout;
-  // ddot1 complete: the 400 b1 blocks arrive, the 257 conv1 parameter
+  // ddot1 complete: the 800 b1 blocks arrive, the 257 conv1 parameter
   // blocks at the end of the same launch wait (sample word 0)
   Handoff td1_pub;
 };
@@ -366,58 +366,83 @@ __global__ __launch_bounds__(256) void hvp_l1_kernel(HvpArgs a) {
 // ---- L2 -----------------------------------------------------------------
 
 // t3 + t4: ty3 = relu'(y3) (bdot3 + conv(y2, Wdot3) + conv(ty2, W3)) for
-// conv3 position p, channels 16 g .. 16 g + 15 (thread (input-channel quad
-// s = t / 16, co) over the 9 taps) — flat rows 16 i .. 16 i + 15, which are
-// fc1 K-chunk i: part[i][n] = sum_j y3[k] Wdot1[k][n] + ty3[k] W1[k][n]
-// (thread t: columns 2t, 2t + 1; whole-row float2 loads issued first).
-__device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, float (*s_r)[17], float* s_ty) {
+// conv3 position p, channels 16 g .. 16 g + 15 (thread (input channel ci =
+// t / 4, output-channel quad c4 = t % 4) over the 9 taps, 16-byte weight
+// loads; the 64 input-channel partials summed in order) — flat rows 16 i ..
+// 16 i + 15, which are fc1 K-chunk i: part[i][n] = sum_j y3[k] Wdot1[k][n] +
+// ty3[k] W1[k][n] (thread (row half rh = t / 128, column quad cq = t % 128):
+// 8 rows of 4 columns each, the two halves added in order).  56 loads per
+// thread, all issued first (a form with 144 scalar conv loads per thread
+// waited for them in several rounds: a wave holds at most 63 in flight).
+struct HvpT34Smem {
+  float r[64][16];  // conv3 input-channel partials
+  float4 c[128];    // fc1 chunk: rows 8 .. 15's sums
+  float ty[16];
+};
+__device__ __forceinline__ void hvp_t34_block(const HvpArgs& a, int i, HvpT34Smem& s) {
   if (DQZ_EXP_HVP_SKIP & 64) return;
   const int t = threadIdx.x, p = i >> 2, g = i & 3;
-  const float *W1 = a.th + a.off[6], *W1d = a.tw + a.off[6];
-  float2 fw[HVP_T4_KC], fwd[HVP_T4_KC];
-  float fy[HVP_T4_KC];
+  const int rh = t >> 7, cq = t & 127;
+  float4 fw[8], fwd[8], fy[2];
 #pragma unroll
-  for (int j = 0; j < HVP_T4_KC; ++j) {
-    const int k = i * HVP_T4_KC + j;
-    fw[j] = *reinterpret_cast<const float2*>(W1 + (int64_t)k * HID + 2 * t);
-    fwd[j] = *reinterpret_cast<const float2*>(W1d + (int64_t)k * HID + 2 * t);
-    fy[j] = a.y3[k];
+  for (int j = 0; j < 8; ++j) {
+    const int64_t k = (int64_t)i * HVP_T4_KC + 8 * rh + j;
+    fw[j] = *reinterpret_cast<const float4*>(a.th + a.off[6] + k * HID + 4 * cq);
+    fwd[j] = *reinterpret_cast<const float4*>(a.tw + a.off[6] + k * HID + 4 * cq);
   }
-  const int oh = p / C3O, ow = p % C3O, s = t >> 4;
-  const int co = 16 * g + (t & 15);
-  const float *W = a.th + a.off[4] + co, *Wd = a.tw + a.off[4] + co;
-  float z = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) fy[h] = *reinterpret_cast<const float4*>(a.y3 + i * HVP_T4_KC + 8 * rh + 4 * h);
+  const int oh = p / C3O, ow = p % C3O, ci = t >> 2, c4 = t & 3;
+  float yv[9], tv[9];
+  float4 wv[9], wdv[9];
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
-    const int kh = tap / 3, kw = tap % 3;
-    const int src = ((oh + kh) * C2O + ow + kw) * C2CO + 4 * s;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int wi = (tap * C3CI + 4 * s + e) * C3CO;
-      z += a.y2[src + e] * Wd[wi] + a.ty2[src + e] * W[wi];
-    }
+    const int src = ((oh + tap / 3) * C2O + ow + tap % 3) * C2CO + ci;
+    const int64_t wi = (int64_t)(tap * C3CI + ci) * C3CO + 16 * g + 4 * c4;
+    yv[tap] = a.y2[src];
+    tv[tap] = a.ty2[src];
+    wv[tap] = *reinterpret_cast<const float4*>(a.th + a.off[4] + wi);
+    wdv[tap] = *reinterpret_cast<const float4*>(a.tw + a.off[4] + wi);
   }
-  s_r[s][t & 15] = z;
+  const int c = 16 * g + (t & 15);
+  const float y3c = a.y3[p * C3CO + c];  // used by t < 16
+  const float b3 = a.tw[a.off[5] + c];
+  float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    z.x += yv[tap] * wdv[tap].x + tv[tap] * wv[tap].x;
+    z.y += yv[tap] * wdv[tap].y + tv[tap] * wv[tap].y;
+    z.z += yv[tap] * wdv[tap].z + tv[tap] * wv[tap].z;
+    z.w += yv[tap] * wdv[tap].w + tv[tap] * wv[tap].w;
+  }
+  *reinterpret_cast<float4*>(&s.r[ci][4 * c4]) = z;
   __syncthreads();
   DQZ_STAMP(17, 1);
   if (t < 16) {
-    const int c = 16 * g + t;
-    float v = a.tw[a.off[5] + c];
+    float v = b3;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v += s_r[k][t];
-    const float ty = a.y3[p * C3CO + c] > 0.f ? v : 0.f;
+    for (int k = 0; k < 64; ++k) v += s.r[k][t];
+    const float ty = y3c > 0.f ? v : 0.f;
     a.ty3[p * C3CO + c] = ty;
-    s_ty[t] = ty;
+    s.ty[t] = ty;
   }
   __syncthreads();
-  float2 zc = make_float2(0.f, 0.f);
+  float4 zc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int j = 0; j < HVP_T4_KC; ++j) {
-    const float ty = s_ty[j];
-    zc.x += fy[j] * fwd[j].x + ty * fw[j].x;
-    zc.y += fy[j] * fwd[j].y + ty * fw[j].y;
+  for (int j = 0; j < 8; ++j) {
+    const float ty = s.ty[8 * rh + j], y = j < 4 ? (&fy[0].x)[j] : (&fy[1].x)[j - 4];
+    zc.x += y * fwd[j].x + ty * fw[j].x;
+    zc.y += y * fwd[j].y + ty * fw[j].y;
+    zc.z += y * fwd[j].z + ty * fw[j].z;
+    zc.w += y * fwd[j].w + ty * fw[j].w;
   }
-  *reinterpret_cast<float2*>(a.part + (int64_t)i * HID + 2 * t) = zc;
+  if (rh == 1) s.c[cq] = zc;
+  __syncthreads();
+  if (rh == 0) {
+    const float4 u = s.c[cq];
+    *reinterpret_cast<float4*>(a.part + (int64_t)i * HID + 4 * cq) =
+        make_float4(zc.x + u.x, zc.y + u.y, zc.z + u.z, zc.w + u.w);
+  }
 }
 
 // b2: ddot2[pix][ci] = relu'(y2) sum_{taps, co} (d3 Wdot3 + ddot3 W3) (the
@@ -462,64 +487,60 @@ __device__ __forceinline__ void hvp_b2_block(const HvpArgs& a, int i, float (*s_
 
 constexpr int HVP_L2_BLOCKS = HVP_T34 + HVP_B2;  // 520
 __global__ __launch_bounds__(256) void hvp_l2_kernel(HvpArgs a) {
-  __shared__ float s_r[16][17];
-  __shared__ float s_ty[16];
+  __shared__ HvpT34Smem s;
   const int i = blockIdx.x;
   DQZ_STAMP(17, 0);
   if (i < HVP_T34)
-    hvp_t34_block(a, i, s_r, s_ty);
+    hvp_t34_block(a, i, s);
   else
-    hvp_b2_block(a, i - HVP_T34, s_r);
+    hvp_b2_block(a, i - HVP_T34, reinterpret_cast<float(*)[17]>(&s.r[0][0]));
   DQZ_STAMP(17, 3);
 }
 
 // ---- L3 -----------------------------------------------------------------
 
 // b1: ddot1[pix][ci] = relu'(y1) sum_{taps, co} (d2 Wdot2 + ddot2 W2) (the
-// transposed conv2, stride 2: at most 2 x 2 live taps).  Block pix; thread
-// (ci = t / 8, output-channel octet cs = t % 8).
-__device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*s_r)[9]) {
+// transposed conv2, stride 2: at most 2 x 2 live taps).  Block (pix, input
+// channel half hh); thread (ci = 16 hh + t / 16, output-channel quad cq =
+// t % 16): 16 loads of 16 bytes, the 16 quads' sums on DPP row shifts (a
+// block per pixel with 8-channel threads held 128 VGPRs of operands, which
+// cut the launch's resident blocks to 3 per CU).
+constexpr int HVP_B1 = 2 * C1M;  // 800
+__device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int i) {
   if (DQZ_EXP_HVP_SKIP & 4) {
     a.td1_pub.arrive(0);
     return;
   }
-  const int t = threadIdx.x;
-  const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
+  const int t = threadIdx.x, pix = i >> 1, hh = i & 1;
+  const int ih = pix / C1O, iw = pix % C1O, cq = t & 15, ci = 16 * hh + (t >> 4);
   // the 2 x 2 taps of this pixel's stride phase, every operand loaded before
   // the first product (taps outside the output clamped and skipped, in order)
-  float4 w[4][2], wd[4][2], d[4][2], dd[4][2];
+  float4 w[4], wd[4], d[4], dd[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
     const int oh = min(max((ih - kh) / C2S, 0), C2O - 1), ow = min(max((iw - kw) / C2S, 0), C2O - 1);
-    const int src = (oh * C2O + ow) * C2CO + 8 * cs;
-    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      w[q][h] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
-      wd[q][h] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
-      d[q][h] = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
-      dd[q][h] = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
-    }
+    const int src = (oh * C2O + ow) * C2CO + 4 * cq;
+    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 4 * cq;
+    w[q] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi);
+    wd[q] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi);
+    d[q] = *reinterpret_cast<const float4*>(a.d2 + src);
+    dd[q] = *reinterpret_cast<const float4*>(a.td2 + src);
   }
+  const float y1 = a.y1[pix * C1CO + ci];
   float z = 0.f;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
     if (ih < kh || (ih - kh) / C2S >= C2O || iw < kw || (iw - kw) / C2S >= C2O) continue;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      z += ((d[q][h].x * wd[q][h].x + dd[q][h].x * w[q][h].x) + (d[q][h].y * wd[q][h].y + dd[q][h].y * w[q][h].y)) +
-           ((d[q][h].z * wd[q][h].z + dd[q][h].z * w[q][h].z) + (d[q][h].w * wd[q][h].w + dd[q][h].w * w[q][h].w));
+    z += ((d[q].x * wd[q].x + dd[q].x * w[q].x) + (d[q].y * wd[q].y + dd[q].y * w[q].y)) +
+         ((d[q].z * wd[q].z + dd[q].z * w[q].z) + (d[q].w * wd[q].w + dd[q].w * w[q].w));
   }
-  s_r[ci][cs] = z;
-  __syncthreads();
-  if (t < C2CI) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += s_r[t][k];
-    store_sc1_f1(a.td1, C1M * C1CO * 4, pix * C1CO + t, a.y1[pix * C1CO + t] > 0.f ? v : 0.f);
-  }
+  z += dpp_f<0x111>(z);  // row_shr 1 / 2 / 4 / 8: lane 15 of each 16-lane row holds the row's sum
+  z += dpp_f<0x112>(z);
+  z += dpp_f<0x114>(z);
+  z += dpp_f<0x118>(z);
+  if (cq == 15) store_sc1_f1(a.td1, C1M * C1CO * 4, pix * C1CO + ci, y1 > 0.f ? z : 0.f);
   a.td1_pub.arrive(0);
 }
 
@@ -691,19 +712,19 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
 
 // L3: b1 first, then every parameter block that does not need ddot1 (the
 // fc2 / bias rows first: the longest-lived), then conv1's, which wait
-// in-launch for the 400 b1 blocks (all dispatched before any of them on
+// in-launch for the 800 b1 blocks (all dispatched before any of them on
 // every XCD, so the wait cannot hold a b1 block out).  With the conv1 blocks
 // right after b1, 257 pollers slowed every other block of the launch (its
 // span 15.6 -> 25 us, profiles/r05/s27).
-constexpr int HVP_L3_BLOCKS = C1M + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
+constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,547
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-  constexpr int GH = C1M, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
+  constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
   if (i < GH) {
-    hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
+    hvp_b1_block(a, i);
   } else {
     const HqOut ho(a);
     if (i < G2)

@@ -1345,7 +1345,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     // ddot1's in-launch hand-off: words after the Adam re-seed counter, the
     // one-transition learner's error word (dqz_learner_sync_status)
     hv.td1_pub = Handoff{H->arrive + Handoff::kStride, H->arrive + 2 * Handoff::kStride,
-                         L1->sync + 16 * Handoff::kStride, C1M, HVP_G_C1, L1->spin_max};
+                         L1->sync + 16 * Handoff::kStride, HVP_B1, HVP_G_C1, L1->spin_max};
     // three launches (hvp.hpp): the tangent forward and backward side by
     // side, then the parameter blocks of H_q w
     hipLaunchKernelGGL(hvp_l1_kernel, dim3(HVP_L1_BLOCKS), dim3(256), 0, st, hv);
