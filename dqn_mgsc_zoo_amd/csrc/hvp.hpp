@@ -42,6 +42,9 @@
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
 #endif
+#ifndef DQZ_HVP_C1_EARLY
+#define DQZ_HVP_C1_EARLY 0
+#endif
 
 namespace dqz {
 
@@ -72,7 +75,7 @@ struct HvpArgs {
   const float *vdir, *J, *gq, *td;
   float bound;
   float* vout;
-  // ddot1 complete: the 800 b1 blocks arrive, the 257 conv1 parameter
+  // ddot1 complete: the 400 b1 blocks arrive, the 257 conv1 parameter
   // blocks at the end of the same launch wait (sample word 0)
   Handoff td1_pub;
 };
@@ -500,47 +503,50 @@ __global__ __launch_bounds__(256) void hvp_l2_kernel(HvpArgs a) {
 // ---- L3 -----------------------------------------------------------------
 
 // b1: ddot1[pix][ci] = relu'(y1) sum_{taps, co} (d2 Wdot2 + ddot2 W2) (the
-// transposed conv2, stride 2: at most 2 x 2 live taps).  Block (pix, input
-// channel half hh); thread (ci = 16 hh + t / 16, output-channel quad cq =
-// t % 16): 16 loads of 16 bytes, the 16 quads' sums on DPP row shifts (a
-// block per pixel with 8-channel threads held 128 VGPRs of operands, which
-// cut the launch's resident blocks to 3 per CU).
-constexpr int HVP_B1 = 2 * C1M;  // 800
-__device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int i) {
+// transposed conv2, stride 2: at most 2 x 2 live taps).  Block pix; thread
+// (ci = t / 8, output-channel octet cs = t % 8).
+__device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*s_r)[9]) {
   if (DQZ_EXP_HVP_SKIP & 4) {
     a.td1_pub.arrive(0);
     return;
   }
-  const int t = threadIdx.x, pix = i >> 1, hh = i & 1;
-  const int ih = pix / C1O, iw = pix % C1O, cq = t & 15, ci = 16 * hh + (t >> 4);
+  const int t = threadIdx.x;
+  const int ih = pix / C1O, iw = pix % C1O, cs = t & 7, ci = t >> 3;
   // the 2 x 2 taps of this pixel's stride phase, every operand loaded before
   // the first product (taps outside the output clamped and skipped, in order)
-  float4 w[4], wd[4], d[4], dd[4];
+  float4 w[4][2], wd[4][2], d[4][2], dd[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
     const int oh = min(max((ih - kh) / C2S, 0), C2O - 1), ow = min(max((iw - kw) / C2S, 0), C2O - 1);
-    const int src = (oh * C2O + ow) * C2CO + 4 * cq;
-    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 4 * cq;
-    w[q] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi);
-    wd[q] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi);
-    d[q] = *reinterpret_cast<const float4*>(a.d2 + src);
-    dd[q] = *reinterpret_cast<const float4*>(a.td2 + src);
+    const int src = (oh * C2O + ow) * C2CO + 8 * cs;
+    const int64_t wi = ((kh * C2K + kw) * C2CI + ci) * C2CO + 8 * cs;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      w[q][h] = *reinterpret_cast<const float4*>(a.th + a.off[2] + wi + 4 * h);
+      wd[q][h] = *reinterpret_cast<const float4*>(a.tw + a.off[2] + wi + 4 * h);
+      d[q][h] = *reinterpret_cast<const float4*>(a.d2 + src + 4 * h);
+      dd[q][h] = *reinterpret_cast<const float4*>(a.td2 + src + 4 * h);
+    }
   }
-  const float y1 = a.y1[pix * C1CO + ci];
   float z = 0.f;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int kh = (ih & 1) + C2S * (q >> 1), kw = (iw & 1) + C2S * (q & 1);
     if (ih < kh || (ih - kh) / C2S >= C2O || iw < kw || (iw - kw) / C2S >= C2O) continue;
-    z += ((d[q].x * wd[q].x + dd[q].x * w[q].x) + (d[q].y * wd[q].y + dd[q].y * w[q].y)) +
-         ((d[q].z * wd[q].z + dd[q].z * w[q].z) + (d[q].w * wd[q].w + dd[q].w * w[q].w));
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      z += ((d[q][h].x * wd[q][h].x + dd[q][h].x * w[q][h].x) + (d[q][h].y * wd[q][h].y + dd[q][h].y * w[q][h].y)) +
+           ((d[q][h].z * wd[q][h].z + dd[q][h].z * w[q][h].z) + (d[q][h].w * wd[q][h].w + dd[q][h].w * w[q][h].w));
   }
-  z += dpp_f<0x111>(z);  // row_shr 1 / 2 / 4 / 8: lane 15 of each 16-lane row holds the row's sum
-  z += dpp_f<0x112>(z);
-  z += dpp_f<0x114>(z);
-  z += dpp_f<0x118>(z);
-  if (cq == 15) store_sc1_f1(a.td1, C1M * C1CO * 4, pix * C1CO + ci, y1 > 0.f ? z : 0.f);
+  s_r[ci][cs] = z;
+  __syncthreads();
+  if (t < C2CI) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += s_r[t][k];
+    store_sc1_f1(a.td1, C1M * C1CO * 4, pix * C1CO + t, a.y1[pix * C1CO + t] > 0.f ? v : 0.f);
+  }
   a.td1_pub.arrive(0);
 }
 
@@ -692,7 +698,11 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
     for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
   }
   DQZ_STAMP(18, 1);
+#if DQZ_HVP_C1_EARLY
+  a.td1_pub.wait<40>(0);  // its barrier also publishes s_x
+#else
   a.td1_pub.wait(0);  // its barrier also publishes s_x
+#endif
   DQZ_STAMP(18, 2);
   float tv[50];       // this thread's ddot1 column
 #pragma unroll
@@ -712,19 +722,43 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
 
 // L3: b1 first, then every parameter block that does not need ddot1 (the
 // fc2 / bias rows first: the longest-lived), then conv1's, which wait
-// in-launch for the 800 b1 blocks (all dispatched before any of them on
+// in-launch for the 400 b1 blocks (all dispatched before any of them on
 // every XCD, so the wait cannot hold a b1 block out).  With the conv1 blocks
 // right after b1, 257 pollers slowed every other block of the launch (its
 // span 15.6 -> 25 us, profiles/r05/s27).
-constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,547
+constexpr int HVP_B1 = C1M;  // 400
+constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
+#if DQZ_HVP_C1_EARLY  // timing experiment: conv1's blocks right after b1, polling every ~1 us
+  constexpr int G1 = HVP_B1, GH = G1 + HVP_G_C1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3,
+                GE = GF + HVP_G_FC;
+  const int i = blockIdx.x;
+  DQZ_STAMP(18, 0);
+  if (i < G1) {
+    hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
+  } else {
+    const HqOut ho(a);
+    if (i < GH)
+      hvp_g_conv1(a, i - G1, s_r, s_x, ho);
+    else if (i < G2)
+      hvp_g_hidden(a, i - GH, s_r, ho);
+    else if (i < G3)
+      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
+    else if (i < GF)
+      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
+    else if (i < GE)
+      hvp_g_fc1(a, i - GF, ho);
+  }
+  DQZ_STAMP(18, 3);
+  return;
+#endif
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
   if (i < GH) {
-    hvp_b1_block(a, i);
+    hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
   } else {
     const HqOut ho(a);
     if (i < G2)
