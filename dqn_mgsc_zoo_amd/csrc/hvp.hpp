@@ -752,8 +752,7 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
       hvp_g_fc1(a, i - GF, ho);
   }
   DQZ_STAMP(18, 3);
-  return;
-#endif
+#else
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
@@ -773,6 +772,7 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
       hvp_g_conv1(a, i - G1, s_r, s_x, ho);
   }
   DQZ_STAMP(18, 3);
+#endif
 }
 
 // The second order's elementwise stages run in gradient epilogues: the
