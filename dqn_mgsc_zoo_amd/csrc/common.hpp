@@ -290,13 +290,11 @@ struct Handoff {
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + b * kStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // SLEEP: s_sleep argument between polls (64 clocks per unit)
-  template <int SLEEP = 4>
   __device__ __forceinline__ void wait(int b) const {
     if (threadIdx.x == 0) {
       unsigned spins = 0;
       while (__hip_atomic_load(cnt + b * kStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        __builtin_amdgcn_s_sleep(SLEEP);
+        __builtin_amdgcn_s_sleep(4);
         if (++spins > spin_max) {
           __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;

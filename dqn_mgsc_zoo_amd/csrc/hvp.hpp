@@ -42,9 +42,6 @@
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
 #endif
-#ifndef DQZ_HVP_C1_EARLY
-#define DQZ_HVP_C1_EARLY 0
-#endif
 
 namespace dqz {
 
@@ -698,11 +695,7 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
     for (int p = t; p < C1M; p += 256) s_x[p] = 1.f;  // bias row: sum_p ddot1
   }
   DQZ_STAMP(18, 1);
-#if DQZ_HVP_C1_EARLY
-  a.td1_pub.wait<40>(0);  // its barrier also publishes s_x
-#else
   a.td1_pub.wait(0);  // its barrier also publishes s_x
-#endif
   DQZ_STAMP(18, 2);
   float tv[50];       // this thread's ddot1 column
 #pragma unroll
@@ -725,34 +718,13 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
 // in-launch for the 400 b1 blocks (all dispatched before any of them on
 // every XCD, so the wait cannot hold a b1 block out).  With the conv1 blocks
 // right after b1, 257 pollers slowed every other block of the launch (its
-// span 15.6 -> 25 us, profiles/r05/s27).
+// span 15.6 -> 25 us, profiles/r05/s27; polling every ~1 us instead, 30 us,
+// s31: the b1 blocks' arrivals queue behind the polls of the same word).
 constexpr int HVP_B1 = C1M;  // 400
 constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-#if DQZ_HVP_C1_EARLY  // timing experiment: conv1's blocks right after b1, polling every ~1 us
-  constexpr int G1 = HVP_B1, GH = G1 + HVP_G_C1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3,
-                GE = GF + HVP_G_FC;
-  const int i = blockIdx.x;
-  DQZ_STAMP(18, 0);
-  if (i < G1) {
-    hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));
-  } else {
-    const HqOut ho(a);
-    if (i < GH)
-      hvp_g_conv1(a, i - G1, s_r, s_x, ho);
-    else if (i < G2)
-      hvp_g_hidden(a, i - GH, s_r, ho);
-    else if (i < G3)
-      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
-    else if (i < GF)
-      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
-    else if (i < GE)
-      hvp_g_fc1(a, i - GF, ho);
-  }
-  DQZ_STAMP(18, 3);
-#else
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
@@ -772,7 +744,6 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
       hvp_g_conv1(a, i - G1, s_r, s_x, ho);
   }
   DQZ_STAMP(18, 3);
-#endif
 }
 
 // The second order's elementwise stages run in gradient epilogues: the

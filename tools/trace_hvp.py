@@ -32,9 +32,6 @@ RANGES = {
     18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g fc1', 1498),
                 ('g conv1', 1890)], 2147, ('x staged', 'ddot1 wait')),
 }
-if os.environ.get('HVP_C1_EARLY') == '1':  # the -DDQZ_HVP_C1_EARLY=1 timing build's L3 order
-  RANGES[18] = ('L3', [('b1', 0), ('g conv1', 400), ('g hidden', 657), ('g conv2', 665), ('g conv3', 1178),
-                       ('g fc1', 1755)], 2147, ('x staged', 'ddot1 wait'))
 
 
 def main():
