@@ -550,9 +550,9 @@ __device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*
 // ---- the parameter-gradient blocks of H_q w (L3) -------------------------
 //   [257] conv1 rows k (row 256 = bias): sum_p x_p[k] ddot1[p][co] over 8
 //         position splits (thread (split, co)), after b1's hand-off;
-//   [2 x 513] conv2 rows (two 32-channel halves, 8 position splits),
-//   [577] conv3 rows (4 position splits; last row = bias):
-//         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) (thread (split, co));
+//   [513] conv2 rows, [577] conv3 rows (last row = bias):
+//         sum_p (ydot[src] d[p][co] + y[src] ddot[p][co]) over 4 position
+//         splits (thread (split, co));
 //   [8]   fc2 / fc1 bias / fc2 bias: hdot = relu'(h) (bdot1 + sum of t4's
 //         chunk partials), the fc2 column a = hdot; 64 hidden units per
 //         block, the 196 chunk partials of each in 4 groups of 49 loads;
@@ -560,23 +560,16 @@ __device__ __forceinline__ void hvp_b1_block(const HvpArgs& a, int pix, float (*
 // Every per-thread sum issues all its loads before the first addition
 // (round 5: the position and chunk loops waited for one round trip per
 // iteration, 13-21 serial trips, and kept the gradient launch at 12.2 us).
-constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = 2 * (C2KK + 1), HVP_G_C3 = C3KK + 1, HVP_G_H = HID / 64;
+constexpr int HVP_G_C1 = C1KK + 1, HVP_G_C2 = C2KK + 1, HVP_G_C3 = C3KK + 1, HVP_G_H = HID / 64;
 constexpr int HVP_G_FC = FLAT * HID / 16 / 256;  // 392 (hvp_g_fc1: 16 elements per thread)
 
-// Row k of a conv layer's H_q w: NSP position splits x CB output channels
-// per block (the block's channel half h when CB < CO), every per-thread
-// sum's loads issued first; at most 4 x ceil(P / NSP) loads per thread
-// (conv2 at 4 splits took 84, past a wave's 63 in flight).
-template <int IH, int CI, int K, int S, int CO, int OH, int NSP>
+template <int IH, int CI, int K, int S, int CO, int OH>
 __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y, const float* yd, const float* d,
-                                               const float* dd, int k, int h, int64_t off_w, int64_t off_b,
-                                               float (*s_r)[64], const HqOut& ho) {
+                                               const float* dd, int k, int64_t off_w, int64_t off_b, float (*s_r)[64],
+                                               const HqOut& ho) {
   if (DQZ_EXP_HVP_SKIP & 8) return;
-  constexpr int CB = 256 / NSP;
-  static_assert(NSP == 4 || NSP == 8, "position splits");
-  static_assert(CO % CB == 0, "channel blocks");
-  const int t = threadIdx.x, cl = t % CB, co = h * CB + cl, sp = t / CB;
-  constexpr int P = OH * OH, PS = (P + NSP - 1) / NSP;
+  const int t = threadIdx.x, co = t & 63, sp = t >> 6;  // 4 position splits
+  constexpr int P = OH * OH, PS = (P + 3) / 4;
   const int p0 = sp * PS;
   float g = 0.f;
   if (k == K * K * CI) {
@@ -602,15 +595,14 @@ __device__ __forceinline__ void hvp_g_conv_row(const HvpArgs& a, const float* y,
     for (int j = 0; j < PS; ++j)
       if (p0 + j < P) g += u0[j] * u1[j] + w0[j] * w1[j];
   }
-  s_r[sp][cl] = g;
+  s_r[sp][co] = g;
   __syncthreads();
-  if (t < CB) {
-    float v = (s_r[0][t] + s_r[1][t]) + (s_r[2][t] + s_r[3][t]);
-    if constexpr (NSP == 8) v += (s_r[4][t] + s_r[5][t]) + (s_r[6][t] + s_r[7][t]);
+  if (t < CO) {
+    const float v = (s_r[0][t] + s_r[1][t]) + (s_r[2][t] + s_r[3][t]);
     if (k == K * K * CI)
-      ho.put(a, off_b + co, v);
+      ho.put(a, off_b + t, v);
     else
-      ho.put(a, off_w + (int64_t)k * CO + co, v);
+      ho.put(a, off_w + (int64_t)k * CO + t, v);
   }
 }
 
@@ -729,7 +721,7 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
 // span 15.6 -> 25 us, profiles/r05/s27; polling every ~1 us instead, 30 us,
 // s31: the b1 blocks' arrivals queue behind the polls of the same word).
 constexpr int HVP_B1 = C1M;  // 400
-constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,660
+constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
@@ -743,11 +735,9 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
     if (i < G2)
       hvp_g_hidden(a, i - GH, s_r, ho);
     else if (i < G3)
-      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O, 8>(a, a.y1, a.ty1, a.d2, a.td2, (i - G2) >> 1, (i - G2) & 1,
-                                                        a.off[2], a.off[3], s_r, ho);
+      hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
     else if (i < GF)
-      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O, 4>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, 0, a.off[4], a.off[5], s_r,
-                                                    ho);
+      hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
     else if (i < G1)
       hvp_g_fc1(a, i - GF, ho);
     else

@@ -412,7 +412,6 @@ __device__ __forceinline__ float meta_s_row(const float4 (&r)[META_DOT_SLOTS / 4
 // first reduction (the loops over the partials had issued one load per
 // dependent iteration); entries and partials past those take the loops.
 constexpr int META_ADAM_LP = 16;
-constexpr int META_ADAM_LP4 = 4;  // meta_adam_chunks_kernel: 4 float4 of partials per thread
 __device__ __forceinline__ void meta_adam_body(const MetaAdamArgs& a) {
   __shared__ float sbuf[META_THREADS / 64];
   const int t = threadIdx.x;
@@ -602,14 +601,9 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
 #pragma unroll
     for (int u = 0; u < META_DOT_SLOTS / 4; ++u) dr[u] = q[u];
   }
-  // the loss partials as 16-byte loads: 4 x 4 per thread (16 scalar loads
-  // took the block past a wave's 63 loads in flight, so its last loads —
-  // x, p, m, v — waited for the first to return).  The buffer holds
-  // nparts2 >= FLAT * HID / 256 floats, so the 4,096 read are in range.
-  static_assert(FLAT * HID / 256 >= 4 * META_ADAM_LP4 * META_THREADS, "loss partial buffer");
-  float4 lpv[META_ADAM_LP4];
+  float lpv[META_ADAM_LP];
 #pragma unroll
-  for (int r = 0; r < META_ADAM_LP4; ++r) lpv[r] = reinterpret_cast<const float4*>(a.loss_part)[t + r * META_THREADS];
+  for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
   const float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
   const int32_t cnt = *a.count + 1;
   LogitRun r = *a.run;
@@ -631,14 +625,9 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   float lp = 0.f;
   if (leader) {
 #pragma unroll
-    for (int u = 0; u < META_ADAM_LP4; ++u) {
-      const int j = 4 * (t + u * META_THREADS);
-      const float e[4] = {lpv[u].x, lpv[u].y, lpv[u].z, lpv[u].w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (j + c < a.nparts) lp += e[c];
-    }
-    for (int j = t + 4 * META_ADAM_LP4 * META_THREADS; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
+    for (int u = 0; u < META_ADAM_LP; ++u)
+      if (t + u * META_THREADS < a.nparts) lp += lpv[u];
+    for (int j = t + META_ADAM_LP * META_THREADS; j < a.nparts; j += META_THREADS) lp += a.loss_part[j];
     lp = block_sum_f32(lp, sbuf);
   }
   const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);

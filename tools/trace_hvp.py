@@ -29,8 +29,8 @@ B, A, M = 32, 6, 100
 RANGES = {
     16: ('L1', [('t12', 0), ('s1', 324), ('b3', 325)], 521, ('tile staged', 'ty1 reduced')),
     17: ('L2', [('t34', 0), ('b2', 196)], 520, ('ty3 sums', '')),
-    18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 1434), ('g fc1', 2011),
-                ('g conv1', 2403)], 2660, ('x staged', 'ddot1 wait')),
+    18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g fc1', 1498),
+                ('g conv1', 1890)], 2147, ('x staged', 'ddot1 wait')),
 }
 
 
