@@ -139,14 +139,15 @@ def test_meta_update_matches_oracle(device, meta_batch):
   np.testing.assert_allclose(state.mu, ref['adam_m'], atol=1e-5 * np.abs(ref['adam_m']).max())
 
 
-@pytest.mark.parametrize('bound,meta_batch', [(5.0, 8), (1.0 / 32, 8), (5.0, 260)])
-def test_second_order_meta_update_matches_oracle(device, bound, meta_batch):
+@pytest.mark.parametrize('bound,meta_batch,a', [(5.0, 8, 6), (1.0 / 32, 8, 6), (5.0, 260, 6), (5.0, 8, 18)])
+def test_second_order_meta_update_matches_oracle(device, bound, meta_batch, a):
   """dqn_mgsc_batched_reservoir: no stop_gradient on theta'' (HVP path);
-  meta_batch 260 runs as two chunks (256 + 4 padded to 256)."""
+  meta_batch 260 runs as two chunks (256 + 4 padded to 256).  A = 18 takes
+  the HVP's other branches: b3 gathers Wdot2[:, a] instead of staging Wdot2
+  in LDS (A > 16), and the fc2 / bias puts run in two batches (A + 1 > 9)."""
   from dqn_mgsc_zoo_amd import learner as learner_lib
   from dqn_mgsc_zoo_amd import networks
   from dqn_mgsc_zoo_amd import replay as replay_lib
-  a = 6
   net = networks.dqn_atari_network(a)
   online = net.init(51)
   target = helpers.perturbed_tree(online, 52)
@@ -164,19 +165,20 @@ def test_second_order_meta_update_matches_oracle(device, bound, meta_batch):
   pos = rng.choice(logits.size, meta_batch, replace=False).astype(np.int32)
   ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
   ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
-  ot = replay_lib.Transition(ot_tm1, 2, 1.0, 0.99, ot_t)
+  oa = 2 if a == 6 else 13  # A = 18: the online action past the first put batch
+  ot = replay_lib.Transition(ot_tm1, oa, 1.0, 0.99, ot_t)
   mb = dict(s_tm1=helpers.stacks_from(host['frames'], host['fidx'], slots, 0),
             a_tm1=host['action'][slots], r_t=host['reward'][slots],
             discount_t=host['discount'][slots],
             s_t=helpers.stacks_from(host['frames'], host['fidx'], slots, 1))
   ref = learner_ref.meta_update(
       _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
-      dict(s_tm1=ot_tm1, a_tm1=2, r_t=1.0, discount_t=0.99, s_t=ot_t),
+      dict(s_tm1=ot_tm1, a_tm1=oa, r_t=1.0, discount_t=0.99, s_t=ot_t),
       np.zeros(meta_batch), np.zeros(meta_batch), 0, grad_error_bound=bound,
       stop_gradient=False)
   first = learner_ref.meta_update(
       _f64(online), _f64(target), _f64(mu), _f64(nu), mb, logits[pos],
-      dict(s_tm1=ot_tm1, a_tm1=2, r_t=1.0, discount_t=0.99, s_t=ot_t),
+      dict(s_tm1=ot_tm1, a_tm1=oa, r_t=1.0, discount_t=0.99, s_t=ot_t),
       np.zeros(meta_batch), np.zeros(meta_batch), 0, grad_error_bound=bound)
   meta.set_online_transition(ot)
   logits_d = torch.from_numpy(logits).to(device)
