@@ -42,9 +42,6 @@
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
 #endif
-#ifndef DQZ_HVP_L3_ORDER
-#define DQZ_HVP_L3_ORDER 0
-#endif
 
 namespace dqz {
 
@@ -716,23 +713,21 @@ __device__ __forceinline__ void hvp_g_conv1(const HvpArgs& a, int k, float (*s_r
   }
 }
 
-// L3: b1 first, then every parameter block that does not need ddot1 (the
+// L3: b1 first, then the conv parameter rows that do not need ddot1 (the
 // fc2 / bias rows first: the longest-lived), then conv1's, which wait
 // in-launch for the 400 b1 blocks (all dispatched before any of them on
-// every XCD, so the wait cannot hold a b1 block out).  With the conv1 blocks
+// every XCD, so the wait cannot hold a b1 block out), then the streaming fc1
+// range, which fills the slots while conv1's rows finish (conv1's rows last:
+// span 14.2 us against 12.9, profiles/r05/s33).  With the conv1 blocks
 // right after b1, 257 pollers slowed every other block of the launch (its
-// span 15.6 -> 25 us, profiles/r05/s27; polling every ~1 us instead, 30 us,
-// s31: the b1 blocks' arrivals queue behind the polls of the same word).
+// span 15.6 -> 25 us, s27; polling every ~1 us instead, 30 us, s31: the b1
+// blocks' arrivals queue behind the polls of the same word).
 constexpr int HVP_B1 = C1M;  // 400
 constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC + HVP_G_C1;  // 2,147
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-#if DQZ_HVP_L3_ORDER  // experiment: conv1's rows before the fc1 range
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, G1 = G3 + HVP_G_C3, GF = G1 + HVP_G_C1;
-#else
-  constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, GF = G3 + HVP_G_C3, G1 = GF + HVP_G_FC;
-#endif
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
   if (i < GH) {
@@ -743,12 +738,12 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
       hvp_g_hidden(a, i - GH, s_r, ho);
     else if (i < G3)
       hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
-    else if (i < G3 + HVP_G_C3)
+    else if (i < G1)
       hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
-    else if (i >= GF && i < GF + HVP_G_FC)
-      hvp_g_fc1(a, i - GF, ho);
-    else
+    else if (i < GF)
       hvp_g_conv1(a, i - G1, s_r, s_x, ho);
+    else
+      hvp_g_fc1(a, i - GF, ho);
   }
   DQZ_STAMP(18, 3);
 }

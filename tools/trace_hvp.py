@@ -29,12 +29,9 @@ B, A, M = 32, 6, 100
 RANGES = {
     16: ('L1', [('t12', 0), ('s1', 324), ('b3', 325)], 521, ('tile staged', 'ty1 reduced')),
     17: ('L2', [('t34', 0), ('b2', 196)], 520, ('ty3 sums', '')),
-    18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g fc1', 1498),
-                ('g conv1', 1890)], 2147, ('x staged', 'ddot1 wait')),
+    18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g conv1', 1498),
+                ('g fc1', 1755)], 2147, ('x staged', 'ddot1 wait')),
 }
-if os.environ.get('HVP_L3_ORDER') == '1':  # the -DDQZ_HVP_L3_ORDER=1 build: conv1's rows before fc1's
-  RANGES[18] = ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g conv1', 1498),
-                       ('g fc1', 1755)], 2147, ('x staged', 'ddot1 wait'))
 
 
 def main():
