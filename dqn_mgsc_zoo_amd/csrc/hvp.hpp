@@ -42,9 +42,6 @@
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
 #endif
-#ifndef DQZ_HVP_L3_ORDER
-#define DQZ_HVP_L3_ORDER 0
-#endif
 
 namespace dqz {
 
@@ -730,11 +727,7 @@ constexpr int HVP_L3_BLOCKS = HVP_B1 + HVP_G_H + HVP_G_C2 + HVP_G_C3 + HVP_G_FC 
 __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_r[8][64];
   __shared__ float s_x[C1M];
-#if DQZ_HVP_L3_ORDER == 2  // experiment: conv1's rows between conv2's and conv3's
-  constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G1 = G2 + HVP_G_C2, G3 = G1 + HVP_G_C1, GF = G3 + HVP_G_C3;
-#else
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, G1 = G3 + HVP_G_C3, GF = G1 + HVP_G_C1;
-#endif
   const int i = blockIdx.x;
   DQZ_STAMP(18, 0);
   if (i < GH) {
@@ -743,11 +736,11 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
     const HqOut ho(a);
     if (i < G2)
       hvp_g_hidden(a, i - GH, s_r, ho);
-    else if (i < G2 + HVP_G_C2)
+    else if (i < G3)
       hvp_g_conv_row<C1O, C1CO, C2K, C2S, C2CO, C2O>(a, a.y1, a.ty1, a.d2, a.td2, i - G2, a.off[2], a.off[3], s_r, ho);
-    else if (i >= G3 && i < G3 + HVP_G_C3)
+    else if (i < G1)
       hvp_g_conv_row<C2O, C2CO, C3K, 1, C3CO, C3O>(a, a.y2, a.ty2, a.d3, a.td3, i - G3, a.off[4], a.off[5], s_r, ho);
-    else if (i >= G1 && i < G1 + HVP_G_C1)
+    else if (i < GF)
       hvp_g_conv1(a, i - G1, s_r, s_x, ho);
     else
       hvp_g_fc1(a, i - GF, ho);

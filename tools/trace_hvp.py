@@ -32,9 +32,6 @@ RANGES = {
     18: ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv3', 921), ('g conv1', 1498),
                 ('g fc1', 1755)], 2147, ('x staged', 'ddot1 wait')),
 }
-if os.environ.get('HVP_L3_ORDER') == '2':  # the -DDQZ_HVP_L3_ORDER=2 build: conv1's rows before conv3's
-  RANGES[18] = ('L3', [('b1', 0), ('g hidden', 400), ('g conv2', 408), ('g conv1', 921), ('g conv3', 1178),
-                       ('g fc1', 1755)], 2147, ('x staged', 'ddot1 wait'))
 
 
 def main():
