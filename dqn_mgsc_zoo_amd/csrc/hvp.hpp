@@ -37,7 +37,8 @@
 // Timing-only builds (tools/gpu_hvp_split.sh): DQZ_EXP_HVP_SKIP is a mask of
 // block ranges that return at once (1 t12, 2 b3, 4 b1's sums — its arrival
 // stays, 8 conv2 / conv3 parameter rows, 16 fc1 parameters, 32 conv1
-// parameter rows, 64 t34, 128 b2).  The numerics of those builds are wrong
+// parameter rows, 64 t34, 128 b2; 256 / 512: t12 without its input-tile /
+// Wdot1 loads).  The numerics of those builds are wrong
 // by design.
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
@@ -165,13 +166,15 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const int px = min(t + 256 * u, N - 1) >> 2;  // element e = pixel * 4 + channel, channel = t % 4
-      xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
+      xb[u] = (DQZ_EXP_HVP_SKIP & 256) ? (unsigned)px : fr[(px / T12_IN) * FW + px % T12_IN];
     }
   }
   constexpr int W1Q = C1KK * C1CO / 4 / 256;  // 8 float4 per thread
   float4 wl[W1Q];
 #pragma unroll
-  for (int u = 0; u < W1Q; ++u) wl[u] = reinterpret_cast<const float4*>(a.tw + a.off[0])[t + 256 * u];
+  for (int u = 0; u < W1Q; ++u)
+    wl[u] = (DQZ_EXP_HVP_SKIP & 512) ? make_float4(t, u, 0.f, 1.f)
+                                     : reinterpret_cast<const float4*>(a.tw + a.off[0])[t + 256 * u];
   float y1v[2];
   int p1[2];
 #pragma unroll
