@@ -37,8 +37,7 @@
 // Timing-only builds (tools/gpu_hvp_split.sh): DQZ_EXP_HVP_SKIP is a mask of
 // block ranges that return at once (1 t12, 2 b3, 4 b1's sums — its arrival
 // stays, 8 conv2 / conv3 parameter rows, 16 fc1 parameters, 32 conv1
-// parameter rows, 64 t34, 128 b2; 256 / 512: t12 without its input-tile /
-// Wdot1 loads).  The numerics of those builds are wrong
+// parameter rows, 64 t34, 128 b2).  The numerics of those builds are wrong
 // by design.
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
@@ -133,7 +132,7 @@ constexpr int T12_IN = C1S * 3 + C1K;  // 20
 struct HvpT12Smem {
   float4 in[T12_IN * T12_IN];  // [row][col], the 4 channels of one pixel
   union {
-    float w1[C1KK][C1CO];       // Wdot1, staged with 16-byte loads
+    float w1[C1KK][C1CO];       // Wdot1, staged by 16-byte global_load_lds (lane-linear)
     float r[16][C1K][C1CO];     // then: conv1 kh partials per window position
   };
   float t1[16][C1CO];           // ty1 over the window
@@ -157,8 +156,8 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   const int oh = p / C2O, ow = p % C2O;
   const int kh = t >> 5, co = t & 31;
   // the input tile's bytes (the theta' forward's copy: one trip, no slot ->
-  // frame-index -> frame chain) and every other load together (no branch
-  // among the loads: a branch made the compiler drain them all)
+  // frame-index -> frame chain), Wdot1 and the window's y1 (no branch among
+  // the loads: a branch made the compiler drain them all)
   constexpr int N = T12_IN * T12_IN * FC, R = (N + 255) / 256;  // 1600 tile elements, 7 rounds
   unsigned xb[R];
   {
@@ -166,15 +165,21 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const int px = min(t + 256 * u, N - 1) >> 2;  // element e = pixel * 4 + channel, channel = t % 4
-      xb[u] = (DQZ_EXP_HVP_SKIP & 256) ? (unsigned)px : fr[(px / T12_IN) * FW + px % T12_IN];
+      xb[u] = fr[(px / T12_IN) * FW + px % T12_IN];
     }
   }
+  // Wdot1 straight into LDS (global_load_lds, 16 bytes a lane: no registers,
+  // in flight beside the tile's bytes; through registers the scheduler issued
+  // them after the bytes had landed, or spilled them)
   constexpr int W1Q = C1KK * C1CO / 4 / 256;  // 8 float4 per thread
-  float4 wl[W1Q];
+  {
+    const float4* wg = reinterpret_cast<const float4*>(a.tw + a.off[0]);
+    float4* wl = reinterpret_cast<float4*>(&s.w1[0][0]);
 #pragma unroll
-  for (int u = 0; u < W1Q; ++u)
-    wl[u] = (DQZ_EXP_HVP_SKIP & 512) ? make_float4(t, u, 0.f, 1.f)
-                                     : reinterpret_cast<const float4*>(a.tw + a.off[0])[t + 256 * u];
+    for (int u = 0; u < W1Q; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(wg + t + 256 * u),
+                                       (__attribute__((address_space(3))) void*)(wl + 256 * u + 64 * (t >> 6)), 16, 0, 0);
+  }
   float y1v[2];
   int p1[2];
 #pragma unroll
@@ -183,6 +188,18 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
     p1[h] = (2 * oh + (pos >> 2)) * C1O + 2 * ow + (pos & 3);
     y1v[h] = a.y1[p1[h] * C1CO + co];
   }
+  const float b1v = a.tw[a.off[1] + co];
+  {
+    float* in = reinterpret_cast<float*>(s.in);
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (t + 256 * u < N) in[t + 256 * u] = u8n(xb[u]);
+  }
+  __syncthreads();
+  DQZ_STAMP(16, 1);
+  // the conv2 operands, in flight under the conv1 tangent (issued before the
+  // barrier, they held it until every one had landed: 4.4 us to the staged
+  // tile against 3.2 with no loads at all, profiles/r05/s35)
   const int tap = t >> 4, cq = (t >> 2) & 3, cg = t & 3;
   const int src = ((2 * oh + (tap >> 2)) * C1O + 2 * ow + (tap & 3)) * C1CO + 8 * cg;
   const int64_t wo = (int64_t)(tap * C2CI + 8 * cg) * C2CO + 16 * g + 4 * cq;
@@ -197,17 +214,6 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   const int c2 = 16 * g + (t & 15);
   const float y2v = a.y2[p * C2CO + c2];  // used by t < 16
   const float b2v = a.tw[a.off[3] + c2];
-  const float b1v = a.tw[a.off[1] + co];
-  {
-    float* in = reinterpret_cast<float*>(s.in);
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (t + 256 * u < N) in[t + 256 * u] = u8n(xb[u]);
-#pragma unroll
-    for (int u = 0; u < W1Q; ++u) reinterpret_cast<float4*>(&s.w1[0][0])[t + 256 * u] = wl[u];
-  }
-  __syncthreads();
-  DQZ_STAMP(16, 1);
   float wv[C1K * FC];  // row kh of Wdot1, column co: (kw, ci) as j = 4 kw + ci
 #pragma unroll
   for (int j = 0; j < C1K * FC; ++j) wv[j] = s.w1[kh * C1K * FC + j][co];
