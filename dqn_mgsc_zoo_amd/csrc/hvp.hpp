@@ -133,15 +133,15 @@ struct HvpT12Smem {
   float4 in[T12_IN * T12_IN];  // [row][col], the 4 channels of one pixel
   union {
     float w1[C1KK][C1CO];       // Wdot1, staged by 16-byte global_load_lds (lane-linear)
-    float r[16][C1K][C1CO];     // then: conv1 kh partials per window position
+    float r[4][16][C1CO];       // then: the waves' conv1 partials [wave][position][channel]
   };
   float t1[16][C1CO];           // ty1 over the window
   float r2[64][16];             // conv2 (tap, input-channel group) partials
 };
 
 // t1 + t2: ty1 = relu'(y1) (bdot1 + sum_k x_p[k] Wdot1[k][co]) over the
-// block's window (thread (kh = t / 32, co = t % 32) sums kw, ci of row kh
-// for each window position; the 8 kh partials are summed in order), then
+// block's window (an f32 MFMA product per wave over two kh rows; the four
+// wave partials summed in a fixed order), then
 // ty2 = relu'(y2) (bdot2 + conv(y1, Wdot2) + conv(ty1, W2)) for 16 channels
 // (thread (tap = t / 16, co quad cq = t / 4 % 4, input-channel group cg =
 // t % 4): 4 output channels x 8 input channels with 16-byte loads; the 64
@@ -214,34 +214,35 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   const int c2 = 16 * g + (t & 15);
   const float y2v = a.y2[p * C2CO + c2];  // used by t < 16
   const float b2v = a.tw[a.off[3] + c2];
-  float wv[C1K * FC];  // row kh of Wdot1, column co: (kw, ci) as j = 4 kw + ci
+  // conv1 tangent on v_mfma_f32_16x16x4_f32 (exact f32 products):
+  // D[pos][co] = sum_k x[pos][k] Wdot1[k][co], k = (kh, kw, ci), wave w
+  // summing kh = 2 w, 2 w + 1 (16 K-steps of 4), two 16-channel tiles.
+  // Lane l holds A[pos = l % 16][k = 4 s + l / 16] and B[k][co = l % 16]; D
+  // rows 4 (l / 16) .. + 3, column l % 16.  (VALU dot products from LDS
+  // took 4.7 us of the block, s36.)
+  {
+    const int lane = t & 63, wv = t >> 6, mi = lane & 15, kq = lane >> 4;
+    const float* inf = reinterpret_cast<const float*>(s.in);
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < C1K * FC; ++j) wv[j] = s.w1[kh * C1K * FC + j][co];
-  float zp[16];
-#pragma unroll
-  for (int pos = 0; pos < 16; ++pos) {
-    const float4* row = s.in + (4 * (pos >> 2) + kh) * T12_IN + 4 * (pos & 3);
-    float z = 0.f;
-#pragma unroll
-    for (int kw = 0; kw < C1K; ++kw) {
-      const float4 x = row[kw];
-      z += x.x * wv[4 * kw];
-      z += x.y * wv[4 * kw + 1];
-      z += x.z * wv[4 * kw + 2];
-      z += x.w * wv[4 * kw + 3];
+    for (int st = 0; st < 16; ++st) {
+      const int khh = 2 * wv + (st >> 3), kw = st & 7, k = khh * C1K * FC + kw * FC + kq;
+      const float av = inf[((4 * (mi >> 2) + khh) * T12_IN + 4 * (mi & 3) + kw) * 4 + kq];
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, s.w1[k][mi], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, s.w1[k][16 + mi], acc1, 0, 0, 0);
     }
-    zp[pos] = z;
-  }
-  __syncthreads();  // s.r overwrites s.w1
+    __syncthreads();  // s.r overwrites s.w1
 #pragma unroll
-  for (int pos = 0; pos < 16; ++pos) s.r[pos][kh][co] = zp[pos];
+    for (int r = 0; r < 4; ++r) {
+      s.r[wv][4 * kq + r][mi] = acc0[r];
+      s.r[wv][4 * kq + r][16 + mi] = acc1[r];
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int pos = kh + 8 * h, dy = pos >> 2, dx = pos & 3;
-    float v = b1v;
-#pragma unroll
-    for (int k = 0; k < C1K; ++k) v += s.r[pos][k][co];
+    const float v = b1v + ((s.r[0][pos][co] + s.r[1][pos][co]) + (s.r[2][pos][co] + s.r[3][pos][co]));
     const float ty = y1v[h] > 0.f ? v : 0.f;
     s.t1[pos][co] = ty;
     if (g == 0 && (dy < 2 || oh == C2O - 1) && (dx < 2 || ow == C2O - 1)) a.ty1[p1[h] * C1CO + co] = ty;
