@@ -223,21 +223,13 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
   {
     const int lane = t & 63, wv = t >> 6, mi = lane & 15, kq = lane >> 4;
     const float* inf = reinterpret_cast<const float*>(s.in);
-    // every operand read before the first product (one LDS latency, not 16)
-    float av[16], b0[16], b1[16];
-#pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const int khh = 2 * wv + (st >> 3), kw = st & 7, k = khh * C1K * FC + kw * FC + kq;
-      av[st] = inf[((4 * (mi >> 2) + khh) * T12_IN + 4 * (mi & 3) + kw) * 4 + kq];
-      b0[st] = s.w1[k][mi];
-      b1[st] = s.w1[k][16 + mi];
-    }
-    __builtin_amdgcn_sched_barrier(0);  // the scheduler had interleaved them again, one wait per step
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], b0[st], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], b1[st], acc1, 0, 0, 0);
+      const int khh = 2 * wv + (st >> 3), kw = st & 7, k = khh * C1K * FC + kw * FC + kq;
+      const float av = inf[((4 * (mi >> 2) + khh) * T12_IN + 4 * (mi & 3) + kw) * 4 + kq];
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, s.w1[k][mi], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, s.w1[k][16 + mi], acc1, 0, 0, 0);
     }
     __syncthreads();  // s.r overwrites s.w1
 #pragma unroll
