@@ -46,8 +46,7 @@
 #ifndef DQZ_LAYOUT_PAD
 #define DQZ_LAYOUT_PAD 540
 #endif
-#define DQZ_STR(x) #x
-#define DQZ_XSTR(x) DQZ_STR(x)
+
 
 namespace dqz {
 
