@@ -773,10 +773,6 @@ constexpr int FC1X1_BLOCKS = FLAT / FC1X1_ROWS;  // 98
 template <int AMAX, int SMAX, int ZMAX>
 __global__ __launch_bounds__(512) void head_dx1_kernel(HeadArgs h, Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float s_dz[HID];
-#if DQZ_LAYOUT_PAD2 > 0
-  if constexpr (AMAX == 32 && ZMAX == 3)
-    if (a.w_off < 0) asm volatile(".fill " DQZ_XSTR(DQZ_LAYOUT_PAD2) ", 4, 0xbf800000");
-#endif
   DQZ_STAMP(5, 0);
   const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
   const int row0 = FC1X1_ROWS * blockIdx.x + 16 * half;

@@ -17,12 +17,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define DQZ_STR(x) #x
 #define DQZ_XSTR(x) DQZ_STR(x)
-// Code-layout experiment ("Code layout"): never-executed s_nop
-// words in head_dx1_kernel<32, 7, 3>, which the compiler emits between the
-// learner's head and its forward / backward kernels (0: none)
-#ifndef DQZ_LAYOUT_PAD2
-#define DQZ_LAYOUT_PAD2 0
-#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------------------
