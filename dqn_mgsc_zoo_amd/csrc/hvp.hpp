@@ -44,7 +44,7 @@
 #endif
 // hvp_l3_kernel's code-layout filler, in 4-byte words ("Code layout")
 #ifndef DQZ_LAYOUT_PAD
-#define DQZ_LAYOUT_PAD 540
+#define DQZ_LAYOUT_PAD 476
 #endif
 
 
