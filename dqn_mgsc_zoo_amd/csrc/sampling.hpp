@@ -1252,9 +1252,6 @@ __device__ __forceinline__ void per_publish_weight(const PerSampleArgs& a, int b
 __global__ __launch_bounds__(ST_FAST) void per_add_kernel(double* tree, int64_t cap, int levels, int32_t remove_idx,
                                                           int32_t add_idx, double priority, const double* max_seen,
                                                           double alpha, int32_t* index_to_slot, int32_t slot) {
-#if DQZ_LAYOUT_PAD0 > 0  // code-layout experiment: moves every kernel emitted after this one
-  if (cap < 0) asm volatile(".fill " DQZ_XSTR(DQZ_LAYOUT_PAD0) ", 4, 0xbf800000");
-#endif
   const int i = threadIdx.x;
   int64_t leaf = -1;
   double v = 0.0;
