@@ -887,10 +887,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const int B8 = (c3.B + 7) / 8 * 8;
   constexpr int NF = 4 * (FLAT / 16);  // 784 fc1 dW blocks (a multiple of 8)
   int i = blockIdx.x;
-#if DQZ_LAYOUT_PAD3 > 0  // code-layout experiment: moves bwd_bc_kernel<false>, emitted after this one
-  if constexpr (WB)
-    if (c3.B < 0) asm volatile(".fill " DQZ_XSTR(DQZ_LAYOUT_PAD3) ", 4, 0xbf800000");
-#endif
   if constexpr (WB) {
     if (i < 8) {
       if (i == 0 && threadIdx.x < 64) per_write_back_wave(wb, reinterpret_cast<char*>(smem));

@@ -17,9 +17,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define DQZ_STR(x) #x
 #define DQZ_XSTR(x) DQZ_STR(x)
-#ifndef DQZ_LAYOUT_PAD3
-#define DQZ_LAYOUT_PAD3 0
-#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------------------
