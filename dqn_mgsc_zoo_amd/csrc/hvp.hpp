@@ -54,8 +54,9 @@ struct HvpArgs {
   // x: the online transition's s_tm1 bytes [4][84][84], copied by the theta'
   // forward's conv1 stage (Conv1Src::xout)
   const uint8_t* x;
-  const int32_t* slot;
-  const int32_t* action;  // store action table (a = action[slot])
+  // the one-transition learner's batch record {a as int bits, r, d, 0}, which
+  // the theta' forward copied from the store (a in one trip, not slot -> action)
+  const float4* rec;
   const float* th;        // primal params theta'
   const float* tw;        // tangent params w (same layout)
   int64_t off[10];
@@ -281,7 +282,7 @@ __device__ __forceinline__ void hvp_t12_block(const HvpArgs& a, int i, HvpT12Sme
 // for the gradient blocks.
 __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
   const int t = threadIdx.x;
-  const int act = a.action[a.slot[0]];
+  const int act = __float_as_int(a.rec[0].x);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int n = t + 256 * h;
@@ -304,14 +305,13 @@ __device__ __forceinline__ void hvp_s1_block(const HvpArgs& a, float* s_w) {
 // 16 rows per block, wave w rows 16 i + 4 w .. + 3 (lane l: columns 8 l ..
 // 8 l + 7, 16-byte loads, all four rows' loads issued together); the lane's
 // eight ddot4 = relu'(h) Wdot2[n][a] are formed here.  For A <= 16 the block
-// stages all of Wdot2 (512 x A) in LDS beside the row loads, so the slot ->
-// action chain runs under them instead of before a third trip (the gathers
-// of column a).
+// stages all of Wdot2 (512 x A) in LDS beside the row loads, so a's load
+// runs under them instead of before another trip (the gathers of column a).
 __device__ __forceinline__ void hvp_b3_block(const HvpArgs& a, int i, float* s_w2) {
   if (DQZ_EXP_HVP_SKIP & 2) return;
   constexpr int R = 4;
   const int t = threadIdx.x, lane = t & 63, k0 = 16 * i + R * (t >> 6);
-  const int act = a.action[a.slot[0]];
+  const int act = __float_as_int(a.rec[0].x);
   const bool staged = a.A <= 16;
   float4 wq[8];  // Wdot2 as float4: 128 A elements, A / 2 per thread (A <= 16; always in range)
 #pragma unroll
@@ -637,7 +637,7 @@ __device__ __forceinline__ void hvp_g_hidden(const HvpArgs& a, int i, float (*s_
   s_r[q][nl] = zq;
   __syncthreads();
   if (q != 0) return;
-  const int act = a.action[a.slot[0]];
+  const int act = __float_as_int(a.rec[0].x);
   const float z = a.tw[a.off[7] + n] + ((s_r[0][nl] + s_r[1][nl]) + (s_r[2][nl] + s_r[3][nl]));
   const float hd = a.h[n] > 0.f ? z : 0.f;
   // the row's A fc2 entries and the fc1 bias: every put's loads before its

@@ -1308,8 +1308,7 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
     const int nparts1 = 4 * (FLAT / 16) + (int)update_blocks(L1->sz, A, L1->shared_bias ? 1 : A);
     HvpArgs hv{};
     hv.x = H->x1;
-    hv.slot = online_slot;
-    hv.action = S1->action;
+    hv.rec = reinterpret_cast<const float4*>(L1->rec);
     hv.th = H->thp;
     hv.tw = H->nu1;
     for (int i = 0; i < 10; ++i) hv.off[i] = L1->off[i];
