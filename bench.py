@@ -470,9 +470,15 @@ def selftest_cpu(args, g, rem):
   elapsed_max = reps.max_over_ranks(elapsed)
   per_rank = reps.gather_stats([counters['steps'] - warm, elapsed,
                                 counters['syncs'], counters['gathers']])
-  # device identities: stand-ins here (DQZ_SELFTEST_DEVICE overrides the
-  # per-rank default, so a test can make two ranks collide)
-  stand_in = os.environ.get('DQZ_SELFTEST_DEVICE', 'stand-in-%d' % reps.rank)
+  # device identities: stand-ins here.  DQZ_SELFTEST_DEVICE overrides the
+  # per-rank default so a test can make ranks collide: a plain name applies
+  # to every rank, 'r=name,...' to the ranks it lists
+  stand_in = 'stand-in-%d' % reps.rank
+  spec = os.environ.get('DQZ_SELFTEST_DEVICE')
+  if spec and '=' not in spec:
+    stand_in = spec
+  elif spec:
+    stand_in = dict(kv.split('=', 1) for kv in spec.split(',')).get(str(reps.rank), stand_in)
   devices = reps.gather_objects(
       dict(replicas_lib.device_identity(reps.local_rank, stand_in=stand_in),
            fill_s=0.0))
@@ -490,11 +496,14 @@ def selftest_cpu(args, g, rem):
         'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed_max / args.steps,
         'chunks': [g, rem],
         'per_rank_steps': [int(v) for v in per_rank[:, 0]],
+        # the fields the GPU line carries per rank (the stand-in step's rate)
+        'per_rank_steps_per_s': [round(float(v[0] / v[1]), 2) for v in per_rank],
+        'per_gpu_min_steps_per_s': round(float((per_rank[:, 0] / per_rank[:, 1]).min()), 2),
         'per_rank_target_syncs': [int(v) for v in per_rank[:, 2]],
         'per_rank_stats_gathers': [int(v) for v in per_rank[:, 3]],
         'devices': devices,
         'rccl': {'backend': reps.backend, 'world': reps.world,
-                 'last_in_loop_gather': {
+                 'last_in_loop_gather': None if 'stats' not in last else {
                      'steps_done': [int(v) for v in last['stats'][:, 0]],
                      'value': [float(v) for v in last['stats'][:, 1]]}}}),
           flush=True)
@@ -639,6 +648,69 @@ class Workload:
       del meta
     return out
 
+  def time_mgsc_learn(self, graph_steps=20, reps=10):
+    """MGSC only: config 3's whole learn step as the reference runs it on a
+    learn frame (dqn_mgsc_batched/agent.py:253-275, 302-357): the M = 100
+    meta-update (a fresh meta batch each step: uniform without replacement,
+    positions = slots as in the reservoir buffer; the meta batch's logits
+    written back, the running log-sum-exp kept), then the learned-logit draw
+    of 32 slots and the DQN step (one call, the draw inside the forward
+    launch).  A hipGraph of `graph_steps` such steps is replayed `reps`
+    times between HIP events on the capture stream; first and second order
+    (the batched and the reservoir agent).  The per-frame replay add
+    (running log-mean-exp, 14 us per add at 1M) and the host's
+    meta-batch draw are outside the timed graph."""
+    if self.algo != 'mgsc':
+      return {}
+    from dqn_mgsc_zoo_amd import learner as learner_lib  # pylint: disable=g-import-not-at-top
+    dev = self.slots.device
+    rng = np.random.default_rng(400)
+    cap = self.logit_buf.logits.numel()
+    sets = torch.from_numpy(np.stack([
+        rng.choice(cap, META_BATCH, replace=False).astype(np.int32)
+        for _ in range(graph_steps)])).to(dev)
+    lrn, lb, store = self.lrn, self.logit_buf, self.store
+    out = {}
+    for order in (0, 1):
+      meta = learner_lib.MetaLearner(lrn, META_BATCH, learner_lib.adam(2.5e-4),
+                                     second_order=bool(order))
+      meta.set_online_transition(self.meta_online)
+      counter = torch.zeros((1,), dtype=torch.int64, device=dev)
+
+      def learn_step(k, meta=meta, counter=counter):
+        ms = sets[k]
+        meta.update(store, ms, lb.logits, ms, logit_buffer=lb)
+        lrn.step_logits(store, lb, self.slots, seed=7, counter=counter)
+
+      side = torch.cuda.Stream(dev)
+      side.wait_stream(torch.cuda.current_stream(dev))
+      with torch.cuda.stream(side):
+        for k in range(3):  # eager warm-up: the buffer's running state is known
+          learn_step(k)
+      torch.cuda.current_stream(dev).wait_stream(side)
+      graph = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(graph):
+        for k in range(graph_steps):
+          learn_step(k)
+      graph.replay()
+      graph.replay()
+      e0 = torch.cuda.Event(enable_timing=True)
+      e1 = torch.cuda.Event(enable_timing=True)
+      e0.record()
+      for _ in range(reps):
+        graph.replay()
+      e1.record()
+      e1.synchronize()
+      us = 1e3 * e0.elapsed_time(e1) / (reps * graph_steps)
+      status = lrn.sync_status() | meta.sync_status()
+      key = '%s_order' % ('second' if order else 'first')
+      out[key] = {'us_per_learn_step': round(us, 2),
+                  'learn_steps_per_s': round(1e6 / us, 1),
+                  'meta_batch': META_BATCH, 'batch': BATCH,
+                  'steps_timed': reps * graph_steps, 'health': int(status)}
+      del graph, meta
+    return out
+
   def time_samplers(self, iters):
     """Average ms per launch of each sampler call, back to back on the
     launch stream (HIP events on that stream)."""
@@ -774,6 +846,7 @@ def run_gpu(args, g, rem):
     phases = {('conv_fwd' if k == 'conv1_fwd' else k): v for k, v in phases.items()}
   sampler_ms = wl.time_samplers(args.profile_iters)
   meta_ms = wl.time_meta(max(20, args.profile_iters // 10))
+  mgsc_learn = wl.time_mgsc_learn()
   q_tm1, td, loss = lrn.fetch_outputs()
   torch.cuda.synchronize(dev)
   finite = bool(torch.isfinite(lrn.online).all().item())
@@ -894,6 +967,10 @@ def run_gpu(args, g, rem):
                             'achieved_tflops': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS,
                             'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 4)}
     out['meta_roofline'] = meta_roof
+    # config 3 as one learn frame of the reference: meta-update (M = 100),
+    # then the learned-logit draw and the DQN step, in one captured graph;
+    # `value` above stays the learner part alone
+    out['mgsc_learn_step'] = mgsc_learn
   if world == 1 and args.cpu_seconds > 0:
     out['cpu_baseline'] = cpu_baseline(args.cpu_seconds, algo)
   else:

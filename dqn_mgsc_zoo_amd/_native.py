@@ -229,6 +229,8 @@ SIGNATURES = {
         [_vp, ctypes.POINTER(DqzParams), ctypes.POINTER(DqzStore), _vp,
          ctypes.POINTER(DqzStore), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'dqz_meta_outputs': (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    'dqz_meta_sync_status': (_int, [_vp, _vp]),
+    'dqz_meta_debug_stall': (_int, [_vp, _int, ctypes.c_uint]),
 }
 
 _lib = None

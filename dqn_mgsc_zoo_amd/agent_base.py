@@ -117,7 +117,7 @@ class DeviceDqnAgent(parts.Agent):
     reference's jitted update would.  Called every HEALTH_CHECK_PERIOD learn
     steps, at every target sync and from get_state.
     """
-    status = self._learner.sync_status()
+    status = self._health_word()
     first, last = self._last_health_check, self._learn_steps
     self._last_health_check = self._learn_steps
     if status & 2:
@@ -130,6 +130,11 @@ class DeviceDqnAgent(parts.Agent):
           'those updates are invalid; restore the agent from a checkpoint' % (
               first + 1, last, self._frame_t))
     return status
+
+  def _health_word(self) -> int:
+    """The device health word check_learner_health reads (agents with more
+    device state, e.g. the MGSC meta-update, OR theirs in)."""
+    return self._learner.sync_status()
 
   def reset(self) -> None:
     self._transition_accumulator.reset()

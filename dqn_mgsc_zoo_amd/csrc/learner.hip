@@ -59,8 +59,8 @@ struct dqz_learner {
   float *w3p, *w2p;  // dX-ordered weight copies written by fc1_dx_kernel each step
   double* per_wb;    // [B] the fused PER draw's unnormalised IS weights (conv1 -> head)
   int32_t* ga;
-  int32_t* sync;  // hand-off words (x Handoff::kStride): bwd cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each, err,
-                  // dz1 cnt/ack (B = 1, head_dx1_kernel)
+  int32_t* sync;  // hand-off words (x Handoff::kStride): dy2 cnt/ack [B] each, fwd y1/y2 cnt/ack [3B] each,
+                  // dy1 cnt/ack [B] each, then the error word (dqz_learner_sync_status)
   unsigned spin_max = 1u << 24;  // hand-off polls before a wait gives up
   void* block;
 };
@@ -1116,8 +1116,10 @@ struct dqz_meta {
   float *ty1, *ty2, *ty3, *td4, *td3, *td2, *td1, *s1;
   uint8_t* x1;  // [4][84][84] the online transition's s_tm1 bytes (written by the theta' forward)
   float* dotp;  // [C][META_DOT_SLOTS] the tangent launch's dot-product partials (one chunk)
-  int* arrive;  // [0] meta_adam_chunks_kernel's re-seed arrival counter, [kStride, 3 kStride) the
-                // HVP's ddot1 hand-off words (all zero between launches)
+  int* arrive;  // (x Handoff::kStride) [0] meta_adam_chunks_kernel's re-seed arrival counter, [1, 3) the
+                // HVP's ddot1 hand-off words, [3] the Adam entry counter (all zero between launches),
+                // [4] the meta-level error word (dqz_meta_sync_status)
+  unsigned spin_max = 1u << 24;  // polls before the Adam leader's entry wait gives up
   int nparts2;
   void* block;
 };
@@ -1164,7 +1166,7 @@ int dqz_meta_create(const dqz_meta_config* cfg, dqz_meta** out) {
                            so * H->total, so * H->total, so * H->nparts2,
                            so * C1M * C1CO, so * C2M * C2CO, so * FLAT, so * HID, so * FLAT,
                            so * C2M * C2CO, so * C1M * C1CO, so, so * HVP_T4_CHUNKS * HID,
-                           (int64_t)C * META_DOT_SLOTS, 3 * Handoff::kStride, so * FC * FB / 4};
+                           (int64_t)C * META_DOT_SLOTS, 5 * Handoff::kStride, so * FC * FB / 4};
   float** ptrs[] = {&H->G, &H->thp, &H->mu1, &H->nu1, &H->J, &H->zv1, &H->zv2, &H->zv3, &H->zvp,
                     &H->x, &H->p, &H->s, &H->dl, &H->loss, &H->loss_part, &H->td,
                     reinterpret_cast<float**>(&H->slots_pad), &H->Gs,
@@ -1477,9 +1479,11 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   ad.run = keep ? logit_buf->run : nullptr;
   ad.dirty = keep ? logit_buf->dirty : nullptr;
   ad.n_logits = keep ? logit_buf->capacity : 0;
-  if (keep && K == 1 && M <= META_THREADS) {
+  // (the fused form's re-seed path addresses the buffer with 32-bit byte offsets)
+  if (keep && K == 1 && M <= META_THREADS && logit_buf->capacity * 4 <= INT32_MAX) {
     // Adam and the re-sums of the chunks it writes in one launch
-    MetaAdamChunks ck{logit_buf->csum, logit_buf->nblocks, H->arrive};
+    MetaAdamChunks ck{logit_buf->csum, logit_buf->nblocks, H->arrive, H->arrive + 3 * Handoff::kStride,
+                      H->arrive + 4 * Handoff::kStride, H->spin_max};
     hipLaunchKernelGGL(meta_adam_chunks_kernel, dim3(logit_buf->nblocks), dim3(META_THREADS), 0, st, ad, ck);
     DQZ_HIP(hipGetLastError());
     return DQZ_OK;
@@ -1487,6 +1491,42 @@ int dqz_meta_update(dqz_meta* H, const dqz_params* P, const dqz_store* S, const 
   hipLaunchKernelGGL(meta_adam_kernel, dim3(1), dim3(META_THREADS), 0, st, ad);
   DQZ_HIP(hipGetLastError());
   if (keep) return chunk_sums(logit_buf, logits, true, st);
+  return DQZ_OK;
+}
+
+int dqz_meta_sync_status(dqz_meta* H, int* status) {
+  if (!H || !status) return fail(DQZ_ERR_INVALID, "null argument");
+  int s_lm = 0, s_l1 = 0, s_own = 0;
+  // (each learner's check clears that learner's words when its word is set)
+  if (int rc = dqz_learner_sync_status(H->lm, &s_lm)) return rc;
+  if (int rc = dqz_learner_sync_status(H->l1, &s_l1)) return rc;
+  DQZ_HIP(hipMemcpy(&s_own, H->arrive + 4 * Handoff::kStride, sizeof(int), hipMemcpyDeviceToHost));
+  *status = s_lm | s_l1 | s_own;
+  if (*status != 0) {
+    // a wait gave up somewhere in the meta-update: late arrivals may have
+    // left counts behind after a reset, so clear every word the meta handle
+    // owns (its learners' words are cleared just above only when their own
+    // word is set: the HVP's ddot1 timeout lands in l1's word)
+    DQZ_HIP(hipMemset(H->arrive, 0, sizeof(int) * 5 * Handoff::kStride));
+    for (dqz_learner* L : {H->lm, H->l1})
+      DQZ_HIP(hipMemset(L->sync, 0, sizeof(int) * ((16 * L->cfg.batch + 3) * Handoff::kStride + 64)));
+    DQZ_HIP(hipDeviceSynchronize());
+  }
+  return DQZ_OK;
+}
+
+int dqz_meta_debug_stall(dqz_meta* H, int poison, unsigned spin_max) {
+  if (!H) return fail(DQZ_ERR_INVALID, "null meta handle");
+  const unsigned sm = spin_max ? spin_max : 1u << 24;
+  H->spin_max = sm;
+  H->lm->spin_max = sm;
+  H->l1->spin_max = sm;
+  if (poison) {
+    const int32_t p = -(1 << 30);
+    DQZ_HIP(hipDeviceSynchronize());
+    DQZ_HIP(hipMemcpy(H->arrive + Handoff::kStride, &p, sizeof(p), hipMemcpyHostToDevice));      // ddot1 cnt
+    DQZ_HIP(hipMemcpy(H->arrive + 3 * Handoff::kStride, &p, sizeof(p), hipMemcpyHostToDevice));  // Adam entry
+  }
   return DQZ_OK;
 }
 

@@ -516,11 +516,23 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
 // writes.  A tripped guard (rare) is handled by the last of the active
 // blocks to arrive, after every block's logit stores drained write-through:
 // re-scan of the buffer and every chunk sum, with L2-bypassing loads.
+//
+// The leader's stores overwrite state every active block reads at entry (m,
+// v, count, run), and nothing says the grid is resident at once (a large
+// buffer has more chunk blocks than the chip holds, or other work holds the
+// CUs).  So every active block, once its entry loads have returned, adds its
+// number of meta entries to `enter`; the entries partition the M positions,
+// so the leader stores only after `enter` reached M.  Only the leader waits,
+// and every other block runs to its end without waiting, so the wait always
+// ends (bounded anyway: spin_max polls, then bit 0 of `err`).
 
 struct MetaAdamChunks {
   double* csum;  // [nblocks]
   int nblocks;
   int* arrive;   // re-seed arrival counter (zero between launches)
+  int* enter;    // active blocks' entry loads done, in meta entries (zero between launches)
+  int* err;      // bit 0: the leader's wait for `enter` gave up
+  unsigned spin_max;
 };
 
 __device__ __forceinline__ float rescan_sc1(const float* x, int64_t n, LogitRun* run, double* dbuf, float* fbuf) {
@@ -570,7 +582,7 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   __shared__ float s_chunk[SM_CHUNK];
   __shared__ float sbuf[META_THREADS / 64];
   __shared__ double dbuf[META_THREADS / 64];
-  __shared__ int s_act, s_far, s_reseed, s_last;
+  __shared__ int s_act, s_far, s_reseed, s_last, s_mine;
   const int k = blockIdx.x, t = threadIdx.x;
   const bool own = t < a.M;
   const int i0 = own ? t : 0;
@@ -611,13 +623,35 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   if (t == 0) {
     s_act = 0;
     s_far = 0;
+    s_mine = 0;
   }
   __syncthreads();
   const bool mine = own && pos0 / SM_CHUNK == k;
-  if (mine) s_act = 1;
+  if (mine) {
+    s_act = 1;
+    atomicAdd(&s_mine, 1);  // LDS
+  }
   __syncthreads();
   const bool leader = k == posl / SM_CHUNK;
   if (!s_act) return;  // (the leader's chunk holds pos[0])
+  // entry loads returned in every wave, then this block's entries arrive
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_fetch_add(ck.enter, s_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (leader) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(ck.enter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.M) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > ck.spin_max) {
+          __hip_atomic_fetch_or(ck.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      // every active block has arrived (or the wait gave up): reset for the next launch
+      __hip_atomic_store(ck.enter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 #pragma unroll
   for (int q = 0; q < SM_PER_LANE / 4; ++q) *reinterpret_cast<float4*>(s_chunk + t * SM_PER_LANE + 4 * q) = cv[q];
   const float s0 = meta_s_row(dr);

@@ -118,6 +118,11 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
       self._upload = store_lib.Uploader(8 * max(self._meta_batch_size, self._batch_size))
     return self._upload
 
+  def _health_word(self) -> int:
+    # the learner's word and the meta-update's (its two learners' hand-offs,
+    # the HVP's ddot1 wait and the fused Adam's entry wait)
+    return super()._health_word() | self._meta.sync_status()
+
   @property
   def meta_learner(self) -> learner_lib.MetaLearner:
     return self._meta

@@ -421,6 +421,21 @@ class MetaLearner:
         _native.stream_handle(stream)))
     return self.probs, self.dlogits, self.td, self.loss
 
+  def sync_status(self):
+    """0 if every bounded wait of the meta-update completed and every loss
+    was finite since the previous check (dqz_meta_sync_status: the batch
+    and one-transition learners' health words and the meta handle's own;
+    synchronises; a non-zero word also clears every hand-off word)."""
+    st = ctypes.c_int(0)
+    _native.check(_native.lib().dqz_meta_sync_status(self._h, ctypes.byref(st)))
+    return st.value
+
+  def debug_stall(self, poison=True, spin_max=0):
+    """Test hook (dqz_meta_debug_stall): cap every bounded wait of the
+    meta handle at `spin_max` polls (0 restores the default) and, with
+    `poison`, make the next update's HVP ddot1 and Adam entry waits run out."""
+    _native.check(_native.lib().dqz_meta_debug_stall(self._h, int(bool(poison)), int(spin_max)))
+
   def get_state(self):
     """optax.adam's state, (ScaleByAdamState(count, mu, nu), EmptyState()),
     with host arrays (dqn_mgsc_batched/agent.py:80,390)."""

@@ -494,6 +494,25 @@ int dqz_meta_update(dqz_meta* meta, const dqz_params* params, const dqz_store* s
 int dqz_meta_outputs(dqz_meta* meta, float* probs, float* dlogits, float* td, float* loss,
                      void* stream);
 
+/* Health word of the meta-update since the previous check (the meta-level
+ * counterpart of dqz_learner_sync_status): the OR of the batch learner's
+ * and the one-transition learner's words (bit 0: an in-launch hand-off wait
+ * gave up, among them the HVP's ddot1 wait; bit 1: a non-finite loss) and of
+ * the meta-update's own word (bit 0: the fused Adam leader's wait for the
+ * other chunk blocks gave up).  Synchronises the device.  A non-zero status
+ * clears every hand-off word of the meta handle (both learners' and its own
+ * arrival counters) and the status; callers treat the meta-updates since
+ * their previous check as invalid. */
+int dqz_meta_sync_status(dqz_meta* meta, int* status);
+
+/* Diagnostic (tests): from the next meta-update on, every bounded wait of the
+ * meta handle gives up after `spin_max` polls (0 restores 2^24); poison != 0
+ * sets the HVP's ddot1 arrival counter far below its arrivals (second order)
+ * and the Adam entry counter far below M, so the next update's waits on them
+ * run out — the timeout path of dqz_meta_sync_status, exercised.
+ * Synchronises the device. */
+int dqz_meta_debug_stall(dqz_meta* meta, int poison, unsigned spin_max);
+
 /* ---- Atari observation preprocessing (processors.py:421-505) -----------
  * The observation branch of processors.atari on device: element-wise max of
  * the last n RGB frames (np.max over the pooled frames), rgb2y

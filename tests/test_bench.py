@@ -147,3 +147,69 @@ def test_world_mismatch_fails():
                   '--selftest-cpu'], env={'WORLD_SIZE': '1'}, timeout=120)
   assert p.returncode != 0
   assert 'WORLD_SIZE=1' in p.stderr
+
+
+def _json_line(p):
+  lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+  assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+  return json.loads(lines[0])
+
+
+def test_gpus8_spawns_eight_ranks_gloo():
+  """World-8 readiness (config 5: 8 independent seeds, one per GPU,
+  run_dqn_normal.sh:5,47): bench.py starts 8 ranks itself, every rank times
+  exactly K steps, the line carries 8 distinct device identities and 8
+  per-rank rates, and value = world x K / max-over-ranks time."""
+  p = _run_bench(['--gpus', '8', '--steps', '20', '--warmup', '5',
+                  '--stats-every', '8', '--target-period', '10',
+                  '--graph-steps', '6', '--selftest-cpu'], timeout=400)
+  assert p.returncode == 0, p.stderr[-3000:]
+  out = _json_line(p)
+  assert out['n_gpus'] == 8 and out['rccl']['world'] == 8
+  assert out['per_rank_steps'] == [20] * 8
+  assert out['per_rank_target_syncs'] == [2] * 8
+  assert out['per_rank_stats_gathers'] == [3] * 8
+  assert out['rccl']['last_in_loop_gather']['steps_done'] == [25] * 8
+  assert len(out['per_rank_steps_per_s']) == 8
+  assert all(v > 0 for v in out['per_rank_steps_per_s'])
+  assert out['per_gpu_min_steps_per_s'] == min(out['per_rank_steps_per_s'])
+  ids = [d['pci'] for d in out['devices']]
+  assert ids == ['stand-in-%d' % r for r in range(8)] and len(set(ids)) == 8
+  # value is the whole-job aggregate over the slowest rank's time
+  assert abs(out['value'] - 8 * 20 / (out['ms_per_step'] * 20 / 1e3)) < 1e-6 * out['value'] + 0.02
+
+
+def test_gpus8_two_ranks_on_one_device_fail():
+  """check_devices' failure path at world 8: rank 5 reporting rank 2's
+  device makes the line invalid (exit 4, no JSON line)."""
+  p = _run_bench(['--gpus', '8', '--steps', '4', '--warmup', '0',
+                  '--selftest-cpu'], env={'DQZ_SELFTEST_DEVICE': '5=stand-in-2'},
+                 timeout=400)
+  assert p.returncode == 4, p.stderr[-3000:]
+  assert 'ranks 2 and 5 report the same device' in p.stderr
+  assert not [l for l in p.stdout.splitlines() if l.startswith('{')]
+
+
+def test_gpus8_under_torch_distributed_run():
+  """The driver's own launch: python -m torch.distributed.run
+  --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 (env://
+  rendezvous, WORLD_SIZE set by the launcher, no ranks spawned here)."""
+  import socket  # pylint: disable=g-import-not-at-top
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  e = dict(os.environ)
+  for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+    e.pop(k, None)
+  e['OMP_NUM_THREADS'] = '1'
+  p = subprocess.run(
+      [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+       '--nproc-per-node', '8', '--master-addr', '127.0.0.1', '--master-port',
+       str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '8', '--steps', '12',
+       '--warmup', '2', '--graph-steps', '5', '--selftest-cpu'],
+      capture_output=True, text=True, timeout=400, env=e, cwd=ROOT)
+  assert p.returncode == 0, p.stderr[-3000:]
+  out = _json_line(p)
+  assert out['n_gpus'] == 8 and out['per_rank_steps'] == [12] * 8
+  assert len({d['pci'] for d in out['devices']}) == 8
+  assert len(out['per_rank_steps_per_s']) == 8

@@ -267,3 +267,110 @@ def test_meta_update_keeps_logit_buffer_state(device, meta_lr):
                                 helpers.canonical_chunk_sums(t_dev.cpu().numpy()))
   # and the buffer samples from the new state (no re-seed needed first)
   assert dev.sample_abs(rng.random(32)).cpu().numpy().max() < cap_logits
+
+
+def _meta_setup(device, m, second_order=False, a=6, seed=80):
+  from dqn_mgsc_zoo_amd import learner as learner_lib
+  from dqn_mgsc_zoo_amd import networks
+  from dqn_mgsc_zoo_amd import replay as replay_lib
+  net = networks.dqn_atari_network(a)
+  online = net.init(seed)
+  target = helpers.perturbed_tree(online, seed + 1)
+  mu, nu = _rand_opt_state(online, seed + 2)
+  lrn = learner_lib.Learner(net, 32, algo='dqn')
+  lrn.set_params(online, target)
+  lrn.set_opt_state(mu, nu)
+  meta = learner_lib.MetaLearner(lrn, m, learner_lib.adam(2.5e-4),
+                                 second_order=second_order)
+  rng = np.random.default_rng(seed + 3)
+  st, host = _store(256, 640, a, seed + 4, device)
+  slots = rng.choice(256, m, replace=False).astype(np.int32)
+  ot_tm1 = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot_t = rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)
+  ot = replay_lib.Transition(ot_tm1, 1, 1.0, 0.99, ot_t)
+  meta.set_online_transition(ot)
+  mb = dict(s_tm1=helpers.stacks_from(host['frames'], host['fidx'], slots, 0),
+            a_tm1=host['action'][slots], r_t=host['reward'][slots],
+            discount_t=host['discount'][slots],
+            s_t=helpers.stacks_from(host['frames'], host['fidx'], slots, 1))
+  trans = dict(s_tm1=ot_tm1, a_tm1=1, r_t=1.0, discount_t=0.99, s_t=ot_t)
+  ref_args = (_f64(online), _f64(target), _f64(mu), _f64(nu), mb)
+  return meta, st, slots, rng, ref_args, trans
+
+
+def test_meta_adam_chunks_with_more_blocks_than_the_chip_holds(device):
+  """the fused Adam's leader stores m, v, count and the
+  running state that every active chunk block reads at entry.  With 2^26
+  logits the launch has 16,384 chunk blocks, far more than are resident at
+  once, the leader's chunk (pos[0]) comes first and the other active chunks
+  are among the last blocks dispatched: every written logit must still be
+  the oracle's single Adam step, the count must advance once and the running
+  log-sum-exp must equal a fresh scan."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  m, cap_logits = 100, 1 << 26
+  meta, st, slots, rng, ref_args, trans = _meta_setup(device, m, seed=90)
+  logits = rng.standard_normal(cap_logits).astype(np.float32)
+  nchunks = cap_logits // 4096
+  pos = np.concatenate([
+      [5], rng.choice(np.arange((nchunks - 40) * 4096, cap_logits), m - 1,
+                      replace=False)]).astype(np.int32)
+  am = (1e-3 * rng.standard_normal(m)).astype(np.float32)
+  av = (1e-6 * rng.random(m)).astype(np.float32)
+  meta.set_state({'count': 4, 'mu': am, 'nu': av})
+  ref = learner_ref.meta_update(*ref_args, logits[pos], trans, am, av, 4)
+  dev = rc._DeviceLogits(cap_logits, device, max_queries=32)  # pylint: disable=protected-access
+  dev.load(logits)
+  dev.sample_abs(rng.random(32))  # a draw re-seeds: the running state is known
+  assert dev.run_state()['known'] == 1
+  meta.update(st, torch.from_numpy(slots).to(device), dev.logits,
+              torch.from_numpy(pos).to(device), logit_buffer=dev)
+  assert meta.sync_status() == 0
+  after = dev.logits[torch.from_numpy(pos.astype(np.int64)).to(device)].cpu().numpy()
+  np.testing.assert_allclose(after, ref['new_logits'], atol=1e-6)
+  state = meta.get_state()[0]
+  assert state.count == 5
+  np.testing.assert_allclose(state.mu, ref['adam_m'], atol=1e-5 * np.abs(ref['adam_m']).max())
+  run = dev.run_state()
+  assert run['valid'] == 1 and run['known'] == 1
+  full = dev.logits.cpu().numpy().astype(np.float64)
+  mx = full.max()
+  want_lse = mx + np.log(np.exp(full - mx).sum())
+  assert abs(run['c'] + np.log(run['S']) - want_lse) < 1e-9 * max(1.0, abs(want_lse))
+
+
+def test_meta_sync_status_reports_and_clears_a_stalled_wait(device):
+  """the second-order meta-update's in-launch waits
+  (the HVP's ddot1 hand-off, the fused Adam's entry wait) report a timeout
+  through dqz_meta_sync_status, which also clears the words, so the next
+  meta-update is correct again."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  m, cap_logits = 8, 20_000
+  meta, st, slots, rng, ref_args, trans = _meta_setup(device, m, second_order=True, seed=100)
+  logits = rng.standard_normal(cap_logits).astype(np.float32)
+  pos = rng.choice(cap_logits, m, replace=False).astype(np.int32)
+  ref = learner_ref.meta_update(*ref_args, logits[pos], trans, np.zeros(m), np.zeros(m), 0,
+                                stop_gradient=False)
+  dev = rc._DeviceLogits(cap_logits, device, max_queries=32)  # pylint: disable=protected-access
+  slots_d = torch.from_numpy(slots).to(device)
+  pos_d = torch.from_numpy(pos).to(device)
+
+  def fresh_run():
+    dev.load(logits)
+    dev.sample_abs(rng.random(32))
+    meta.set_state({'count': 0, 'mu': np.zeros(m, np.float32), 'nu': np.zeros(m, np.float32)})
+    meta.update(st, slots_d, dev.logits, pos_d, logit_buffer=dev)
+
+  fresh_run()
+  assert meta.sync_status() == 0
+  meta.debug_stall(poison=True, spin_max=2000)
+  fresh_run()
+  assert meta.sync_status() & 1  # reported ...
+  assert meta.sync_status() == 0  # ... and cleared by the read
+  meta.debug_stall(poison=False, spin_max=0)
+  fresh_run()
+  assert meta.sync_status() == 0
+  _, dlogits, _, loss = [t.cpu().numpy() for t in meta.fetch_outputs()]
+  np.testing.assert_allclose(loss[0], ref['loss'], rtol=2e-5)
+  np.testing.assert_allclose(dlogits, ref['dlogits'], atol=2e-5 * np.abs(ref['dlogits']).max())
+  after = dev.logits.cpu().numpy()
+  np.testing.assert_allclose(after[pos], ref['new_logits'], atol=1e-6)
