@@ -814,6 +814,7 @@ __global__ __launch_bounds__(512) void head_dx1_kernel(HeadArgs h, Fc1BwdArgs a)
   DQZ_STAMP(5, 3);
 }
 
+#ifdef DQZ_STEP_TU
 // head_dx1_kernel's launch: the head_kernel template choice (launch_head)
 inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStream_t st) {
   if (h.S > 7 || h.Z < 1 || h.Z > 3 || h.B != 1) return hipErrorInvalidValue;
@@ -831,8 +832,9 @@ inline hipError_t launch_head_dx1(const HeadArgs& h, const Fc1BwdArgs& f, hipStr
   }
   return hipGetLastError();
 }
+#endif  // DQZ_STEP_TU
 
-__global__ __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
+DQZ_STEP_KERNEL __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[FC1X_SMEM];
   fc1_dx_block(a, smem, blockIdx.x);
 }

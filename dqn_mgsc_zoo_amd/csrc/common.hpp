@@ -20,7 +20,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------------------
-// errors (thread-local message behind dqz_last_error)
+// Two translation units, two code objects.  learner_step.hip (DQZ_STEP_TU
+// defined) holds the learner step's kernels and their launchers; learner.hip
+// holds every other kernel (samplers, logit buffers, the MGSC meta-update and
+// HVP, preprocessing).  Each TU is compiled to its own code object, so the
+// learner step's code is laid out by its own sources alone: no edit to another
+// kernel can move it ("Code layout").  A kernel defined in a
+// header both TUs include is a plain kernel in the TU it belongs to and an
+// uninstantiated template (never emitted) in the other.
+#ifdef DQZ_STEP_TU
+#define DQZ_STEP_KERNEL __global__
+#define DQZ_OTHER_KERNEL template <int = 0> __global__
+#else
+#define DQZ_STEP_KERNEL template <int = 0> __global__
+#define DQZ_OTHER_KERNEL __global__
+#endif
+
+// ---------------------------------------------------------------------------
+// errors (thread-local message behind dqz_last_error; one instance for both
+// translation units: an inline function's static)
 
 inline std::string& err_buf() {
   static thread_local std::string s;
@@ -186,7 +204,7 @@ struct Rms {
 // tools/trace_step.py reads them back with dqz_debug_trace().
 #ifdef DQZ_TRACE
 constexpr int TRACE_KERNELS = 20, TRACE_BLOCKS = 4096, TRACE_SLOTS = 4;
-__device__ unsigned long long g_dqz_trace[TRACE_KERNELS * TRACE_BLOCKS * TRACE_SLOTS];
+static __device__ unsigned long long g_dqz_trace[TRACE_KERNELS * TRACE_BLOCKS * TRACE_SLOTS];
 #define DQZ_STAMP(kid, slot)                                                                              \
   do {                                                                                                    \
     if (threadIdx.x == 0) {                                                                               \

@@ -668,14 +668,14 @@ __device__ __forceinline__ void fc1_gemv_block(const Fc1FwdArgs& a, float* smem,
   }
 }
 
-__global__ __launch_bounds__(256) void fc1_gemv_kernel(Fc1FwdArgs a) {
+DQZ_STEP_KERNEL __launch_bounds__(256) void fc1_gemv_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ __attribute__((aligned(16))) float smem[FC1_GEMV_SMEM];
   fc1_gemv_block(a, smem, blockIdx.x);
   DQZ_STAMP(3, 3);
 }
 
-__global__ __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
+DQZ_STEP_KERNEL __launch_bounds__(256) void fc1_fwd32_kernel(Fc1FwdArgs a) {
   DQZ_STAMP(3, 0);
   __shared__ float s_red[4 * FC1_32RW];
   fc1_fwd_block32<false>(a, s_red, blockIdx.x);

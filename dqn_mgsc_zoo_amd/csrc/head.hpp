@@ -377,6 +377,7 @@ __global__ __launch_bounds__(512) void head_kernel(HeadArgs h) {
   head_body<AMAX, SMAX, ZMAX>(h, blockIdx.x);
 }
 
+#ifdef DQZ_STEP_TU  // (the launchers instantiate the step's kernels: its TU only)
 // Head launch: AMAX 8 covers Pong-style minimal action sets, 32 the rest.
 template <int SMAX, int ZMAX>
 inline void launch_head_z(const HeadArgs& h, int grid, hipStream_t st) {
@@ -395,6 +396,7 @@ inline hipError_t launch_head(const HeadArgs& h, int grid, hipStream_t st) {
   }
   return hipGetLastError();
 }
+#endif  // DQZ_STEP_TU
 
 struct UpdArgs {
   float *th, *mu, *nu;
@@ -703,12 +705,12 @@ inline unsigned update_blocks(const int64_t sz[10], int A, int nb2) {
   return (unsigned)((nsmall + UPD_PARAMS - 1) / UPD_PARAMS + (nconv + UPD_PARAMS - 1) / UPD_PARAMS);
 }
 
-__global__ __launch_bounds__(256) void update_kernel(UpdArgs u) {
+DQZ_STEP_KERNEL __launch_bounds__(256) void update_kernel(UpdArgs u) {
   __shared__ float2 s_part[UPD_GROUPS][UPD_PAIRS];
   update_body(u, s_part, blockIdx.x);
 }
 
-__global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
+DQZ_OTHER_KERNEL void sample_uniform_kernel(int64_t base, int64_t size, int64_t capacity, int n, uint64_t seed,
                                       uint64_t* counter, int32_t* out) {
   DQZ_STAMP(10, 0);
   const uint64_t ctr = *counter;
@@ -719,7 +721,7 @@ __global__ void sample_uniform_kernel(int64_t base, int64_t size, int64_t capaci
   DQZ_STAMP(10, 3);
 }
 
-__global__ void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx, const int32_t* slots, int n,
+DQZ_OTHER_KERNEL void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx, const int32_t* slots, int n,
                                      int which, uint8_t* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)n * FB) return;
@@ -737,7 +739,7 @@ __global__ void gather_stacks_kernel(const uint8_t* frames, const int32_t* fidx,
 // One replay add (dqz_store_put): block i < t.num_frames copies new frame i
 // (441 x 16 B) into its pool row; block 0 also writes the transition record.
 // `frames` may be pinned host memory (read over the fabric).
-__global__ __launch_bounds__(256) void store_put_kernel(uint8_t* pool, int32_t* fidx, int32_t* action, float* reward,
+DQZ_OTHER_KERNEL __launch_bounds__(256) void store_put_kernel(uint8_t* pool, int32_t* fidx, int32_t* action, float* reward,
                                                         float* discount, dqz_transition_put t,
                                                         const uint8_t* frames) {
   constexpr int Q = FB / 16;  // 441

@@ -42,10 +42,6 @@
 #ifndef DQZ_EXP_HVP_SKIP
 #define DQZ_EXP_HVP_SKIP 0
 #endif
-// hvp_l3_kernel's code-layout filler, in 4-byte words ("Code layout")
-#ifndef DQZ_LAYOUT_PAD
-#define DQZ_LAYOUT_PAD 476
-#endif
 
 
 namespace dqz {
@@ -744,12 +740,6 @@ __global__ __launch_bounds__(256) void hvp_l3_kernel(HvpArgs a) {
   __shared__ float s_x[C1M];
   constexpr int GH = HVP_B1, G2 = GH + HVP_G_H, G3 = G2 + HVP_G_C2, G1 = G3 + HVP_G_C3, GF = G1 + HVP_G_C1;
   const int i = blockIdx.x;
-  // Code-layout pin ("Code layout"): DQZ_LAYOUT_PAD never-executed
-  // s_nop words (A >= 1), so the learner's template kernels, which the compiler
-  // emits after every non-template kernel, keep the addresses they were
-  // measured fastest at (the HVP rework had moved them by 2.3 KB and the
-  // graph-replayed learner step lost 1.8 % with identical learner ISA, s40).
-  if (a.A < 0) asm volatile(".fill " DQZ_XSTR(DQZ_LAYOUT_PAD) ", 4, 0xbf800000");
   DQZ_STAMP(18, 0);
   if (i < GH) {
     hvp_b1_block(a, i, reinterpret_cast<float(*)[9]>(&s_r[0][0]));

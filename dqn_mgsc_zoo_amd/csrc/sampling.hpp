@@ -65,7 +65,7 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sbuf) {
 // (float4 loads), takes their max, then sums exp(x - max): one expf per logit.
 // clear_pos (>= 0): that slot is set to -inf first (the reservoir replace)
 // by the block that owns it, which is the only block that reads it.
-__global__ __launch_bounds__(SM_THREADS) void lse_partial_kernel(float* __restrict__ x, int64_t n,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void lse_partial_kernel(float* __restrict__ x, int64_t n,
                                                                  MaxSum* __restrict__ part, int64_t clear_pos) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
   const int64_t base = (int64_t)blockIdx.x * SM_CHUNK;
@@ -147,7 +147,7 @@ __device__ __forceinline__ float logmeanexp_item(float lse, int64_t size) {
 // Pass 2 (one block): lse = m + log(s); optional logit write of a new item:
 // logits[write_pos] = size == 0 ? 0 : lse - log(size) (log-mean-exp); seeds
 // the running state `run` (may be null) from the scan.
-__global__ __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __restrict__ part, int nparts,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void lse_final_kernel(const MaxSum* __restrict__ part, int nparts,
                                                                float* lse_out, float* logits, int64_t write_pos,
                                                                int64_t size, LogitRun* run) {
   __shared__ MaxSum sbuf[SM_THREADS / 64];
@@ -255,7 +255,7 @@ __device__ __forceinline__ double chunk_sum(const float* __restrict__ x, int64_t
 
 // One block per chunk: csum[k] = chunk_sum(k) about the running state's c;
 // with `dirty`, only the chunks flagged by a writer (flags cleared).
-__global__ __launch_bounds__(SM_THREADS) void chunk_sums_kernel(const float* __restrict__ x, int64_t n,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void chunk_sums_kernel(const float* __restrict__ x, int64_t n,
                                                                 const LogitRun* run, double* __restrict__ csum,
                                                                 int* __restrict__ dirty) {
   __shared__ double s_wave[SM_THREADS / 64];
@@ -310,7 +310,7 @@ __device__ __forceinline__ bool run_ok(double s_before, double s_after, float x,
 // add / reservoir replace with the running state (one block), then the chunk
 // sums of the (at most two) chunks it wrote.  A tripped guard re-seeds the
 // state and every chunk sum in this block (rare).
-__global__ __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* __restrict__ x, int64_t n,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* __restrict__ x, int64_t n,
                                                                         LogitRun* run, double* __restrict__ csum,
                                                                         int64_t clear_pos, int64_t write_pos,
                                                                         int64_t size, float* lse_out) {
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(SM_THREADS) void logits_add_running_kernel(float* _
 
 // One write x[pos] = v passed by value (popleft's -inf), keeping the running
 // state and the chunk sum (one block).
-__global__ __launch_bounds__(SM_THREADS) void logits_put1_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void logits_put1_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
                                                                  double* __restrict__ csum, int64_t pos, float v) {
   __shared__ int s_valid;
   __shared__ float s_c;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(SM_THREADS) void logits_put1_kernel(float* __restri
 // value, as numpy fancy assignment does), keeping the running state; the
 // written chunks are flagged for chunk_sums_kernel (all of them after a
 // re-seed).
-__global__ __launch_bounds__(SM_THREADS) void logits_write_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void logits_write_kernel(float* __restrict__ x, int64_t n, LogitRun* run,
                                                                   int* __restrict__ dirty,
                                                                   const int64_t* __restrict__ pos,
                                                                   const float* __restrict__ val, int m) {
@@ -438,13 +438,13 @@ __global__ __launch_bounds__(SM_THREADS) void logits_write_kernel(float* __restr
 
 // Plain writes while the host cannot vouch for the running state (the next
 // use re-seeds it and every chunk sum).
-__global__ void logits_scatter_kernel(float* __restrict__ x, const int64_t* __restrict__ pos,
+DQZ_OTHER_KERNEL void logits_scatter_kernel(float* __restrict__ x, const int64_t* __restrict__ pos,
                                       const float* __restrict__ val, int m) {
   if (threadIdx.x == 0)
     for (int i = 0; i < m; ++i) x[pos[i]] = val[i];  // in order: a repeated slot keeps its last value
 }
 
-__global__ void logits_scatter1_kernel(float* __restrict__ x, int64_t pos, float v) {
+DQZ_OTHER_KERNEL void logits_scatter1_kernel(float* __restrict__ x, int64_t pos, float v) {
   if (threadIdx.x == 0) x[pos] = v;
 }
 
@@ -457,7 +457,7 @@ __device__ __forceinline__ double philox_uniform(uint64_t seed, uint64_t ctr, in
 }
 
 // Uniform doubles in [0, 1) from Philox, counter advanced on device.
-__global__ void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, double* out) {
+DQZ_OTHER_KERNEL void philox_uniform_kernel(uint64_t seed, uint64_t* counter, int n, double* out) {
   const uint64_t ctr = *counter;
   for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = philox_uniform(seed, ctr, i);
   __syncthreads();
@@ -624,7 +624,7 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
 // Diagnostics (dqz_logits_probs / dqz_logits_terms), one block per chunk:
 // p = t / total as f32 (the draw's distribution), the terms t themselves, the
 // running lse and c.
-__global__ __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __restrict__ x, int64_t n,
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void logit_terms_kernel(const float* __restrict__ x, int64_t n,
                                                                  const LogitRun* run, const double* __restrict__ csum,
                                                                  int nblocks, float* __restrict__ p_out,
                                                                  float* __restrict__ t_out, float* lse_out,
@@ -688,7 +688,7 @@ struct SampleSync {
   int* words;
 };
 
-__global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
     const float* __restrict__ x, int64_t n, const LogitRun* run, const double* __restrict__ csum, int nblocks,
     SampleSync sync, uint64_t seed, uint64_t* counter, const double* __restrict__ uniforms, int nq,
     int32_t* __restrict__ out_slots, int64_t* __restrict__ out_idx) {
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
 
 // Single workgroup: write n leaves, then recompute their ancestors level by
 // level (duplicate parents write identical values).
-__global__ __launch_bounds__(1024) void sumtree_set_kernel(double* tree, int64_t cap, int levels,
+DQZ_OTHER_KERNEL __launch_bounds__(1024) void sumtree_set_kernel(double* tree, int64_t cap, int levels,
                                                            const int64_t* idx, const double* vals, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     __hip_atomic_store(&tree[cap + idx[i]], vals[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -793,7 +793,7 @@ __device__ __forceinline__ void sumtree_set_small_body(double* tree, int levels,
   }
 }
 
-__global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree, int64_t cap, int levels,
+DQZ_OTHER_KERNEL __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree, int64_t cap, int levels,
                                                                     const int64_t* idx, const double* vals, int n) {
   const int i = threadIdx.x;
   sumtree_set_small_body(tree, levels, n, i < n ? cap + idx[i] : -1, i < n ? vals[i] : 0.0);
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(ST_FAST) void sumtree_set_small_kernel(double* tree
 // *max_seen = max(*max_seen, max p), leaf = p^alpha (0 -> 0), sum-tree
 // set.  A slot drawn twice keeps its last draw's value (numpy fancy
 // assignment order in SumTree.set).  n <= ST_FAST.
-__global__ __launch_bounds__(ST_FAST) void per_write_back_kernel(double* tree, int64_t cap, int levels,
+DQZ_OTHER_KERNEL __launch_bounds__(ST_FAST) void per_write_back_kernel(double* tree, int64_t cap, int levels,
                                                                  const int32_t* slots, const float* td, double alpha,
                                                                  int n, double* max_seen) {
   __shared__ double s_max[ST_FAST / 64];
@@ -975,7 +975,7 @@ __device__ __forceinline__ Descent halfwave_descend(const double* tree, int64_t 
 }
 
 // One half-wave per target; -1 when out of range.
-__global__ __launch_bounds__(256) void sumtree_query_kernel(const double* __restrict__ tree, int64_t cap,
+DQZ_OTHER_KERNEL __launch_bounds__(256) void sumtree_query_kernel(const double* __restrict__ tree, int64_t cap,
                                                             int levels, const double* __restrict__ targets, int n,
                                                             int64_t* __restrict__ out) {
   const int i = blockIdx.x * 8 + (threadIdx.x >> 5), l = threadIdx.x & 31;
@@ -1171,7 +1171,7 @@ __device__ __forceinline__ PerPick per_pick(const PerSampleArgs& a, int l, const
 // importance_sampling_weights (replay.py:344-376) of one draw, unnormalised.
 __device__ __forceinline__ double per_weight(double up, double prob, double beta) { return pow(up / prob, beta); }
 
-__global__ __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
+DQZ_OTHER_KERNEL __launch_bounds__(1024) void per_sample_kernel(PerSampleArgs a) {
   __shared__ double s_top[PS_TOP_NODES];  // node i at s_top[i], i in [1, 2^(dtop + 1))
   __shared__ double s_w[1024];
   const bool inj = a.inj_u != nullptr;
@@ -1249,7 +1249,7 @@ __device__ __forceinline__ void per_publish_weight(const PerSampleArgs& a, int b
 // tree index (or -1) gets 0, the new one (priority >= 0 ? priority :
 // *max_seen) ** alpha (0 -> 0, _power), ancestors rebuilt, and
 // index_to_slot[add] = slot.  One launch of ST_FAST threads, two live.
-__global__ __launch_bounds__(ST_FAST) void per_add_kernel(double* tree, int64_t cap, int levels, int32_t remove_idx,
+DQZ_OTHER_KERNEL __launch_bounds__(ST_FAST) void per_add_kernel(double* tree, int64_t cap, int levels, int32_t remove_idx,
                                                           int32_t add_idx, double priority, const double* max_seen,
                                                           double alpha, int32_t* index_to_slot, int32_t slot) {
   const int i = threadIdx.x;

@@ -17,9 +17,18 @@ device's state checks every one of the 50 updates, with realistic carried
 moments (nu - mu^2 small under the sqrt) and a target sync in the middle
 (dqn/agent.py:155-156), at the single-step bars:
 
-  q, td: atol 1e-4; loss rtol 1e-4;
-  update p_new - p_old, per leaf: relative Frobenius norm <= 1e-3;
-  mu, nu per leaf: relative Frobenius norm <= 1e-4.
+  q, td: atol 1e-4; loss rtol 1e-4 (every step);
+  update p_new - p_old, mu, nu, per leaf, relative Frobenius norm: the
+  median step <= 1e-4 (update) / 1e-5 (mu, nu), every step <= 1e-2 / 3e-3.
+
+The two-level bar is the discontinuity again: the batch is unfiltered, so a
+step can carry a kink flip (or, for double-Q, a near-tie of the online
+argmax at s_t that picks the other action's target) and then its gradient
+differs in whole units.  The independent f32 implementation from the same
+fp64 states on the same batches (round 6, CPU) shows exactly that: typical
+steps 2-5e-5 (update) and 1-6e-7 (mu, nu), worst double-Q step 4.8e-3 /
+1.3e-3 / 4.8e-4.  A step above 1e-4 prints its ReLU margin (oracle
+relu_margin) so the cause can be read off the log.
 
 PER also checks the sum tree after every priority write-back
 (prioritized/agent.py:187-206), MGSC the logits and the Adam moments after
@@ -39,8 +48,8 @@ pytestmark = pytest.mark.gpu
 
 STEPS = 50
 SYNC_AT = 25  # target <- online after this step's learn
-UPDATE_BAR = 1e-3  # single-step unfiltered measured <= 3.6e-5 (test_learner_gpu.py)
-MOMENT_BAR = 1e-4
+UPDATE_MEDIAN, MOMENT_MEDIAN = 1e-4, 1e-5
+UPDATE_BAR, MOMENT_BAR = 1e-2, 3e-3
 
 
 def _rel_err(got, want):
@@ -92,17 +101,26 @@ def _state(lrn):
 
 
 class _Worst:
-  """Largest error of each kind over the trajectory (printed at the end)."""
+  """Every step's error of each kind (median and worst checked and printed
+  at the end)."""
 
   def __init__(self):
     self.v = {}
 
   def add(self, k, x):
-    self.v[k] = max(self.v.get(k, 0.0), float(x))
+    self.v.setdefault(k, []).append(float(x))
+
+  def median(self, k):
+    return float(np.median(self.v[k]))
 
   def report(self, label):
-    print('%s, worst over %d steps: %s' % (
-        label, STEPS, ', '.join('%s %.2e' % kv for kv in sorted(self.v.items()))))
+    print('%s over %d steps (median / worst): %s' % (
+        label, STEPS, ', '.join('%s %.2e / %.2e' % (k, np.median(v), max(v))
+                                for k, v in sorted(self.v.items()))))
+    if 'update' in self.v:
+      assert self.median('update') <= UPDATE_MEDIAN, self.median('update')
+      assert self.median('mu') <= MOMENT_MEDIAN, self.median('mu')
+      assert self.median('nu') <= MOMENT_MEDIAN, self.median('nu')
 
 
 def _learn_and_check(lrn, st, host, slots, device, worst, algo='dqn', weights=None,
@@ -129,6 +147,9 @@ def _learn_and_check(lrn, st, host, slots, device, worst, algo='dqn', weights=No
   worst.add('update', ue)
   worst.add('mu', me)
   worst.add('nu', ne)
+  if max(ue, 10 * me, 10 * ne) > 1e-4:
+    print('  step with update %.2e mu %.2e nu %.2e: ReLU margin of its batch %.1e' % (
+        ue, me, ne, learner_ref.relu_margin(p, _batch(host, slots)[0])))
   assert ue <= UPDATE_BAR, ue
   assert me <= MOMENT_BAR, me
   assert ne <= MOMENT_BAR, ne
@@ -263,7 +284,8 @@ def test_fifty_step_mgsc_trajectory(device, second_order):
     ad1 = meta.get_state()[0]
     assert int(ad1.count) == mref['adam_count']
     sm = np.abs(mref['adam_m']).max()
-    np.testing.assert_allclose(ad1.mu, mref['adam_m'], atol=1e-5 * sm)
+    # (m carries every step's dlogits, each within 2e-5 of its max: test_meta_gpu)
+    np.testing.assert_allclose(ad1.mu, mref['adam_m'], atol=1e-4 * sm)
     worst.add('adam_m', np.abs(np.asarray(ad1.mu) - mref['adam_m']).max() / sm)
     run = dev.run_state()
     a64 = after.astype(np.float64)

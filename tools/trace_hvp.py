@@ -50,7 +50,7 @@ def main():
   meta = learner_lib.MetaLearner(lrn, M, learner_lib.adam(2.5e-4), second_order=True)
   meta.set_online_transition(ot)
   ms = torch.from_numpy(rng.choice(cap, M, replace=False).astype(np.int32)).to(dev)
-  fn = _native.lib().dqz_debug_trace
+  fn = _native.lib().dqz_debug_trace_other  # the HVP kernels' code object
   fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
   buf = np.zeros(K * NB * NS, np.uint64)
   for _ in range(3):
