@@ -870,6 +870,15 @@ DQZ_STEP_KERNEL __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // boundary saved (16,210 against 16,244 steps/s; first-order meta-update
 // 193 -> 201 us; profiles/r05/s13).  With a thousand update blocks polling
 // three shared words the launch ran 1.3x slower (s10-s12).  Removed.)
+// Wave issue priority (s_setprio): the conv3 / conv2 dX waves 3, the conv1
+// dW waves (the launch's tail, behind dy1) 2, every other dW wave the default
+// 0, so on a SIMD shared with dW waves the chain's instructions issue first
+// (round 6: +0.1 / +0.4 / +1.1 % in three interleaved A/B sessions; conv2 /
+// conv3 dW at 1 as well: +0.3 %; the forward's conv2 / conv3 consumers above
+// their producers: -0.8 %; profiles/r06/prio).
+// (Round 6, also measured and not kept: the fc1 RMSProp outputs and the conv
+// dW slabs as write-through sc1 stores, so the backward leaves 32 MB fewer
+// dirty lines for the boundary before the update: -0.8 %, r06/prio.)
 // (Round 5, also removed: the dX chain on XCDs 0..L-1 and the dW sets on the
 // other XCDs.  With L = 4 the chain ended 0.5 us sooner, but the dW side
 // became the tail (+2.8 us) and the boundary after the launch grew 2.8 ->
@@ -899,6 +908,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c3.B);
     if (!sj.valid) return;
+    __builtin_amdgcn_s_setprio(3);  // the dX chain first (see above)
     DQZ_STAMP(6, 0);
     conv3_bwd_dx<true>(c3, smem, sj.s, sj.job & 3, sj.job >> 2);
     DQZ_STAMP(6, 3);
@@ -914,6 +924,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   if (i < 8 * B8) {
     const SampleJob sj = xcd_sample_job_at(i, 8, c2.B);
     if (!sj.valid) return;
+    __builtin_amdgcn_s_setprio(3);  // the dX chain first (see above)
     DQZ_STAMP(7, 0);
     conv2_bwd_dx<true, true>(c2, smem, sj.s, (sj.job & 3) >> 1, sj.job & 1, sj.job >> 2);
     DQZ_STAMP(7, 3);
@@ -940,6 +951,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       c1.sync1.wait(sj.s);
       return;
     }
+    __builtin_amdgcn_s_setprio(2);  // the launch's tail next
     conv1_dw_half(c1, smem, sj.job >> 1, sj.job & 1, sj.s);
     return;
   }
