@@ -878,7 +878,9 @@ DQZ_STEP_KERNEL __launch_bounds__(256) void fc1_dx_kernel(Fc1BwdArgs a) {
 // their producers: -0.8 %; profiles/r06/prio).
 // (Round 6, also measured and not kept: the fc1 RMSProp outputs and the conv
 // dW slabs as write-through sc1 stores, so the backward leaves 32 MB fewer
-// dirty lines for the boundary before the update: -0.8 %, r06/prio.)
+// dirty lines for the boundary before the update: -0.8 %, r06/prio; the
+// XCD's dirty lines written back early instead, by an agent-scope release
+// fence in the last 8 / 32 fc1 dW blocks: -1.9 / -6.6 %, r06/wbl2.)
 // (Round 5, also removed: the dX chain on XCDs 0..L-1 and the dW sets on the
 // other XCDs.  With L = 4 the chain ended 0.5 us sooner, but the dW side
 // became the tail (+2.8 us) and the boundary after the launch grew 2.8 ->
