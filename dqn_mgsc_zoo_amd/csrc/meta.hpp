@@ -637,21 +637,7 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   // entry loads returned in every wave, then this block's entries arrive
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) {
-    __hip_atomic_fetch_add(ck.enter, s_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (leader) {
-      unsigned spins = 0;
-      while (__hip_atomic_load(ck.enter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.M) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > ck.spin_max) {
-          __hip_atomic_fetch_or(ck.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      // every active block has arrived (or the wait gave up): reset for the next launch
-      __hip_atomic_store(ck.enter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (t == 0) __hip_atomic_fetch_add(ck.enter, s_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int q = 0; q < SM_PER_LANE / 4; ++q) *reinterpret_cast<float4*>(s_chunk + t * SM_PER_LANE + 4 * q) = cv[q];
   const float s0 = meta_s_row(dr);
@@ -667,19 +653,41 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   const float c1 = 1.f - powf(a.b1, (float)cnt), c2 = 1.f - powf(a.b2, (float)cnt);
   double dS = 0.0;
   float nx = 0.f;
+  float g = 0.f, m = 0.f, v = 0.f;
   if (own) {  // meta_adam_body's arithmetic, in the same order
-    const float g = s0 - p0 * tot;
-    const float m = (1.f - a.b1) * g + a.b1 * m0;
-    const float v = (1.f - a.b2) * (g * g) + a.b2 * v0;
+    g = s0 - p0 * tot;
+    m = (1.f - a.b1) * g + a.b1 * m0;
+    v = (1.f - a.b2) * (g * g) + a.b2 * v0;
     const float mh = m / c1;
     const float vh = v / c2;
     nx = x0 + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
-    if (leader) {
+  }
+  if (leader) {
+    // the leader's first store of state another block reads at entry: every
+    // active block's entries have arrived (the wait sits after this block's
+    // own arithmetic, which overlaps it; the later stores of count and run
+    // come after this point too)
+    if (t == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(ck.enter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.M) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > ck.spin_max) {
+          __hip_atomic_fetch_or(ck.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      // every active block has arrived (or the wait gave up): reset for the next launch
+      __hip_atomic_store(ck.enter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (own) {
       a.m[t] = m;
       a.v[t] = v;
       a.dlogits[t] = g;
       a.s_out[t] = s0;
     }
+  }
+  if (own) {
     if (r.valid) {
       dS = run_term(nx, r.c) - run_term(x0, r.c);
       if (nx != -INFINITY && (double)nx - (double)r.c >= 80.0) s_far = 1;
