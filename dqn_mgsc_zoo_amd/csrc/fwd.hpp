@@ -550,6 +550,11 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 // 3's order; round 4's interleaved order made the kernel 0.2-0.3 us slower,
 // fc1 4.90-4.96 -> 4.69-4.75 us back to back and 16,171 -> 16,248 steps/s,
 // three interleaved rounds, profiles/r05/c2).
+// (Round 6: the same loads issued all before the first MFMA, held there by a
+// sched_barrier, W1 first or y3 first — the source order alone does not do
+// it, the compiler interleaves them with the MFMAs at ~10 in flight: fc1
+// 4.75 -> 5.35 / 5.45 us back to back, the step -0.8 / -0.5 %, the meta-update
+// +10 us; profiles/r06/fc1_order.)
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
 // (Round 5: 8 waves per block, 56 k each, measured 4.70 -> 4.86 us and
