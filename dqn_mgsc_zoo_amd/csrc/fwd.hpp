@@ -555,6 +555,12 @@ constexpr int FC1_32RW = 32 * 33;  // one wave's 32 x 32 tile, row stride 33
 // it, the compiler interleaves them with the MFMAs at ~10 in flight: fc1
 // 4.75 -> 5.35 / 5.45 us back to back, the step -0.8 / -0.5 %, the meta-update
 // +10 us; profiles/r06/fc1_order.)
+// And timing-only (numerics wrong): the same W1 bytes as 16-byte loads, 14
+// instead of 56 per lane: 4.72 -> 4.36 us, the step +1.6 % (part of it the
+// code-layout shift of the kernels after this one), with every load ahead of
+// the MFMAs 5.3 us; a correct form needs each lane's four k values of one
+// column regathered (LDS staging or cross-lane moves), not built
+// (profiles/r06/fc1_order).
 // DOT: the MGSC tangent launches' form (per-row dot products with dz1 instead
 // of partial stores); the learner's fc1_fwd32_kernel compiles without it.
 // (Round 5: 8 waves per block, 56 k each, measured 4.70 -> 4.86 us and
