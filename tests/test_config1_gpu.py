@@ -35,7 +35,7 @@ def _params_host(tree):
           for m, d in tree.items()}
 
 
-def _make(seed=1):
+def _make(seed=1, min_replay_fraction=1e-4, target_period=TARGET_PERIOD, eps_decay=20_000):
   from dqn_mgsc_zoo_amd import learner as learner_lib
   from dqn_mgsc_zoo_amd import networks
   from dqn_mgsc_zoo_amd import parts
@@ -54,9 +54,9 @@ def _make(seed=1):
       transition_accumulator=replay_lib.TransitionAccumulator(),
       replay=replay, batch_size=32,
       exploration_epsilon=parts.LinearSchedule(
-          begin_t=0, decay_steps=20_000, begin_value=1.0, end_value=0.1),
-      min_replay_capacity_fraction=1e-4, learn_period=LEARN_PERIOD,
-      target_network_update_period=TARGET_PERIOD, grad_error_bound=BOUND,
+          begin_t=0, decay_steps=eps_decay, begin_value=1.0, end_value=0.1),
+      min_replay_capacity_fraction=min_replay_fraction, learn_period=LEARN_PERIOD,
+      target_network_update_period=target_period, grad_error_bound=BOUND,
       rng_key=np.array([0, seed], np.uint32))
   return agent, replay
 
@@ -134,3 +134,57 @@ def test_config1_dqn_agent_1m_replay_run_loop(device):
   st = agent._store()  # pylint: disable=protected-access
   np.testing.assert_array_equal(st.gather_stacks(slots, 0).cpu().numpy(), s_tm1)
   np.testing.assert_array_equal(st.gather_stacks(slots, 1).cpu().numpy(), s_t)
+
+
+def test_config1_at_the_reference_schedule(device):
+  """Config 1 at dqn/run_atari.py's own schedule:
+  min_replay_capacity_fraction 0.05 of the 1M replay (learning starts once
+  50,000 transitions are in, dqn/agent.py:149-150), learn period 16, target
+  period 40,000 frames (dqn/run_atari.py:77-79; the copy only once learning
+  runs, dqn/agent.py:155-156), epsilon 1 -> 0.1 over 4M frames from the
+  start of learning.  processors.atari repeats each action 4 times
+  (processors.py), so 50,000 transitions take ~200,000 frames: 241,000
+  frames through parts.run_loop, no learn step before the replay holds
+  50,000 transitions, then one every 16 frames, a target copy at every
+  multiple of 40,000 frames once learning runs (240,000 among them), each
+  equal to the online parameters of its frame, the replay's invariants, a
+  finite loss and a clean health word."""
+  from dqn_mgsc_zoo_amd import parts
+  from dqn_mgsc_zoo_amd import synthetic
+  min_frac, period = 0.05, 40_000
+  agent, replay = _make(seed=7, min_replay_fraction=min_frac, target_period=period,
+                        eps_decay=4_000_000)
+  lrn = agent.learner
+  learns, syncs, sizes = [], [], []
+  orig_learn, orig_sync = agent._learn, lrn.sync_target  # pylint: disable=protected-access
+
+  def learn():
+    learns.append(agent._frame_t)  # pylint: disable=protected-access
+    sizes.append(replay.size)
+    orig_learn()
+
+  def sync(stream=None):
+    orig_sync(stream)
+    syncs.append((agent._frame_t, torch.equal(lrn.target, lrn.online)))  # pylint: disable=protected-access
+
+  agent._learn = learn  # pylint: disable=protected-access
+  lrn.sync_target = sync
+  env = synthetic.SyntheticAtari(episode_len=27_000, seed=8)
+  loop = parts.run_loop(agent, env, max_steps_per_episode=108_000)
+  for _ in range(241_000):
+    next(loop)
+  torch.cuda.synchronize()
+  need = int(min_frac * CAPACITY)
+  assert learns and min(sizes) >= need
+  assert all(f % LEARN_PERIOD == 0 for f in learns)
+  # one learn per 16 frames from the first frame the replay was full enough
+  assert learns == list(range(learns[0], learns[-1] + 1, LEARN_PERIOD))
+  assert len(learns) > 2_000
+  assert 240_000 in [f for f, _ in syncs]
+  assert all(f % period == 0 and f >= learns[0] and eq for f, eq in syncs)
+  ok, msg = replay.check_valid()
+  assert ok, msg
+  _, _, loss = lrn.fetch_outputs()
+  assert np.isfinite(float(loss.item()))
+  assert torch.isfinite(lrn.online).all()
+  assert agent.check_learner_health() == 0
