@@ -239,6 +239,30 @@ __device__ __forceinline__ float wave_sum(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
+// The same fold on a double (each 32-bit half moved by the same DPP
+// control), left in lane 63 without the broadcast.  Lane 63's additions are
+// exactly those a Hillis-Steele inclusive scan performs there (step o adds
+// the value lane 63 - o held before the step; the lanes a row_shr leaves
+// unread are never on lane 63's path), so the result has the bits of that
+// scan's last lane.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, ROW_MASK, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double wave_fold63_f64(double v) {
+  v += dpp_d<0x111>(v);
+  v += dpp_d<0x112>(v);
+  v += dpp_d<0x114>(v);
+  v += dpp_d<0x118>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  return v;
+}
+
 // Sum of a 256-thread block's values v (wave sums in a fixed order),
 // deterministic, result in every thread.  s: 4 floats of LDS.
 __device__ __forceinline__ float block_sum256(float v, float* s) {

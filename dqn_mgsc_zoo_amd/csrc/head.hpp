@@ -73,16 +73,10 @@ __device__ __forceinline__ dqz_action eps_greedy(const float* q, int A, double e
 }
 
 // Maximum of a wave's non-negative doubles (the PER importance weights), in
-// every lane: the DPP row scan of wave_sum with max (lanes whose DPP source is
-// outside the row read 0, the identity here), then readlane 63.  Max is exact
-// in any order, so the result equals a shuffle butterfly's bit for bit.
-template <int CTRL, int ROW_MASK = 0xf>
-__device__ __forceinline__ double dpp_d(double v) {
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
+// every lane: the DPP row scan of wave_sum with max (common.hpp dpp_d; lanes
+// whose DPP source is outside the row read 0, the identity here), then
+// readlane 63.  Max is exact in any order, so the result equals a shuffle
+// butterfly's bit for bit.
 __device__ __forceinline__ double wave_max_nonneg(double m) {
   m = fmax(m, dpp_d<0x111>(m));
   m = fmax(m, dpp_d<0x112>(m));

@@ -526,6 +526,13 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_kernel(MetaAdamArgs a)
 // and every other block runs to its end without waiting, so the wait always
 // ends (bounded anyway: spin_max polls, then bit 0 of `err`).
 
+// An empty asm that the compiler must take as a new definition of x (so no
+// later use waits on the load that produced it).
+template <class T>
+__device__ __forceinline__ void launder_v(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
 struct MetaAdamChunks {
   double* csum;  // [nblocks]
   int nblocks;
@@ -572,9 +579,7 @@ __device__ __forceinline__ double chunk_sum_sc1(const float* x, int64_t n, int k
   double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], c);
-  double tot;
-  (void)block_scan_excl_f64(lane, s_wave, &tot);
-  return tot;
+  return block_total_f64(lane, s_wave);
 }
 
 __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdamArgs a, MetaAdamChunks ck) {
@@ -586,10 +591,11 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   const int k = blockIdx.x, t = threadIdx.x;
   const bool own = t < a.M;
   const int i0 = own ? t : 0;
+  DQZ_STAMP(19, 0);
   // Every load is issued before the block learns whether it is active (the
   // positions are loaded with the rest): one round trip instead of two, for
   // the inactive blocks' wasted loads (L2 hits but for their own chunk)
-  const int32_t pos0 = a.pos[i0];
+  int32_t pos0 = a.pos[i0];
   const int32_t posl = a.pos[0];
   // this chunk's logits (before the writes) into LDS, under the Adam loads
   float4 cv[SM_PER_LANE / 4];
@@ -616,8 +622,8 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   float lpv[META_ADAM_LP];
 #pragma unroll
   for (int r = 0; r < META_ADAM_LP; ++r) lpv[r] = a.loss_part[min(t + r * META_THREADS, a.nparts - 1)];
-  const float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
-  const int32_t cnt = *a.count + 1;
+  float x0 = a.x[i0], p0 = a.p[i0], m0 = a.m[i0], v0 = a.v[i0];
+  int32_t cnt = *a.count + 1;
   LogitRun r = *a.run;
   __builtin_amdgcn_sched_barrier(0);
   if (t == 0) {
@@ -637,11 +643,32 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
   // entry loads returned in every wave, then this block's entries arrive
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) __hip_atomic_fetch_add(ck.enter, s_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DQZ_STAMP(19, 1);
+  // The compiler's wait counts know nothing of that s_waitcnt, and the
+  // atomic below is issued by one lane only: at the merge after it, a use of
+  // the latest load would wait with vmcnt(0), i.e. for the atomic's reply too
+  // (a device-scope RMW of one word that every active block hits, microseconds
+  // in the trace).  So every loaded value is consumed or passed through an
+  // empty asm (which the compiler must take as a new definition) first.
 #pragma unroll
   for (int q = 0; q < SM_PER_LANE / 4; ++q) *reinterpret_cast<float4*>(s_chunk + t * SM_PER_LANE + 4 * q) = cv[q];
-  const float s0 = meta_s_row(dr);
+  float s0 = meta_s_row(dr);
+  launder_v(s0);
+  launder_v(x0);
+  launder_v(p0);
+  launder_v(m0);
+  launder_v(v0);
+  launder_v(cnt);
+  launder_v(r.S);
+  launder_v(r.c);
+  launder_v(r.valid);
+  launder_v(pos0);
+#pragma unroll
+  for (int u = 0; u < META_ADAM_LP; ++u) launder_v(lpv[u]);
+  if (t == 0) __hip_atomic_fetch_add(ck.enter, s_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DQZ_STAMP(13, 0);
   const float tot = block_sum_f32(own ? s0 : 0.f, sbuf);
+  DQZ_STAMP(13, 1);
   float lp = 0.f;
   if (leader) {
 #pragma unroll
@@ -662,6 +689,7 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
     const float vh = v / c2;
     nx = x0 + (-a.lr) * (mh / (sqrtf(vh) + a.eps));
   }
+  DQZ_STAMP(13, 2);
   if (leader) {
     // the leader's first store of state another block reads at entry: every
     // active block's entries have arrived (the wait sits after this block's
@@ -702,9 +730,11 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
     }
     return;
   }
+  DQZ_STAMP(19, 2);
   dS = block_sum_f64(dS, dbuf);  // fixed order: the same in every block (also a barrier for s_chunk / s_far)
   if (t == 0) s_reseed = s_far || !run_ok(r.S, r.S + dS, -INFINITY, r.c);
   __syncthreads();
+  DQZ_STAMP(13, 3);
   const bool reseed = s_reseed;
   if (!reseed) {
     if (mine) a.logits[pos0] = nx;
@@ -714,8 +744,9 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
     double lane = 0.0;
 #pragma unroll
     for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], r.c);
-    double ctot;
-    (void)block_scan_excl_f64(lane, dbuf, &ctot);
+    DQZ_STAMP(12, 0);
+    const double ctot = block_total_f64(lane, dbuf);
+    DQZ_STAMP(12, 1);
     if (t == 0) {
       ck.csum[k] = ctot;
       if (leader) {
@@ -725,6 +756,7 @@ __global__ __launch_bounds__(META_THREADS) void meta_adam_chunks_kernel(MetaAdam
         *a.loss = lp;
       }
     }
+    DQZ_STAMP(19, 3);
     return;
   }
   // re-seed (rare): logits out write-through, the last active block re-scans

@@ -202,6 +202,23 @@ __device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, 
   return excl;
 }
 
+// block_scan_excl_f64's *tot alone, with the same bits: each wave's total by
+// the DPP fold (wave_fold63_f64: VALU moves where the scan's shuffles are
+// ds_bpermute round trips), then the same wave-order combine.  All threads
+// of the block (full waves).
+__device__ __forceinline__ double block_total_f64(double v, double* s_wave) {
+  v = wave_fold63_f64(v);
+  if ((threadIdx.x & 63) == 63) s_wave[threadIdx.x >> 6] = v;
+  __syncthreads();
+  constexpr int W = SM_THREADS / 64;
+  double all = 0.0;
+#pragma unroll
+  for (int w = 0; w < W - 1; ++w) all += s_wave[w];
+  const double r = s_wave[W - 1] + all;
+  __syncthreads();
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // Chunk sums of the sampling terms, kept at write time.
 //
@@ -210,7 +227,7 @@ __device__ __forceinline__ double block_scan_excl_f64(double v, double* s_wave, 
 // shift c, and the float64 CDF over them.  The buffer keeps one float64 sum
 // per chunk of SM_CHUNK logits: csum[k] = chunk_sum(k) — lane t sums its 16
 // consecutive terms in index order, then block_scan_excl_f64's fixed-order
-// total — a pure function of (logits, c).  Every write recomputes the chunks
+// total (block_total_f64) — a pure function of (logits, c).  Every write recomputes the chunks
 // it touched (the add / put kernels in their own block; the explicit writes
 // and the meta-update through dirty flags and chunk_sums_kernel), and a
 // re-seed (new c) recomputes all of them.  A draw is then a two-level search
@@ -248,9 +265,7 @@ __device__ __forceinline__ double chunk_sum(const float* __restrict__ x, int64_t
   double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) lane += chunk_term(xv[i], c);
-  double tot;
-  (void)block_scan_excl_f64(lane, s_wave, &tot);
-  return tot;
+  return block_total_f64(lane, s_wave);
 }
 
 // One block per chunk: csum[k] = chunk_sum(k) about the running state's c;
