@@ -1,5 +1,13 @@
 // bwd.hpp — backward kernels specialised for the NatureQNetwork at small B.
 #pragma once
+// Timing-only probes (numerics wrong by design): DQZ_EXP_DXFAST / _DWFAST
+// run a third of the conv3 / conv2 dX (dW) MFMA K steps.
+#ifndef DQZ_EXP_DXFAST
+#define DQZ_EXP_DXFAST 0
+#endif
+#ifndef DQZ_EXP_DWFAST
+#define DQZ_EXP_DWFAST 0
+#endif
 #include "common.hpp"
 #include "conv1.hpp"
 #include "fwd.hpp"
@@ -220,7 +228,7 @@ __device__ __forceinline__ void conv3_bwd_dx(const Conv3BwdArgs& a, float* s_win
 #pragma unroll
   for (int m = 0; m < 3; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int kk = 0; kk < 36; ++kk) {
+  for (int kk = 0; kk < 36; ++kk) if (!DQZ_EXP_DXFAST || kk % 3 == 0) {
     const int tp = kk >> 2;  // tap' = kh'*3 + kw'
     const int off = (tp / 3) * C3X_RS + (tp % 3) * C3X_S + 4 * (kk & 3);
 #pragma unroll
@@ -301,7 +309,7 @@ __device__ __forceinline__ void conv3_bwd_dw(const Conv3BwdArgs& a, float* s_win
   // float4 (the products and their k order are those of the transposed form,
   // so the values are the same bits)
 #pragma unroll
-  for (int kk = 0; kk < 13; ++kk)
+  for (int kk = 0; kk < 13; ++kk) if (!DQZ_EXP_DWFAST || kk % 3 == 0)
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const int off = (tp / 3) * C3W_RS + (tp % 3) * C3W_S;
@@ -421,7 +429,7 @@ __device__ __forceinline__ void conv2_bwd_dx(const Conv2BwdArgs& a, float* s_win
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   float last[4] = {0.f, 0.f, 0.f, 0.f};  // pixels 96..99 (a = 9, c = 6..9), this lane's k rows
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
+  for (int kk = 0; kk < 16; ++kk) if (!DQZ_EXP_DXFAST || kk % 3 == 0) {
     const int tp = kk >> 2;  // (u', v') = (tp >> 1, tp & 1)
     const int off = (tp >> 1) * C2X_RS + (tp & 1) * C2X_S + 4 * (kk & 3);
 #pragma unroll
@@ -540,7 +548,7 @@ __device__ __forceinline__ void conv2_bwd_dw_split(const Conv2BwdArgs& a, float*
   // A = dy2 (rows: co), B = y1 (columns: ci): a lane's accumulators are four
   // consecutive co, stored as one float4 (same bits as the transposed form)
 #pragma unroll
-  for (int kk = 0; kk < 21; ++kk)
+  for (int kk = 0; kk < 21; ++kk) if (!DQZ_EXP_DWFAST || kk % 3 == 0)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const float av = s_win[pb[kk] + 16 * mt];

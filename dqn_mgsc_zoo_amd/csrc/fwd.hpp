@@ -381,6 +381,154 @@ __device__ __forceinline__ void conv3_fwd_body(const LayerFwdArgs& a, float* s_i
   DQZ_STAMP(2, 3);
 }
 
+// ---- conv3 forward on bf16 MFMA with three-piece operands (build option) ----
+// -DDQZ_CONV3_BF16X3 (off by default; round 6, profiles/r06/bf16x3/): both
+// operands of every product are f32, each the exact sum of three bf16 pieces
+// (split3_bf16), and the six largest of the nine piece products (hi hi, hi
+// mid, mid hi, hi lo, mid mid, lo hi) leave out terms below 2^-24 of |x w|:
+// f32 accuracy on v_mfma_f32_16x16x32_bf16 (16 cycles for K = 32, against
+// 8 x 32 on v_mfma_f32_16x16x4_f32).  Wave w takes the row-tile pair th =
+// w & 1 (positions 32 th + [0, 32), past 48 clamped and dropped) and the K
+// half kh = w >> 1 (k = (kh*3 + kw)*64 + ci in [288 kh, +288): nine K steps
+// of 32 = 32 consecutive ci of one tap).  Weight fragments are split while
+// the job waits for its input; the window once, at staging.  LDS image (bf16
+// units): pixel (ih, iw), piece q, channel ci at ih * C3B_RS + iw * C3B_S +
+// 64 q + ci; a lane's A fragment is 8 consecutive ci (one ds_read_b128); in
+// dwords the pixel stride is 136 = 8 and the row stride 1272 = 56 (mod 64),
+// so position p starts at 8p (mod 64) and each 16-lane group of the read
+// covers the 64 banks once.  Parity-green (the learner and 50-step
+// trajectory tests); the forward launch 16.06 -> 15.78 us back to back, the
+// graph-replayed step within noise (16,276 against 16,336 steps/s over four
+// interleaved rounds), so the default stays f32.
+#ifdef DQZ_CONV3_BF16X3
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+constexpr int C3B_S = 272, C3B_RS = 2544, C3B_WIN = 9 * C3B_RS;  // bf16: 22,896 (45.8 KB)
+static_assert(C3B_WIN * 2 <= (int)kConv1FwdSmem, "conv3 bf16 pieces fit the forward launch's LDS");
+
+__device__ __forceinline__ bf16x8v pk_bf16x8(const unsigned (&v)[8]) {
+  return __builtin_bit_cast(bf16x8v, make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                                v[6] | (v[7] << 16)));
+}
+
+template <bool WAIT>
+__device__ __forceinline__ void conv3_fwd_body_bf3(const LayerFwdArgs& a, float* s_in, const SampleJob sj) {
+  DQZ_STAMP(2, 0);
+  const int nq = sj.job, b = sj.s % a.B, z = sj.s / a.B;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int th = w & 1, kh = w >> 1;
+  const float* W = a.nz.p[z] + a.w_off;  // [576][64], k = (kh*3 + kw)*64 + ci
+  const float bv = a.nz.p[z][a.b_off + 16 * nq + (t & 15)];  // epilogue bias, loaded early
+  // B fragments: K step s -> k0 = 288 kh + 32 s; lane (n, g): k0 + 8 g + j, co = 16 nq + n
+  bf16x8v wb[9][3];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    float wv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[j] = W[(288 * kh + 32 * s + 8 * g + j) * C3CO + 16 * nq + n];
+    unsigned h[8], m[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_bf16(wv[j], h[j], m[j], l[j]);
+    wb[s][0] = pk_bf16x8(h);
+    wb[s][1] = pk_bf16x8(m);
+    wb[s][2] = pk_bf16x8(l);
+  }
+  // split now, under the hand-off wait (the compiler would sink it into the MFMA loop)
+#pragma unroll
+  for (int s = 0; s < 9; ++s)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(wb[s][q]));
+  const float4* src = reinterpret_cast<const float4*>(a.in + ((int64_t)z * a.B + b) * (C2M * C2CO));
+  constexpr int NQ4 = C2M * C2CO / 4;  // 1296
+  if constexpr (WAIT) a.wait.wait(sj.s);
+  float4 r[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    if constexpr (WAIT)
+      r[q] = load_sc1_f4(src, NQ4 * 16, min(t + 256 * q, NQ4 - 1));
+    else
+      r[q] = src[min(t + 256 * q, NQ4 - 1)];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every window load in flight before the first LDS store
+  uint16_t* s16 = reinterpret_cast<uint16_t*>(s_in);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int i = t + 256 * q;
+    if (i < NQ4) {
+      const int pix = i >> 4, ci = (i & 15) * 4;
+      uint16_t* d = s16 + (pix / C2O) * C3B_RS + (pix % C2O) * C3B_S + ci;
+      unsigned h[4], m[4], l[4];
+      split3_bf16(r[q].x, h[0], m[0], l[0]);
+      split3_bf16(r[q].y, h[1], m[1], l[1]);
+      split3_bf16(r[q].z, h[2], m[2], l[2]);
+      split3_bf16(r[q].w, h[3], m[3], l[3]);
+      *reinterpret_cast<uint2*>(d) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      *reinterpret_cast<uint2*>(d + 64) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+      *reinterpret_cast<uint2*>(d + 128) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+    }
+  }
+  DQZ_STAMP(2, 1);
+  __syncthreads();
+  int base[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = min(32 * th + 16 * i + n, C3M - 1);
+    base[i] = (p / C3O) * C3B_RS + (p % C3O) * C3B_S + 8 * g;
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int k0 = 288 * kh + 32 * s, tap = k0 >> 6;
+    const int off = (tap / 3) * C3B_RS + (tap % 3) * C3B_S + (k0 & 63);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint16_t* pa = s16 + base[i] + off;
+      const bf16x8v ah = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const uint4*>(pa));
+      const bf16x8v am = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const uint4*>(pa + 64));
+      const bf16x8v al = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const uint4*>(pa + 128));
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[s][0], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[s][1], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wb[s][0], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wb[s][2], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wb[s][1], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wb[s][0], acc[i], 0, 0, 0);
+    }
+  }
+  DQZ_STAMP(2, 2);
+  __syncthreads();
+  float* s_red = s_in;  // [2 K halves][64 rows, padded][16]
+  constexpr int RW = red_rows(64);
+  static_assert(2 * RW <= C3L_WIN, "conv3 partials fit the window");
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 32 * th + 16 * i + 4 * g + rr;
+      if (row < C3M) s_red[kh * RW + red_idx(row, n)] = acc[i][rr];
+    }
+  __syncthreads();
+  float* out = a.out + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
+  const bool linear = a.linear;  // read once (see conv1_fwd_body)
+  const bool dot = a.dot.part != nullptr;
+  const float* dyp = a.dot.dy + ((int64_t)z * a.B + b) * FLAT + 16 * nq;
+  float dacc = 0.f;
+  for (int i = t; i < C3M * 16; i += 256) {
+    const int k = red_idx(i >> 4, i & 15);
+    const float v = (s_red[k] + s_red[RW + k]) + bv;
+    if (dot)
+      dacc += v * dyp[(i >> 4) * C3CO + (i & 15)];
+    else
+      out[(i >> 4) * C3CO + (i & 15)] = linear ? v : relu(v);
+  }
+  if (dot) {
+    __syncthreads();
+    const float r = block_sum256(dacc, s_in);
+    if (t == 0) a.dot.part[(int64_t)b * META_DOT_SLOTS + a.dot.slot0 + nq] = r;
+  }
+  DQZ_STAMP(2, 3);
+}
+#endif  // DQZ_CONV3_BF16X3
+
 // fwd_conv_kernel's conv3: 8 jobs per sample, job j = output rows
 // [4 (j >> 2), +4 or +3) (28 / 21 positions, 2 MFMA row tiles instead of 3 +
 // the VALU position) x output channels [16 (j & 3), +16); each stages input
@@ -517,7 +665,11 @@ __global__ __launch_bounds__(256) void fwd_conv_kernel(Conv1FwdArgs c1, LayerFwd
     if (j3 == 8)
       conv3_fwd8_body(c3, smem, sj);
     else
+#ifdef DQZ_CONV3_BF16X3
+      conv3_fwd_body_bf3<true>(c3, smem, sj);
+#else
       conv3_fwd_body<true>(c3, smem, sj);
+#endif
   }
 }
 
