@@ -102,6 +102,11 @@ struct dqz_logit_buffer {
   float* lse;
   LogitRun* run;   // running log-sum-exp (sampling.hpp)
   int* sync;       // softmax_sample_kernel's done word (SampleSync)
+  // exact mode (dqz_logits_sample_exact): chunk sums of the exact terms,
+  // chunk maxima, numpy-buffer sums, {c, lse}
+  int nbuf;
+  double* csum_x;
+  float *part_x, *bsum_x, *scal_x;
   bool run_known;  // host side: every write since the last scan went through the library
   int run_adds;    // running adds since the last scan
 };
@@ -119,7 +124,9 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->nblocks = (int)((capacity + SM_CHUNK - 1) / SM_CHUNK);
   const size_t head = (size_t)b->nblocks * (sizeof(MaxSum) + sizeof(double) + sizeof(int));
   const size_t sync_off = (head + 64 + sizeof(LogitRun) + 255) / 256 * 256;
-  const size_t bytes = sync_off + 3 * SampleSync::kStride * sizeof(int);
+  b->nbuf = (int)((capacity + NPX_BUF - 1) / NPX_BUF);
+  const size_t x_off = sync_off + 3 * SampleSync::kStride * sizeof(int);  // 256-aligned
+  const size_t bytes = x_off + (size_t)b->nblocks * (sizeof(double) + sizeof(float)) + (size_t)b->nbuf * sizeof(float) + 64;
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
@@ -136,6 +143,10 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->lse = (float*)(p + head);
   b->run = (LogitRun*)(p + head + 64);
   b->sync = (int*)(p + sync_off);
+  b->csum_x = (double*)(p + x_off);
+  b->part_x = (float*)(p + x_off + (size_t)b->nblocks * sizeof(double));
+  b->bsum_x = b->part_x + b->nblocks;
+  b->scal_x = b->bsum_x + b->nbuf;
   b->run_known = false;
   b->run_adds = 0;
   *out = b;
@@ -292,6 +303,32 @@ int dqz_logits_sample(dqz_logit_buffer* b, const float* logits, const double* un
 int dqz_logits_sample_slots(dqz_logit_buffer* b, const float* logits, uint64_t seed, uint64_t* counter_dev,
                             const double* uniforms, int n, int32_t* out_slots, int64_t* out_idx, void* stream) {
   return logits_sample_impl(b, logits, seed, counter_dev, uniforms, n, out_slots, out_idx, (hipStream_t)stream);
+}
+
+int dqz_logits_sample_exact(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
+                            float* p_out, void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 0 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
+  if (n > 0 && (!uniforms || !out_idx)) return fail(DQZ_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(npx_max_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part_x);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(npx_cmax_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part_x, b->nblocks, b->scal_x);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(npx_bufsum_kernel, dim3(b->nbuf), dim3(SM_THREADS), 0, st, logits, b->capacity, b->scal_x,
+                     b->bsum_x);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(npx_lse_kernel, dim3(1), dim3(64), 0, st, b->bsum_x, b->nbuf, b->scal_x);
+  DQZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(npx_chunk_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->scal_x,
+                     b->csum_x, p_out);
+  DQZ_HIP(hipGetLastError());
+  if (n > 0) {
+    hipLaunchKernelGGL(npx_sample_kernel, dim3(n), dim3(SM_THREADS), 0, st, logits, b->capacity, b->scal_x, b->csum_x,
+                       b->nblocks, uniforms, out_idx);
+    DQZ_HIP(hipGetLastError());
+  }
+  return DQZ_OK;
 }
 
 int dqz_logits_probs(dqz_logit_buffer* b, const float* logits, float* p_out, float* lse_out, void* stream) {

@@ -571,15 +571,16 @@ __device__ __forceinline__ CsumLevel1 csum_level1(const double* __restrict__ csu
 // lanes) the lane (16 terms each) and the slot from the chunk's re-formed
 // terms, whose scan total is csum[chunk].  At most one lane sees the
 // crossing, so it stores the slot directly.
-template <class UF>
-__device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, const LogitRun* run,
-                                                       const double* __restrict__ csum, int nblocks, UF uf) {
+// TF: the term of a logit (chunk_term about the running state's c, or the
+// exact mode's np_expf(x - lse)); csum holds the chunk sums of the same terms.
+template <class TF, class UF>
+__device__ __forceinline__ int64_t softmax_choice_terms(const float* __restrict__ x, int64_t n, TF term,
+                                                        const double* __restrict__ csum, int nblocks, UF uf) {
   __shared__ double s_wave[SM_THREADS / 64];
   __shared__ double s_before, s_tot;
   __shared__ int s_blk;
   __shared__ int64_t s_idx;
   const int t = threadIdx.x;
-  const float c = run->c;
   __shared__ double s_u;
   if (t < 64) {
     const CsumLevel1 r = csum_level1(csum, nblocks, uf);
@@ -600,7 +601,7 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
   double lane = 0.0;
 #pragma unroll
   for (int i = 0; i < SM_PER_LANE; ++i) {
-    p[i] = chunk_term(xv[i], c);
+    p[i] = term(xv[i]);
     lane += p[i];
   }
   double tot2;  // (s_wave is not used again in this call: no trailing barrier)
@@ -634,6 +635,13 @@ __device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__
     idx = s_idx;
   }
   return idx;
+}
+
+template <class UF>
+__device__ __forceinline__ int64_t softmax_choice_body(const float* __restrict__ x, int64_t n, const LogitRun* run,
+                                                       const double* __restrict__ csum, int nblocks, UF uf) {
+  const float c = run->c;
+  return softmax_choice_terms(x, n, [c](float v) { return chunk_term(v, c); }, csum, nblocks, uf);
 }
 
 // Diagnostics (dqz_logits_probs / dqz_logits_terms), one block per chunk:
@@ -727,6 +735,241 @@ DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void softmax_sample_kernel(
       if (!uniforms) *counter = ctr + 1;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Exact mode of the learned-logit draw (dqz_logits_sample_exact): the
+// reference's own float32 probabilities, bit for bit, and its choice.
+//
+// The reference forms p = exp(x - lse), lse = c + log(sum(exp(x - c))), c =
+// max(x), with numpy float32 operations (replay_circular.py:69-76), then
+// Generator.choice(C, n, p) = searchsorted(cumsum(float64(p)) / total, u,
+// 'right') (:205-217, :540-545).  The default draw above forms its terms
+// about the running state's shift instead (so a write costs O(1), not a pass
+// over the buffer), which moves a draw near a CDF step by a float32 ulp of
+// one term.  Here every operation is numpy's: np_expf / np_logf are its SIMD
+// float32 exp and log (AVX2 / AVX-512 loops of loops_exponent_log, constants
+// from its compiled module), the sum is np.sum's (pairwise summation per
+// 8192-element buffer, buffer sums added in order), the subtractions and
+// additions are single float32 operations (no contraction: each product is
+// rounded before its sum, as there).  oracle/numpy_f32.py restates the same
+// operations and tests/test_numpy_f32_cpu.py pins it against numpy.  The
+// choice then sums the float64 terms in this file's chunk order, not
+// numpy's sequential cumsum: the two CDFs differ by float64 rounding (~1e-16
+// relative), so a draw can differ only for a uniform that close to a step.
+// Passes: chunk maxima, c, per-buffer pairwise sums, lse, the exact chunk
+// sums, the draws: six launches, each a pass over the buffer at most.
+
+__device__ __forceinline__ float np_expf(float x) {
+#pragma clang fp contract(off)
+  if (x != x) return x;
+  if (x <= -103.97208404541015625f) return 0.f;
+  if (x >= 88.72283935546875f) return INFINITY;
+  float q = x * 1.442695040888963407359924681001892137f;
+  q = (q + 12582912.f) - 12582912.f;  // rint by the 1.5 * 2^23 magic
+  float r = __fmaf_rn(q, -6.93145752e-1f, x);
+  r = __fmaf_rn(q, -1.42860677e-6f, r);
+  r = __fmaf_rn(q, 0.f, r);
+  float num = __fmaf_rn(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+  num = __fmaf_rn(num, r, 5.114512081637298353406e-02f);
+  num = __fmaf_rn(num, r, 2.473615434895520810817e-01f);
+  num = __fmaf_rn(num, r, 7.257664613233124478488e-01f);
+  num = __fmaf_rn(num, r, 1.f);
+  float den = __fmaf_rn(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+  den = __fmaf_rn(den, r, 1.f);
+  return ldexpf(num / den, (int)q);
+}
+
+// positive normal x (a sum of exponentials whose largest term is 1)
+__device__ __forceinline__ float np_logf(float x) {
+#pragma clang fp contract(off)
+  const unsigned bits = __float_as_uint(x);
+  float e = (float)(int)((bits >> 23) & 0xFFu) - 127.f;
+  float m = __uint_as_float((bits & 0x7FFFFFu) | (126u << 23));
+  float y;
+  if (m <= __uint_as_float(0x3f3504f3u)) {  // sqrt(0.5)
+    y = m + m;
+  } else {
+    y = m;
+    e = e + 1.f;
+  }
+  y = y - 1.f;
+  float num = __fmaf_rn(2.589979117907922693523e-02f, y, 3.808837741388407920751e-01f);
+  num = __fmaf_rn(num, y, 1.480000633576506585156e+00f);
+  num = __fmaf_rn(num, y, 2.112677543073053063722e+00f);
+  num = __fmaf_rn(num, y, 9.999999999999998702752e-01f);
+  num = __fmaf_rn(num, y, 0.f);
+  float den = __fmaf_rn(__uint_as_float(0x3bc083dfu), y, 1.546476374983906719538e-01f);
+  den = __fmaf_rn(den, y, 9.864942958519418960339e-01f);
+  den = __fmaf_rn(den, y, 2.453006071784736363091e+00f);
+  den = __fmaf_rn(den, y, 2.612677543073109236779e+00f);
+  den = __fmaf_rn(den, y, 1.f);
+  return __fmaf_rn(e, 0.693147180559945309417232121458176568f, num / den);
+}
+
+constexpr int NPX_BUF = 8192;   // np.getbufsize(): the reduction's buffer
+constexpr int NPX_LEAF = 128;   // numpy's PW_BLOCKSIZE
+constexpr int NPX_MAXLEAF = 256;
+
+// chunk maxima (np.max is order-free)
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_max_kernel(const float* __restrict__ x, int64_t n,
+                                                              float* __restrict__ part) {
+  __shared__ float sbuf[SM_THREADS / 64];
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, blockIdx.x, xv);
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) m = fmaxf(m, xv[i]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) sbuf[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(sbuf[0], sbuf[1]), fmaxf(sbuf[2], sbuf[3]));
+}
+
+// c = max of the chunk maxima -> scal[0]
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_cmax_kernel(const float* __restrict__ part, int nparts,
+                                                               float* __restrict__ scal) {
+  __shared__ float sbuf[SM_THREADS / 64];
+  float m = -INFINITY;
+  for (int k = threadIdx.x; k < nparts; k += SM_THREADS) m = fmaxf(m, part[k]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) sbuf[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) scal[0] = fmaxf(fmaxf(sbuf[0], sbuf[1]), fmaxf(sbuf[2], sbuf[3]));
+}
+
+// numpy's pairwise sum of one leaf (n <= 128) of the terms np_expf(x - c)
+__device__ __forceinline__ float npx_leaf_sum(const float* __restrict__ x, int64_t lo, int n, float c) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r = r + np_expf(x[lo + i] - c);
+    return r;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = np_expf(x[lo + j] - c);
+  int i = 8;
+  for (; i < n - n % 8; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + np_expf(x[lo + i + j] - c);
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + np_expf(x[lo + i] - c);
+  return res;
+}
+
+// One workgroup per 8192-element buffer: its leaves (numpy's recursion: n
+// <= 128 is a leaf, else halves with the first rounded down to a multiple
+// of 8) listed by thread 0, summed one per thread, combined by thread 0 in
+// the recursion's order -> bsum[buffer].
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_bufsum_kernel(const float* __restrict__ x, int64_t n,
+                                                                 const float* __restrict__ scal,
+                                                                 float* __restrict__ bsum) {
+  __shared__ int s_lo[NPX_MAXLEAF], s_n[NPX_MAXLEAF];
+  __shared__ float s_sum[NPX_MAXLEAF];
+  __shared__ int s_nleaf;
+  const int64_t base = (int64_t)blockIdx.x * NPX_BUF;
+  const int len = (int)min((int64_t)NPX_BUF, n - base);
+  if (threadIdx.x == 0) {
+    // pre-order walk: leaves come out left to right
+    int st_lo[32], st_n[32], sp = 0, nl = 0;
+    st_lo[sp] = 0;
+    st_n[sp++] = len;
+    while (sp > 0) {
+      const int lo = st_lo[--sp], m = st_n[sp];
+      if (m <= NPX_LEAF) {
+        s_lo[nl] = lo;
+        s_n[nl++] = m;
+      } else {
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        st_lo[sp] = lo + m2;  // right half below the left on the stack
+        st_n[sp++] = m - m2;
+        st_lo[sp] = lo;
+        st_n[sp++] = m2;
+      }
+    }
+    s_nleaf = nl;
+  }
+  __syncthreads();
+  const float c = scal[0];
+  for (int l = threadIdx.x; l < s_nleaf; l += SM_THREADS) s_sum[l] = npx_leaf_sum(x, base + s_lo[l], s_n[l], c);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // post-order combine over the same recursion, consuming leaves in order
+    int st_n[32], st_state[32];
+    float st_left[32];
+    int sp = 0, leaf = 0;
+    float ret = 0.f;
+    st_n[sp] = len;
+    st_state[sp++] = 0;
+    while (sp > 0) {
+      const int m = st_n[sp - 1];
+      if (m <= NPX_LEAF) {
+        ret = s_sum[leaf++];
+        --sp;
+      } else {
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        if (st_state[sp - 1] == 0) {  // descend left
+          st_state[sp - 1] = 1;
+          st_n[sp] = m2;
+          st_state[sp++] = 0;
+        } else if (st_state[sp - 1] == 1) {  // left done: keep it, descend right
+          st_left[sp - 1] = ret;
+          st_state[sp - 1] = 2;
+          st_n[sp] = m - m2;
+          st_state[sp++] = 0;
+        } else {  // both done
+          ret = st_left[sp - 1] + ret;
+          --sp;
+        }
+      }
+    }
+    bsum[blockIdx.x] = ret;
+  }
+}
+
+// np.sum = the buffer sums added in order; lse = c + log(sum) -> scal[1]
+DQZ_OTHER_KERNEL void npx_lse_kernel(const float* __restrict__ bsum, int nbuf, float* __restrict__ scal) {
+  if (threadIdx.x != 0) return;
+  float s = 0.f;
+  for (int k = 0; k < nbuf; ++k) s = s + bsum[k];
+  scal[1] = scal[0] + np_logf(s);
+}
+
+// The exact terms p = np_expf(x - lse) per chunk: their float64 chunk sums
+// (block_total_f64, the canonical order) and, if asked, p itself.
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_chunk_kernel(const float* __restrict__ x, int64_t n,
+                                                                const float* __restrict__ scal,
+                                                                double* __restrict__ csum, float* __restrict__ p_out) {
+  __shared__ double s_wave[SM_THREADS / 64];
+  const int k = blockIdx.x;
+  const float lse = scal[1];
+  float xv[SM_PER_LANE];
+  load_chunk_lane(x, n, k, xv);
+  const int64_t base = (int64_t)k * SM_CHUNK + threadIdx.x * SM_PER_LANE;
+  double lane = 0.0;
+#pragma unroll
+  for (int i = 0; i < SM_PER_LANE; ++i) {
+    const float p = np_expf(xv[i] - lse);
+    lane += (double)p;
+    if (p_out && base + i < n) p_out[base + i] = p;
+  }
+  const double tot = block_total_f64(lane, s_wave);
+  if (threadIdx.x == 0) csum[k] = tot;
+}
+
+// One query per block: the two-level search over the exact terms.
+DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_sample_kernel(const float* __restrict__ x, int64_t n,
+                                                                 const float* __restrict__ scal,
+                                                                 const double* __restrict__ csum, int nblocks,
+                                                                 const double* __restrict__ uniforms,
+                                                                 int64_t* __restrict__ out_idx) {
+  const int q = blockIdx.x;
+  const float lse = scal[1];
+  const int64_t idx = softmax_choice_terms(
+      x, n, [lse](float v) { return (double)np_expf(v - lse); }, csum, nblocks, [&] { return uniforms[q]; });
+  if (threadIdx.x == 0) out_idx[q] = idx;
 }
 
 // ---------------------------------------------------------------------------

@@ -99,6 +99,10 @@ class MGSCDqn(agent_base.DeviceDqnAgent):
     call: the replay Generator's uniforms are resolved into slots inside the
     learner's forward launch (Learner.step_logits)."""
     import torch  # pylint: disable=g-import-not-at-top
+    if getattr(self._replay, 'exact_sampling', False):
+      # the reference's own probabilities (dqz_logits_sample_exact), then the step
+      self._learner.step(self._store(), self._replay.sample_slots(self._batch_size))
+      return
     u = self._replay.draw_uniforms(self._batch_size)
     dev = self._learner.device
     if self._slots_cache is None:

@@ -180,6 +180,24 @@ class _DeviceLogits:
                                          nat.stream_handle()))
     return p, lse
 
+  def sample_exact(self, uniforms, probs=False):
+    """The reference's draw exactly (dqz_logits_sample_exact): absolute
+    slots for host uniforms from the reference's own float32 probabilities
+    (numpy's operations, bit for bit), and those probabilities as a device
+    tensor when `probs`."""
+    n = len(uniforms)
+    nat = self._native
+    p = self._torch.empty_like(self.logits) if probs else None
+    if n:
+      u = self._u[:n]
+      u.copy_(self._torch.as_tensor(np.asarray(uniforms, np.float64)))
+      out = self._idx[:n]
+    nat.check(nat.lib().dqz_logits_sample_exact(
+        self._h, nat.ptr(self.logits), nat.ptr(u) if n else None, n, nat.ptr(out) if n else None,
+        nat.ptr(p) if probs else None, nat.stream_handle()))
+    idx = out if n else None
+    return (idx, p) if probs else idx
+
   def sample_slots_philox(self, seed, counter, out_slots, out_idx=None):
     """Learner batch in one launch (dqz_logits_sample_slots): Philox
     uniforms (seed, device int64 counter, advanced on device), softmax-CDF
@@ -209,13 +227,17 @@ class CircularLogitBuffer:
   """Ring of learned logits; sampling probability = softmax over capacity."""
 
   def __init__(self, capacity: int, random_state: np.random.Generator,
-               device='cuda'):
+               device='cuda', exact_sampling=False):
+    """exact_sampling: draw from the reference's own float32 probabilities
+    (dqz_logits_sample_exact: six passes over the buffer per draw) instead
+    of the running-state terms (O(1) per write, a float32 ulp per term)."""
     self._dev = _DeviceLogits(capacity, device)
     self._capacity = capacity
     self._size = 0
     self._left_head = 0
     self._right_head = 0
     self._rng_state = random_state
+    self._exact = bool(exact_sampling)
 
   @property
   def capacity(self) -> int:
@@ -286,7 +308,8 @@ class CircularLogitBuffer:
 
   def sample_slots(self, size: int):
     """Absolute slots (device int64), drawn like Generator.choice(p=softmax)."""
-    return self._dev.sample_abs(self.draw_uniforms(size))
+    u = self.draw_uniforms(size)
+    return self._dev.sample_exact(u) if self._exact else self._dev.sample_abs(u)
 
   def sample(self, size: int) -> np.ndarray:
     """Relative indices, as the reference returns them."""
@@ -437,11 +460,11 @@ class MGSCFiFoTransitionReplay:
   """FIFO replay sampled by softmax(learned logits) (:1217-1312)."""
 
   def __init__(self, capacity: int, structure, random_state: np.random.Generator,
-               encoder=None, decoder=None, device='cuda'):
+               encoder=None, decoder=None, device='cuda', exact_sampling=False):
     del encoder, decoder  # frames live uncompressed in HBM
     self._capacity = capacity
     self._structure = structure
-    self._distribution = CircularLogitBuffer(capacity, random_state, device)
+    self._distribution = CircularLogitBuffer(capacity, random_state, device, exact_sampling)
     self._ring = CircularBuffer(capacity)  # slot of each live item, FIFO order
     self._items = _SlotStorage(capacity, 'ring', device)
     self._t = 0
@@ -470,6 +493,11 @@ class MGSCFiFoTransitionReplay:
   def sample_slots(self, size: int):
     """Device int32 slots drawn by softmax(logits) for the learner."""
     return self._distribution.sample_slots(size).to(dtype=_torch().int32)
+
+  @property
+  def exact_sampling(self) -> bool:
+    """Draws follow the reference's own float32 probabilities exactly."""
+    return self._distribution._exact  # pylint: disable=protected-access
 
   def stack_transitions(self, indices: Sequence[int]):
     return self._items.stack(self._structure, self._slots(indices))
@@ -536,11 +564,12 @@ class MGSCReservoirDistribution:
   """Fixed-slot learned logits for the reservoir replay (:500-565)."""
 
   def __init__(self, rng_state: np.random.Generator, capacity: int,
-               device='cuda'):
+               device='cuda', exact_sampling=False):
     self._capacity = capacity
     self._dev = _DeviceLogits(capacity, device)
     self._size = 0
     self._rng_state = rng_state
+    self._exact = bool(exact_sampling)  # as CircularLogitBuffer's
 
   @property
   def capacity(self) -> int:
@@ -595,7 +624,8 @@ class MGSCReservoirDistribution:
     return self._rng_state.random(size)
 
   def sample_slots(self, size: int):
-    return self._dev.sample_abs(self.draw_uniforms(size))
+    u = self.draw_uniforms(size)
+    return self._dev.sample_exact(u) if self._exact else self._dev.sample_abs(u)
 
   def sample(self, size: int) -> np.ndarray:
     return self.sample_slots(size).cpu().numpy()
@@ -628,12 +658,12 @@ class MGSCReservoirTransitionReplay:
   """Reservoir replay sampled by softmax(learned logits) (:568-664)."""
 
   def __init__(self, capacity: int, structure, random_state: np.random.Generator,
-               encoder=None, decoder=None, device='cuda'):
+               encoder=None, decoder=None, device='cuda', exact_sampling=False):
     del encoder, decoder
     self._capacity = capacity
     self._structure = structure
     self._random_state = random_state
-    self._distribution = MGSCReservoirDistribution(random_state, capacity, device)
+    self._distribution = MGSCReservoirDistribution(random_state, capacity, device, exact_sampling)
     self._items = _SlotStorage(capacity, 'slot', device)
     self._t = 0
 
@@ -657,6 +687,10 @@ class MGSCReservoirTransitionReplay:
 
   def sample_slots(self, size: int):
     return self._distribution.sample_slots(size).to(dtype=_torch().int32)
+
+  @property
+  def exact_sampling(self) -> bool:
+    return self._distribution._exact  # pylint: disable=protected-access
 
   def stack_transitions(self, indices: Sequence[int]):
     return self._items.stack(self._structure, np.asarray(indices))

@@ -348,6 +348,19 @@ int dqz_logits_sample_slots(dqz_logit_buffer* buf, const float* logits, uint64_t
  * (p_out: device f32 [capacity]; probabilities_from_logits,
  * replay_circular.py:69-76) and the running log-sum-exp (lse_out: device
  * f32, may be NULL). */
+/* Exact mode of the learned-logit draw: the reference's own float32
+ * probabilities p = probabilities_from_logits(logits) (replay_circular.py:69-76,
+ * numpy's float32 exp / log / sum operation for operation, bit for bit) into
+ * p_out (capacity floats, or NULL), and n draws for the caller's uniforms
+ * (the Generator's random() stream) as Generator.choice(C, n, p) makes them
+ * (replay_circular.py:205-217, :540-545): searchsorted(cumsum(p) / total, u,
+ * 'right'), the cumsum in float64 in chunk order (a draw can differ from
+ * numpy's sequential cumsum only for a uniform within float64 rounding of a
+ * CDF step).  Six passes over the buffer; independent of the running state.
+ * n = 0: p_out only.  Replaces the reference's `self._rng_state.choice(
+ * self._capacity, size=size, p=self.as_probs())` (replay_circular.py:208). */
+int dqz_logits_sample_exact(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
+                            int64_t* out_idx, float* p_out, void* stream);
 int dqz_logits_probs(dqz_logit_buffer* buf, const float* logits, float* p_out, float* lse_out, void* stream);
 
 /* Diagnostic: the exact terms a draw's CDF is built from, t = expf(x - c)

@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from oracle import learner_ref
+from oracle import replay_ref
 from tests import fake_env
 
 pytestmark = pytest.mark.gpu
@@ -203,7 +204,7 @@ def test_agent_state_round_trip(device, kind):
     assert torch.equal(getattr(a1.learner, which), getattr(a2.learner, which))
 
 
-def _make_mgsc(capacity=192, batch=32, meta_batch=16, seed=0):
+def _make_mgsc(capacity=192, batch=32, meta_batch=16, seed=0, exact=False):
   from dqn_mgsc_zoo_amd import learner as learner_lib
   from dqn_mgsc_zoo_amd import networks
   from dqn_mgsc_zoo_amd import parts
@@ -211,7 +212,7 @@ def _make_mgsc(capacity=192, batch=32, meta_batch=16, seed=0):
   from dqn_mgsc_zoo_amd.dqn_mgsc_batched import agent as agent_lib
   replay = rc.MGSCFiFoTransitionReplay(
       capacity, rc.Transition(None, None, None, None, None),
-      np.random.default_rng(seed))
+      np.random.default_rng(seed), exact_sampling=exact)
   agent = agent_lib.MGSCDqn(
       preprocessor=fake_env.FrameStacker(),
       sample_network_input=np.zeros((84, 84, 4), np.uint8),
@@ -239,6 +240,22 @@ def test_mgsc_agent_run_loop_and_meta_parity(device):
   assert np.isfinite(lg[lg != -np.inf]).all()
   assert not torch.equal(logits0, replay.logits)
   _check_meta_step_against_oracle(agent, replay, stop_gradient=True)
+
+
+def test_mgsc_agent_exact_sampling(device):
+  """The MGSC agent on a replay with exact_sampling: it learns through
+  dqz_logits_sample_exact, and the replay's draws are the reference's
+  Generator.choice on its logits for the same Generator state."""
+  agent, replay = _make_mgsc(exact=True)
+  assert replay.exact_sampling
+  _run(agent, 160)
+  lrn = agent.learner
+  assert torch.isfinite(lrn.online).all()
+  dist = replay._distribution  # pylint: disable=protected-access
+  logits = replay.logits.cpu().numpy()
+  u = copy.deepcopy(dist._rng_state).random(32)  # pylint: disable=protected-access
+  want = (replay_ref.softmax_choice(logits, u) - dist._left_head) % dist.capacity  # pylint: disable=protected-access
+  np.testing.assert_array_equal(dist.sample(32), want)
 
 
 def _check_meta_step_against_oracle(agent, replay, stop_gradient):

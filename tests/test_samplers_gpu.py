@@ -2,7 +2,9 @@
 
 * learned-logit buffers (replay_circular.py): logits after add / popleft /
   replace / setitem within 1e-6 (f32 log-sum-exp summation order differs);
-  softmax-sampled indices bit-exact given the Generator's own uniforms.
+  softmax-sampled indices bit-exact given the Generator's own uniforms;
+  the exact mode's p bit for bit numpy's probabilities_from_logits and its
+  draws Generator.choice's at up to 1M slots.
 * fp64 sum tree: device storage bit-identical to the host SumTree after the
   same set() calls; device queries identical to host queries.
 * device PER sampler: frequencies vs (1-usp) p^a/sum + usp/N (rtol as the
@@ -157,6 +159,54 @@ def test_softmax_choice_large_capacity(device):
   lg[7] = -np.inf
   ref = replay_ref.logits_logmeanexp(lg, cap - 1000)
   np.testing.assert_allclose(dev.logits[7].item(), ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize('cap', [1000, 8193, 100_003, 1_000_000])
+def test_exact_mode_is_the_reference_draw(device, cap):
+  """dqz_logits_sample_exact: p is numpy's probabilities_from_logits bit for
+  bit (replay_ref.softmax_f32 calls numpy on this host), and every draw is
+  Generator.choice's for the same uniforms (replay_ref.softmax_choice).  The
+  restatement the device follows (oracle/numpy_f32.py) is checked against
+  this host's numpy too, so a failure says which side moved."""
+  from oracle import numpy_f32
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  rng = np.random.default_rng(cap)
+  logits = (rng.standard_normal(cap) * 2).astype(np.float32)
+  logits[rng.integers(0, cap, max(1, cap // 1000))] = -np.inf  # empty slots
+  p_np = replay_ref.softmax_f32(logits)
+  assert (numpy_f32.probabilities_f32(logits).view(np.uint32) == p_np.view(np.uint32)).all()
+  dev = rc._DeviceLogits(cap, max_queries=1024)  # pylint: disable=protected-access
+  dev.logits.copy_(torch.from_numpy(logits))
+  u = np.random.default_rng(cap + 1).random(1024)
+  got, p_dev = dev.sample_exact(u, probs=True)
+  p_dev = p_dev.cpu().numpy()
+  bad = int((p_dev.view(np.uint32) != p_np.view(np.uint32)).sum())
+  assert bad == 0, (bad, _ulps(p_dev, p_np).max())
+  np.testing.assert_array_equal(got.cpu().numpy(), replay_ref.softmax_choice(logits, u))
+
+
+def test_exact_mode_wide_and_tied_logits(device):
+  """Exact mode on logits spanning the float32 exp range (terms down to
+  denormals and underflow) and on ties (every logit equal: numpy's uniform
+  p, draws = floor(u C) up to float64 cumsum rounding at the steps)."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap = 300_000
+  rng = np.random.default_rng(11)
+  logits = rng.uniform(-110.0, 0.0, cap).astype(np.float32)
+  logits[rng.integers(0, cap, 100)] = -np.inf
+  dev = rc._DeviceLogits(cap, max_queries=512)  # pylint: disable=protected-access
+  dev.logits.copy_(torch.from_numpy(logits))
+  u = np.random.default_rng(12).random(512)
+  got, p_dev = dev.sample_exact(u, probs=True)
+  p_np = replay_ref.softmax_f32(logits)
+  assert (p_dev.cpu().numpy().view(np.uint32) == p_np.view(np.uint32)).all()
+  assert (p_np == 0).sum() > 0 and ((p_np > 0) & (p_np < np.finfo(np.float32).tiny)).sum() > 0
+  np.testing.assert_array_equal(got.cpu().numpy(), replay_ref.softmax_choice(logits, u))
+  flat = np.zeros(cap, np.float32)
+  dev.logits.copy_(torch.from_numpy(flat))
+  got, p_dev = dev.sample_exact(u, probs=True)
+  assert (p_dev.cpu().numpy().view(np.uint32) == replay_ref.softmax_f32(flat).view(np.uint32)).all()
+  np.testing.assert_array_equal(got.cpu().numpy(), replay_ref.softmax_choice(flat, u))
 
 
 def test_softmax_choice_wide_logits(device):
