@@ -201,6 +201,7 @@ SIGNATURES = {
     'dqz_logits_sample_slots': (
         _int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _int, _vp, _vp, _vp]),
     'dqz_logits_sample_exact': (_int, [_vp, _vp, _vp, _int, _vp, _vp, _vp]),
+    'dqz_logits_add_exact': (_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _vp]),
     'dqz_logits_probs': (_int, [_vp, _vp, _vp, _vp, _vp]),
     'dqz_logits_terms': (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     'dqz_logits_write': (_int, [_vp, _vp, _vp, _vp, _int, _vp]),

@@ -305,12 +305,8 @@ int dqz_logits_sample_slots(dqz_logit_buffer* b, const float* logits, uint64_t s
   return logits_sample_impl(b, logits, seed, counter_dev, uniforms, n, out_slots, out_idx, (hipStream_t)stream);
 }
 
-int dqz_logits_sample_exact(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
-                            float* p_out, void* stream) {
-  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
-  if (n < 0 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
-  if (n > 0 && (!uniforms || !out_idx)) return fail(DQZ_ERR_INVALID, "null argument");
-  hipStream_t st = (hipStream_t)stream;
+// numpy's float32 logsumexp of the whole buffer -> b->scal_x[1] (c in [0])
+static int npx_lse(dqz_logit_buffer* b, const float* logits, hipStream_t st) {
   hipLaunchKernelGGL(npx_max_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->part_x);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(npx_cmax_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part_x, b->nblocks, b->scal_x);
@@ -320,6 +316,35 @@ int dqz_logits_sample_exact(dqz_logit_buffer* b, const float* logits, const doub
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(npx_lse_kernel, dim3(1), dim3(64), 0, st, b->bsum_x, b->nbuf, b->scal_x);
   DQZ_HIP(hipGetLastError());
+  return DQZ_OK;
+}
+
+int dqz_logits_add_exact(dqz_logit_buffer* b, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
+                         void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
+  if (write_pos < 0 || write_pos >= b->capacity || clear_pos >= b->capacity)
+    return fail(DQZ_ERR_INVALID, "position out of range");
+  if (size < 0) return fail(DQZ_ERR_INVALID, "size must be >= 0");
+  hipStream_t st = (hipStream_t)stream;
+  if (clear_pos >= 0) {
+    hipLaunchKernelGGL(npx_clear_kernel, dim3(1), dim3(64), 0, st, logits, clear_pos);
+    DQZ_HIP(hipGetLastError());
+  }
+  if (size > 0)
+    if (int rc = npx_lse(b, logits, st)) return rc;
+  hipLaunchKernelGGL(npx_add_kernel, dim3(1), dim3(64), 0, st, logits, write_pos, size, b->scal_x);
+  DQZ_HIP(hipGetLastError());
+  b->run_known = false;  // the running state did not follow this write
+  return DQZ_OK;
+}
+
+int dqz_logits_sample_exact(dqz_logit_buffer* b, const float* logits, const double* uniforms, int n, int64_t* out_idx,
+                            float* p_out, void* stream) {
+  if (!b || !logits) return fail(DQZ_ERR_INVALID, "null argument");
+  if (n < 0 || n > 65535) return fail(DQZ_ERR_INVALID, "n out of range");
+  if (n > 0 && (!uniforms || !out_idx)) return fail(DQZ_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = npx_lse(b, logits, st)) return rc;
   hipLaunchKernelGGL(npx_chunk_kernel, dim3(b->nblocks), dim3(SM_THREADS), 0, st, logits, b->capacity, b->scal_x,
                      b->csum_x, p_out);
   DQZ_HIP(hipGetLastError());

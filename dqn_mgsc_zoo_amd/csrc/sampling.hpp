@@ -959,6 +959,20 @@ DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_chunk_kernel(const float
   if (threadIdx.x == 0) csum[k] = tot;
 }
 
+// The reference's default logit of an add (replay_circular.py:166-179,
+// :518-533): 0 into an empty buffer, else logsumexp(logits) - np.log(size),
+// the float32 lse minus a float64 log (numpy promotes to float64), stored as
+// float32.  clear_pos >= 0: the reservoir `replace` clears that slot first
+// (npx_clear_kernel, ahead of the lse passes).
+DQZ_OTHER_KERNEL void npx_clear_kernel(float* __restrict__ x, int64_t pos) {
+  if (threadIdx.x == 0) x[pos] = -INFINITY;
+}
+DQZ_OTHER_KERNEL void npx_add_kernel(float* __restrict__ x, int64_t pos, int64_t size,
+                                     const float* __restrict__ scal) {
+  if (threadIdx.x != 0) return;
+  x[pos] = size == 0 ? 0.f : (float)((double)scal[1] - log((double)size));
+}
+
 // One query per block: the two-level search over the exact terms.
 DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_sample_kernel(const float* __restrict__ x, int64_t n,
                                                                  const float* __restrict__ scal,

@@ -97,6 +97,12 @@ class _DeviceLogits:
                                    int(write_pos), int(size), None,
                                    n.stream_handle()))
 
+  def add_default_exact(self, write_pos, size, clear_pos=-1):
+    """The reference's default logit exactly (dqz_logits_add_exact)."""
+    n = self._native
+    n.check(n.lib().dqz_logits_add_exact(self._h, n.ptr(self.logits), int(clear_pos),
+                                         int(write_pos), int(size), n.stream_handle()))
+
   def set(self, positions, values):
     """logits[positions] = values in order, keeping the running log-sum-exp."""
     pos = self._torch.as_tensor(np.asarray(positions, np.int64),
@@ -230,7 +236,9 @@ class CircularLogitBuffer:
                device='cuda', exact_sampling=False):
     """exact_sampling: draw from the reference's own float32 probabilities
     (dqz_logits_sample_exact: six passes over the buffer per draw) instead
-    of the running-state terms (O(1) per write, a float32 ulp per term)."""
+    of the running-state terms (O(1) per write, a float32 ulp per term), and
+    form default logits with its own logsumexp (dqz_logits_add_exact, four
+    passes per add)."""
     self._dev = _DeviceLogits(capacity, device)
     self._capacity = capacity
     self._size = 0
@@ -260,7 +268,10 @@ class CircularLogitBuffer:
     if self.is_full():
       raise BufferError('Buffer is full and cannot be added to. Pop an item first.')
     if item is None:
-      self._dev.add_default(self._right_head, self._size)
+      if self._exact:
+        self._dev.add_default_exact(self._right_head, self._size)
+      else:
+        self._dev.add_default(self._right_head, self._size)
     else:
       self._dev.put(self._right_head, item)
     self._right_head = (self._right_head + 1) % self._capacity
@@ -591,7 +602,10 @@ class MGSCReservoirDistribution:
     if self.is_full():
       raise BufferError('Buffer is full and cannot be added to. Pop an item first.')
     if priority is None:
-      self._dev.add_default(self._size, self._size)
+      if self._exact:
+        self._dev.add_default_exact(self._size, self._size)
+      else:
+        self._dev.add_default(self._size, self._size)
     else:
       self._dev.put(self._size, priority)
     self._size += 1
@@ -602,7 +616,10 @@ class MGSCReservoirDistribution:
       raise BufferError('Buffer should be full before replacing. Current '
                         'size=%d while capacity=%d.' % (self._size, self._capacity))
     if priority is None:
-      self._dev.add_default(idx, self._size, clear_pos=idx)
+      if self._exact:
+        self._dev.add_default_exact(idx, self._size, clear_pos=idx)
+      else:
+        self._dev.add_default(idx, self._size, clear_pos=idx)
     else:
       self._dev.put(idx, priority)
 

@@ -361,6 +361,14 @@ int dqz_logits_sample_slots(dqz_logit_buffer* buf, const float* logits, uint64_t
  * self._capacity, size=size, p=self.as_probs())` (replay_circular.py:208). */
 int dqz_logits_sample_exact(dqz_logit_buffer* buf, const float* logits, const double* uniforms, int n,
                             int64_t* out_idx, float* p_out, void* stream);
+/* Exact mode of the default-logit add (replay_circular.py:166-179 add, :518-533
+ * add / replace): logits[clear_pos] = -inf first when clear_pos >= 0, then
+ * logits[write_pos] = 0 for size 0, else float32(logsumexp(logits) -
+ * log(size)) with numpy's float32 logsumexp (as dqz_logits_sample_exact forms
+ * it) and a float64 log.  Five small launches, four passes over the buffer;
+ * the running state is left unknown (the next default-mode call re-seeds). */
+int dqz_logits_add_exact(dqz_logit_buffer* buf, float* logits, int64_t clear_pos, int64_t write_pos, int64_t size,
+                         void* stream);
 int dqz_logits_probs(dqz_logit_buffer* buf, const float* logits, float* p_out, float* lse_out, void* stream);
 
 /* Diagnostic: the exact terms a draw's CDF is built from, t = expf(x - c)

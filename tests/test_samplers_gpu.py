@@ -38,10 +38,20 @@ def _frame_item(i, rng):
   return replay_lib.Transition(s, i % 6, float(i), 0.99, s)
 
 
-def test_circular_logit_buffer_golden(device):
+def _logits_match(got, want, exact):
+  """Default mode: the running log-sum-exp sums in another order (1e-6);
+  exact mode: the reference's float32 logsumexp, so the same bits."""
+  if exact:
+    np.testing.assert_array_equal(np.asarray(got, np.float32), np.asarray(want, np.float32))
+  else:
+    np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize('exact', [False, True])
+def test_circular_logit_buffer_golden(device, exact):
   from dqn_mgsc_zoo_amd import replay_circular as rc
   g = GOLDEN['circular']['logit_buffer']
-  b = rc.CircularLogitBuffer(g['capacity'], np.random.default_rng(g['seed']))
+  b = rc.CircularLogitBuffer(g['capacity'], np.random.default_rng(g['seed']), exact_sampling=exact)
   for op in g['ops']:
     if op[0] == 'add':
       b.add(op[1])
@@ -49,50 +59,48 @@ def test_circular_logit_buffer_golden(device):
       b.popleft()
     else:
       b[np.array(op[1][0])] = np.array(op[1][1], np.float32)
-    np.testing.assert_allclose(b.logits.cpu().numpy(), op[2], rtol=1e-6,
-                               atol=1e-6)
+    _logits_match(b.logits.cpu().numpy(), op[2], exact)
   assert b._left_head == g['left_head']  # pylint: disable=protected-access
   assert b.sample(5).tolist() == g['sample']
   assert b.sample_uniform(4, replace=False).tolist() == g['sample_uniform']
 
 
-def test_mgsc_fifo_replay_golden(device):
+@pytest.mark.parametrize('exact', [False, True])
+def test_mgsc_fifo_replay_golden(device, exact):
   from dqn_mgsc_zoo_amd import replay_circular as rc
   g = GOLDEN['circular']['mgsc_fifo']
   r = rc.MGSCFiFoTransitionReplay(g['capacity'], rc.Transition(None, None, None, None, None),
-                                  np.random.default_rng(g['seed']))
+                                  np.random.default_rng(g['seed']), exact_sampling=exact)
   for i in range(g['n_add']):
     r.add(rc.Transition(i, 0, 0.0, 1.0, i))
   assert r.sample(5).s_tm1.tolist() == g['sample_items']
   ind, tr, lg = r.batch_of_ids_transitions_and_logits(3)
   assert ind.tolist() == g['meta_indices']
   assert tr.s_tm1.tolist() == g['meta_items']
-  np.testing.assert_allclose(lg, g['meta_logits'], rtol=1e-6, atol=1e-6)
+  _logits_match(lg, g['meta_logits'], exact)
   r.update_priorities(ind, np.array([0.5, -0.25, 1.0], np.float32))
   assert r.sample(4).s_tm1.tolist() == g['sample2_items']
-  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits'], rtol=1e-6,
-                             atol=1e-6)
+  _logits_match(r.logits.cpu().numpy(), g['logits'], exact)
 
 
-def test_mgsc_reservoir_replay_golden(device):
+@pytest.mark.parametrize('exact', [False, True])
+def test_mgsc_reservoir_replay_golden(device, exact):
   from dqn_mgsc_zoo_amd import replay_circular as rc
   g = GOLDEN['circular']['mgsc_reservoir']
   r = rc.MGSCReservoirTransitionReplay(g['capacity'], rc.Transition(None, None, None, None, None),
-                                       np.random.default_rng(g['seed']))
+                                       np.random.default_rng(g['seed']), exact_sampling=exact)
   for i in range(g['n_add']):
     r.add(rc.Transition(i, 0, 0.0, 1.0, i))
-  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits_after_adds'],
-                             rtol=1e-6, atol=1e-6)
+  _logits_match(r.logits.cpu().numpy(), g['logits_after_adds'], exact)
   items = [int(x.s_tm1[0]) for x in r.get(range(g['capacity']))]
   assert items == g['slot_items']
   assert r.sample(5).s_tm1.tolist() == g['sample_items']
   ind, _, lg = r.batch_of_ids_transitions_and_logits(3)
   assert ind.tolist() == g['meta_indices']
-  np.testing.assert_allclose(lg, g['meta_logits'], rtol=1e-6, atol=1e-6)
+  _logits_match(lg, g['meta_logits'], exact)
   r.update_priorities(ind, np.array([1.0, 0.0, -2.0], np.float32))
   assert r.sample(5).s_tm1.tolist() == g['sample2_items']
-  np.testing.assert_allclose(r.logits.cpu().numpy(), g['logits'], rtol=1e-6,
-                             atol=1e-6)
+  _logits_match(r.logits.cpu().numpy(), g['logits'], exact)
 
 
 def _choice_from_p(p, u):
@@ -183,6 +191,29 @@ def test_exact_mode_is_the_reference_draw(device, cap):
   bad = int((p_dev.view(np.uint32) != p_np.view(np.uint32)).sum())
   assert bad == 0, (bad, _ulps(p_dev, p_np).max())
   np.testing.assert_array_equal(got.cpu().numpy(), replay_ref.softmax_choice(logits, u))
+
+
+def test_exact_add_at_full_size(device):
+  """dqz_logits_add_exact at 1M slots: the default logit of an add and of a
+  reservoir replace (clear, then log-mean-exp over the full capacity) equal
+  the reference's logsumexp(logits) - np.log(size) as stored float32."""
+  from dqn_mgsc_zoo_amd import replay_circular as rc
+  cap = 1_000_000
+  rng = np.random.default_rng(21)
+  logits = (rng.standard_normal(cap) * 1.5).astype(np.float32)
+  logits[rng.integers(0, cap, 2000)] = -np.inf
+  dev = rc._DeviceLogits(cap)  # pylint: disable=protected-access
+  dev.logits.copy_(torch.from_numpy(logits))
+  for pos, size, clear in ((17, cap - 3000, -1), (123_456, cap, 123_456), (999_999, 5, -1)):
+    lg = dev.logits.cpu().numpy().copy()
+    if clear >= 0:
+      lg[clear] = -np.inf
+    want = np.float32(replay_ref.logsumexp_f32(lg) - np.log(size))
+    dev.add_default_exact(pos, size, clear_pos=clear)
+    got = dev.logits[pos].item()
+    assert np.float32(got).view(np.uint32) == want.view(np.uint32), (pos, got, want)
+  dev.add_default_exact(3, 0)
+  assert dev.logits[3].item() == 0.0
 
 
 def test_exact_mode_wide_and_tied_logits(device):
