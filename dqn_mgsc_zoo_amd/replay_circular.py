@@ -306,6 +306,8 @@ class CircularLogitBuffer:
     self._dev.set(np.atleast_1d(self._abs(key)), np.atleast_1d(item))
 
   def as_probs(self):
+    if self._exact:  # probabilities_from_logits bit for bit
+      return self._dev.sample_exact([], probs=True)[1]
     t = self._dev.logits
     return (t - self._dev._torch.logsumexp(t, 0)).exp()  # pylint: disable=protected-access
 
@@ -631,6 +633,8 @@ class MGSCReservoirDistribution:
     self._dev.set(np.atleast_1d(key), np.atleast_1d(priority))
 
   def as_probs(self):
+    if self._exact:  # probabilities_from_logits bit for bit
+      return self._dev.sample_exact([], probs=True)[1]
     t = self._dev.logits
     return (t - self._dev._torch.logsumexp(t, 0)).exp()  # pylint: disable=protected-access
 

@@ -61,6 +61,9 @@ def test_circular_logit_buffer_golden(device, exact):
       b[np.array(op[1][0])] = np.array(op[1][1], np.float32)
     _logits_match(b.logits.cpu().numpy(), op[2], exact)
   assert b._left_head == g['left_head']  # pylint: disable=protected-access
+  if exact:  # as_probs = probabilities_from_logits, bit for bit
+    want = replay_ref.softmax_f32(b.logits.cpu().numpy())
+    assert (b.as_probs().cpu().numpy().view(np.uint32) == want.view(np.uint32)).all()
   assert b.sample(5).tolist() == g['sample']
   assert b.sample_uniform(4, replace=False).tolist() == g['sample_uniform']
 
