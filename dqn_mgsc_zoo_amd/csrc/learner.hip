@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <functional>
 #include <cmath>
 #include <vector>
 #include <cstdlib>
@@ -107,9 +109,57 @@ struct dqz_logit_buffer {
   int nbuf;
   double* csum_x;
   float *part_x, *bsum_x, *scal_x;
+  int *prog_full, *prog_last;  // npx_program of a full and of the last buffer
   bool run_known;  // host side: every write since the last scan went through the library
   int run_adds;    // running adds since the last scan
 };
+
+// numpy's pairwise-summation recursion over one buffer of length L
+// (sampling.hpp npx_bufsum_kernel's program): the leaves in order, then the
+// internal additions grouped by height, each (dst, left, right).
+static std::vector<int> npx_program(int L) {
+  std::vector<int> lo, len;
+  std::vector<std::array<int, 4>> ops;  // height, dst, a, b
+  int nleaf = 0;
+  std::function<void(int, int)> leaves = [&](int l, int m) {
+    if (m <= NPX_LEAF) {
+      lo.push_back(l);
+      len.push_back(m);
+      return;
+    }
+    int m2 = m / 2;
+    m2 -= m2 % 8;
+    leaves(l, m2);
+    leaves(l + m2, m - m2);
+  };
+  leaves(0, L);
+  nleaf = (int)lo.size();
+  int next_leaf = 0, next = nleaf;
+  std::function<std::pair<int, int>(int)> build = [&](int m) -> std::pair<int, int> {
+    if (m <= NPX_LEAF) return {next_leaf++, 0};
+    int m2 = m / 2;
+    m2 -= m2 % 8;
+    const auto a = build(m2);
+    const auto b = build(m - m2);
+    const int h = std::max(a.second, b.second) + 1, d = next++;
+    ops.push_back({h, d, a.first, b.first});
+    return {d, h};
+  };
+  const int root = build(L).first;
+  std::stable_sort(ops.begin(), ops.end(), [](const std::array<int, 4>& x, const std::array<int, 4>& y) { return x[0] < y[0]; });
+  const int nlev = ops.empty() ? 0 : ops.back()[0];
+  std::vector<int> prog = {nleaf, nlev, root};
+  prog.insert(prog.end(), lo.begin(), lo.end());
+  prog.insert(prog.end(), len.begin(), len.end());
+  size_t k = 0;
+  for (int h = 1; h <= nlev + 1; ++h) {  // lev_off[h - 1] = first op of height h
+    prog.push_back((int)k);
+    while (k < ops.size() && ops[k][0] == h) ++k;
+  }
+  for (const auto& o : ops) prog.insert(prog.end(), {o[1], o[2], o[3]});
+  if (prog.size() > (size_t)NPX_PROG || next > 2 * NPX_MAXLEAF) std::abort();
+  return prog;
+}
 
 // Running adds between full re-scans of a logit buffer (bounds the running
 // sum's drift; each scan reads the whole buffer once).
@@ -126,7 +176,9 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   const size_t sync_off = (head + 64 + sizeof(LogitRun) + 255) / 256 * 256;
   b->nbuf = (int)((capacity + NPX_BUF - 1) / NPX_BUF);
   const size_t x_off = sync_off + 3 * SampleSync::kStride * sizeof(int);  // 256-aligned
-  const size_t bytes = x_off + (size_t)b->nblocks * (sizeof(double) + sizeof(float)) + (size_t)b->nbuf * sizeof(float) + 64;
+  const size_t prog_off = (x_off + (size_t)b->nblocks * (sizeof(double) + sizeof(float)) + (size_t)b->nbuf * sizeof(float) +
+                            64 + 255) / 256 * 256;
+  const size_t bytes = prog_off + 2 * NPX_PROG * sizeof(int);
   if (hipMalloc(&b->block, bytes) != hipSuccess) {
     delete b;
     return fail(DQZ_ERR_HIP, "hipMalloc of logit scratch failed");
@@ -147,6 +199,17 @@ int dqz_logit_buffer_create(int64_t capacity, int max_queries, dqz_logit_buffer*
   b->part_x = (float*)(p + x_off + (size_t)b->nblocks * sizeof(double));
   b->bsum_x = b->part_x + b->nblocks;
   b->scal_x = b->bsum_x + b->nbuf;
+  b->prog_full = (int*)(p + prog_off);
+  b->prog_last = b->prog_full + NPX_PROG;
+  {
+    const std::vector<int> full = npx_program(NPX_BUF), last = npx_program((int)(capacity - (int64_t)(b->nbuf - 1) * NPX_BUF));
+    if (hipMemcpy(b->prog_full, full.data(), full.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b->prog_last, last.data(), last.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(b->block);
+      delete b;
+      return fail(DQZ_ERR_HIP, "hipMemcpy of the exact-mode programs failed");
+    }
+  }
   b->run_known = false;
   b->run_adds = 0;
   *out = b;
@@ -312,7 +375,7 @@ static int npx_lse(dqz_logit_buffer* b, const float* logits, hipStream_t st) {
   hipLaunchKernelGGL(npx_cmax_kernel, dim3(1), dim3(SM_THREADS), 0, st, b->part_x, b->nblocks, b->scal_x);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(npx_bufsum_kernel, dim3(b->nbuf), dim3(SM_THREADS), 0, st, logits, b->capacity, b->scal_x,
-                     b->bsum_x);
+                     b->bsum_x, b->prog_full, b->prog_last);
   DQZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(npx_lse_kernel, dim3(1), dim3(64), 0, st, b->bsum_x, b->nbuf, b->scal_x);
   DQZ_HIP(hipGetLastError());

@@ -838,95 +838,66 @@ DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_cmax_kernel(const float*
   if (threadIdx.x == 0) scal[0] = fmaxf(fmaxf(sbuf[0], sbuf[1]), fmaxf(sbuf[2], sbuf[3]));
 }
 
-// numpy's pairwise sum of one leaf (n <= 128) of the terms np_expf(x - c)
-__device__ __forceinline__ float npx_leaf_sum(const float* __restrict__ x, int64_t lo, int n, float c) {
-  if (n < 8) {
-    float r = 0.f;
-    for (int i = 0; i < n; ++i) r = r + np_expf(x[lo + i] - c);
-    return r;
-  }
-  float r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = np_expf(x[lo + j] - c);
-  int i = 8;
-  for (; i < n - n % 8; i += 8)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = r[j] + np_expf(x[lo + i + j] - c);
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res = res + np_expf(x[lo + i] - c);
-  return res;
-}
+// One workgroup per 8192-element buffer.  numpy's recursion over a buffer
+// of length L (n <= 128 a leaf, else halves with the first rounded down to a
+// multiple of 8) depends on L alone, so the host lays it out once per buffer
+// length (npx_program, learner.hip): the leaves in order, then the internal
+// nodes' additions (left + right) grouped by height.  Here: the program to
+// LDS, the leaves in parallel (8 lanes per leaf, lane j numpy's accumulator
+// r[j]), then the additions height by height -> bsum[buffer].
+// Program: [nleaf, nlev, root, lo[nleaf], len[nleaf], lev_off[nlev + 1],
+// (dst, a, b)[...]]; node values: leaves 0..nleaf-1, internal nodes after.
+constexpr int NPX_PROG = 1024;
 
-// One workgroup per 8192-element buffer: its leaves (numpy's recursion: n
-// <= 128 is a leaf, else halves with the first rounded down to a multiple
-// of 8) listed by thread 0, summed one per thread, combined by thread 0 in
-// the recursion's order -> bsum[buffer].
 DQZ_OTHER_KERNEL __launch_bounds__(SM_THREADS) void npx_bufsum_kernel(const float* __restrict__ x, int64_t n,
                                                                  const float* __restrict__ scal,
-                                                                 float* __restrict__ bsum) {
-  __shared__ int s_lo[NPX_MAXLEAF], s_n[NPX_MAXLEAF];
-  __shared__ float s_sum[NPX_MAXLEAF];
-  __shared__ int s_nleaf;
+                                                                 float* __restrict__ bsum,
+                                                                 const int* __restrict__ prog_full,
+                                                                 const int* __restrict__ prog_last) {
+  __shared__ int sp[NPX_PROG];
+  __shared__ float s_val[2 * NPX_MAXLEAF];
+  const bool partial = blockIdx.x == gridDim.x - 1 && n % NPX_BUF != 0;
+  const int* prog = partial ? prog_last : prog_full;
+  for (int i = threadIdx.x; i < NPX_PROG; i += SM_THREADS) sp[i] = prog[i];
+  __syncthreads();
+  const int nleaf = sp[0], nlev = sp[1], root = sp[2];
+  const int* p_lo = sp + 3;
+  const int* p_len = p_lo + nleaf;
+  const int* p_lev = p_len + nleaf;
+  const int* p_ops = p_lev + nlev + 1;
   const int64_t base = (int64_t)blockIdx.x * NPX_BUF;
-  const int len = (int)min((int64_t)NPX_BUF, n - base);
-  if (threadIdx.x == 0) {
-    // pre-order walk: leaves come out left to right
-    int st_lo[32], st_n[32], sp = 0, nl = 0;
-    st_lo[sp] = 0;
-    st_n[sp++] = len;
-    while (sp > 0) {
-      const int lo = st_lo[--sp], m = st_n[sp];
-      if (m <= NPX_LEAF) {
-        s_lo[nl] = lo;
-        s_n[nl++] = m;
-      } else {
-        int m2 = m / 2;
-        m2 -= m2 % 8;
-        st_lo[sp] = lo + m2;  // right half below the left on the stack
-        st_n[sp++] = m - m2;
-        st_lo[sp] = lo;
-        st_n[sp++] = m2;
-      }
-    }
-    s_nleaf = nl;
-  }
-  __syncthreads();
   const float c = scal[0];
-  for (int l = threadIdx.x; l < s_nleaf; l += SM_THREADS) s_sum[l] = npx_leaf_sum(x, base + s_lo[l], s_n[l], c);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // post-order combine over the same recursion, consuming leaves in order
-    int st_n[32], st_state[32];
-    float st_left[32];
-    int sp = 0, leaf = 0;
-    float ret = 0.f;
-    st_n[sp] = len;
-    st_state[sp++] = 0;
-    while (sp > 0) {
-      const int m = st_n[sp - 1];
-      if (m <= NPX_LEAF) {
-        ret = s_sum[leaf++];
-        --sp;
-      } else {
-        int m2 = m / 2;
-        m2 -= m2 % 8;
-        if (st_state[sp - 1] == 0) {  // descend left
-          st_state[sp - 1] = 1;
-          st_n[sp] = m2;
-          st_state[sp++] = 0;
-        } else if (st_state[sp - 1] == 1) {  // left done: keep it, descend right
-          st_left[sp - 1] = ret;
-          st_state[sp - 1] = 2;
-          st_n[sp] = m - m2;
-          st_state[sp++] = 0;
-        } else {  // both done
-          ret = st_left[sp - 1] + ret;
-          --sp;
-        }
-      }
+  const int j = threadIdx.x & 7;
+  for (int l = threadIdx.x >> 3; l < nleaf; l += SM_THREADS / 8) {
+    const int64_t lo = base + p_lo[l];
+    const int m = p_len[l];
+    float r = 0.f;
+    if (m >= 8) {
+      r = np_expf(x[lo + j] - c);
+      for (int i = 8 + j; i < m - m % 8; i += 8) r = r + np_expf(x[lo + i] - c);
     }
-    bsum[blockIdx.x] = ret;
+    // r[k] of this leaf's 8-lane group (8-aligned in the wave)
+    const float r1 = __shfl_xor(r, 1, 8), r2 = __shfl_xor(r, 2, 8), r3 = __shfl_xor(r, 3, 8);
+    const float r4 = __shfl_xor(r, 4, 8), r5 = __shfl_xor(r, 5, 8), r6 = __shfl_xor(r, 6, 8), r7 = __shfl_xor(r, 7, 8);
+    if (j == 0) {
+      float res;
+      if (m >= 8) {
+        res = ((r + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (int i = m - m % 8; i < m; ++i) res = res + np_expf(x[lo + i] - c);
+      } else {
+        res = 0.f;
+        for (int i = 0; i < m; ++i) res = res + np_expf(x[lo + i] - c);
+      }
+      s_val[l] = res;
+    }
   }
+  __syncthreads();
+  for (int h = 0; h < nlev; ++h) {
+    for (int k = p_lev[h] + threadIdx.x; k < p_lev[h + 1]; k += SM_THREADS)
+      s_val[p_ops[3 * k]] = s_val[p_ops[3 * k + 1]] + s_val[p_ops[3 * k + 2]];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = s_val[root];
 }
 
 // np.sum = the buffer sums added in order; lse = c + log(sum) -> scal[1]
