@@ -107,15 +107,21 @@ int dqz_learner_destroy(dqz_learner* L) {
     if (!pe.on()) {                                                         \
       __VA_ARGS__;                                                          \
     } else {                                                                \
-      DQZ_HIP(hipEventRecord(pe.e0, st));                                   \
-      for (int r_ = 0; r_ < pe.reps; ++r_) {                                \
-        __VA_ARGS__;                                                        \
+      /* best of three trials: a stalled launching thread lets the queue */ \
+      /* drain, and the idle device time would count as the phase's      */ \
+      float best_ = 0.f;                                                    \
+      for (int t_ = 0; t_ < 3; ++t_) {                                      \
+        DQZ_HIP(hipEventRecord(pe.e0, st));                                 \
+        for (int r_ = 0; r_ < pe.reps; ++r_) {                              \
+          __VA_ARGS__;                                                      \
+        }                                                                   \
+        DQZ_HIP(hipEventRecord(pe.e1, st));                                 \
+        DQZ_HIP(hipEventSynchronize(pe.e1));                                \
+        float ms_ = 0.f;                                                    \
+        (void)hipEventElapsedTime(&ms_, pe.e0, pe.e1);                      \
+        if (t_ == 0 || ms_ < best_) best_ = ms_;                            \
       }                                                                     \
-      DQZ_HIP(hipEventRecord(pe.e1, st));                                   \
-      DQZ_HIP(hipEventSynchronize(pe.e1));                                  \
-      float ms_ = 0.f;                                                      \
-      (void)hipEventElapsedTime(&ms_, pe.e0, pe.e1);                        \
-      pe.ms[i] = ms_ / (float)pe.reps;                                      \
+      pe.ms[i] = best_ / (float)pe.reps;                                    \
     }                                                                       \
   } while (0)
 

@@ -186,10 +186,12 @@ int dqz_learner_grad(dqz_learner* learner, const dqz_params* params, const dqz_s
 
 /* Per-phase kernel time: runs one learner step in which every phase's
  * launch is repeated `iters` times back to back between two hipEvents on
- * `stream`; phase_ms[i] = average milliseconds per launch (the kernel's
- * duration in a saturated stream, comparable to rocprofv3 --kernel-trace).
- * Phases that update state (4, 6, 9) apply their update `iters` times: call
- * it on a scratch copy or after the timed work.  Synchronises the stream. */
+ * `stream`, three times; phase_ms[i] = the best trial's average
+ * milliseconds per launch (the kernel's duration in a saturated stream,
+ * comparable to rocprofv3 --kernel-trace; the best of three drops a trial
+ * whose launching thread stalled and let the device idle).  Phases that
+ * update state (4, 6, 9) apply their update 3 x `iters` times: call it on a
+ * scratch copy or after the timed work.  Synchronises the stream. */
 int dqz_learner_profile(dqz_learner* learner, const dqz_params* params, const dqz_store* store,
                         const int32_t* slots, const float* is_weights, int iters, float* phase_ms,
                         void* stream);
